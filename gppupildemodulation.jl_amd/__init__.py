@@ -1,0 +1,29 @@
+"""gpdemod — MI355X-native drop-in for the demodulateall hot path of
+FerreolS/GPPupilDemodulation.jl (src/Modulation.jl:344-435).
+
+The package directory name contains a dot, so load it by path, e.g.::
+
+    import importlib.util, sys
+    spec = importlib.util.spec_from_file_location(
+        "gpdemod", "gppupildemodulation.jl_amd/__init__.py",
+        submodule_search_locations=["gppupildemodulation.jl_amd"])
+    gpdemod = importlib.util.module_from_spec(spec); sys.modules["gpdemod"] = gpdemod
+    spec.loader.exec_module(gpdemod)
+
+(`gpdemod_loader.load()` at the repo root does exactly this.)
+"""
+from ._lib import (GPD_FIT_OFFSETS, GPD_METHOD_EXACT, GPD_METHOD_HARMONIC, GPD_ONLY_HIGH,
+                   GPD_RECENTER, GPD_ST_EXACT, GPD_ST_FALLBACK, GPD_ST_MAXFUN, GPD_ST_NAN,
+                   GPD_ST_REFIT, PARAM_DTYPE, GpdError, load, timings)
+from .demod import (M_2PI, Diode, FaintStates, MetState, ModulationNoOffsets,
+                    ModulationWithOffsets, Side, buildstates, chi2_batch, demodulateall, fc_column_of,
+                    fit_batch, idx)
+
+__all__ = [
+    "GPD_FIT_OFFSETS", "GPD_METHOD_EXACT", "GPD_METHOD_HARMONIC", "GPD_ONLY_HIGH", "GPD_RECENTER",
+    "GPD_ST_EXACT", "GPD_ST_FALLBACK", "GPD_ST_MAXFUN", "GPD_ST_NAN", "GPD_ST_REFIT",
+    "PARAM_DTYPE", "GpdError", "load", "timings", "M_2PI", "Diode", "FaintStates", "MetState",
+    "ModulationNoOffsets", "ModulationWithOffsets", "Side", "buildstates", "chi2_batch",
+    "demodulateall",
+    "fc_column_of", "fit_batch", "idx",
+]

@@ -1,0 +1,119 @@
+"""ctypes binding of libgpdemod.so (include/gpdemod.h).
+
+The product path has no CPU fallback: if the HIP library is missing this module raises on
+import, and every compute entry point returns GPD_E_NODEV when no GPU is visible.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgpdemod.so")
+
+GPD_ABI_VERSION = 1
+GPD_FIT_OFFSETS = 0x1
+GPD_RECENTER = 0x2
+GPD_ONLY_HIGH = 0x4
+GPD_METHOD_EXACT = 0x10
+GPD_METHOD_HARMONIC = 0x20
+
+GPD_ST_REFIT = 0x1
+GPD_ST_MAXFUN = 0x2
+GPD_ST_NAN = 0x4
+GPD_ST_EXACT = 0x8
+GPD_ST_FALLBACK = 0x10
+
+GPD_OK = 0
+GPD_E_ARG = -1
+GPD_E_HIP = -2
+GPD_E_NODEV = -3
+GPD_E_OOM = -4
+GPD_E_UNSAFE = -5
+
+PARAM_DTYPE = np.dtype(
+    [("c", np.complex128), ("a", np.complex128), ("b", np.float64), ("phi", np.float64),
+     ("chi2", np.float64), ("nfev", np.int32), ("status", np.int32)], align=True)
+assert PARAM_DTYPE.itemsize == 64
+
+# every symbol declared in include/gpdemod.h
+EXPORTS = ("gpd_version", "gpd_strerror", "gpd_device_count", "gpd_fit_batch",
+           "gpd_fit_batch_dev", "gpd_chi2_batch", "gpd_chi2_batch_dev", "gpd_buildstates",
+           "gpd_synth_fill_dev", "gpd_last_timings")
+
+
+class GpdError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"gpdemod error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def load():
+    """Load libgpdemod.so (built in-tree by __graft_entry__.build() / build.py)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not found: the HIP extension is not built "
+            "(run `python -c 'import __graft_entry__ as g; g.build()'`). No CPU fallback exists.")
+    L = ctypes.CDLL(LIB_PATH)
+    V, I64, I32, U32, D = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_double
+    L.gpd_version.restype = ctypes.c_int
+    L.gpd_version.argtypes = []
+    L.gpd_strerror.restype = ctypes.c_char_p
+    L.gpd_strerror.argtypes = [ctypes.c_int]
+    L.gpd_device_count.restype = ctypes.c_int
+    L.gpd_device_count.argtypes = []
+    common = [I64, I64, V, V, I64, V, I64, I64, V, V, D, V, U32, I32, V, V, I64]
+    L.gpd_fit_batch.restype = ctypes.c_int
+    L.gpd_fit_batch.argtypes = common + [I32, ctypes.c_char_p, ctypes.c_size_t]
+    L.gpd_fit_batch_dev.restype = ctypes.c_int
+    L.gpd_fit_batch_dev.argtypes = common + [ctypes.c_int, V, ctypes.c_char_p, ctypes.c_size_t]
+    chi = [I64, I64, V, V, I64, V, I64, I64, V, V, D, V, U32, V]
+    L.gpd_chi2_batch.restype = ctypes.c_int
+    L.gpd_chi2_batch.argtypes = chi + [I32, ctypes.c_char_p, ctypes.c_size_t]
+    L.gpd_chi2_batch_dev.restype = ctypes.c_int
+    L.gpd_chi2_batch_dev.argtypes = chi + [ctypes.c_int, V, ctypes.c_char_p, ctypes.c_size_t]
+    L.gpd_buildstates.restype = ctypes.c_int
+    L.gpd_buildstates.argtypes = [I64, V, I64, V, I64, V, D, D, V]
+    L.gpd_synth_fill_dev.restype = ctypes.c_int
+    L.gpd_synth_fill_dev.argtypes = [I64, I64, I64, ctypes.c_uint64, D, D, D, ctypes.c_int, D, V, V,
+                                     I64, V, I64, V, V, ctypes.c_int, V]
+    L.gpd_last_timings.restype = ctypes.c_int
+    L.gpd_last_timings.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                   ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+    if L.gpd_version() != GPD_ABI_VERSION:
+        raise ImportError(f"libgpdemod ABI {L.gpd_version()} != {GPD_ABI_VERSION}")
+    _lib = L
+    return L
+
+
+def ptr(a) -> ctypes.c_void_p | None:
+    if a is None:
+        return None
+    if isinstance(a, int):
+        return ctypes.c_void_p(a)
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def check(rc: int, errbuf=None):
+    if rc != GPD_OK:
+        L = load()
+        msg = errbuf.value.decode(errors="replace") if errbuf is not None else ""
+        raise GpdError(rc, f"{L.gpd_strerror(rc).decode()}: {msg}")
+
+
+def timings(device: int = 0):
+    """Per-kernel HIP-event timings (ms) of the last gpd_fit_batch_dev call on `device`."""
+    L = load()
+    cap = 16
+    names = (ctypes.c_char_p * cap)()
+    ms = (ctypes.c_double * cap)()
+    n = L.gpd_last_timings(device, names, ms, cap)
+    return {names[i].decode(): ms[i] for i in range(n)}

@@ -1,0 +1,165 @@
+// Device building blocks for the demodulation engine (gfx950).
+//
+//  * Julia Complex{Float64} arithmetic (Base.:*, Base.:/ robust division, exp(im·x)) so the
+//    exact evaluator reproduces the reference's per-sample rounding
+//    (src/Modulation.jl:137,143-146,189-192).  Built with -ffp-contract=off.
+//  * Bessel J_n(b), n = 0..K+1, by Miller's backward recurrence — the coefficients of the
+//    Jacobi–Anger expansion e^{-j b sin θ} = Σ_n J_n(b) e^{-j n θ} used by the harmonic path.
+//  * Deterministic workgroup reductions (xor-butterfly inside a wave, fixed-order across waves):
+//    every lane ends with bit-identical totals, so optimizer control flow stays uniform.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+namespace gpd {
+
+struct c64 {
+    double re, im;
+};
+
+__device__ __forceinline__ c64 cmul(c64 x, c64 y) {  // Base.:*(::ComplexF64, ::ComplexF64)
+    return {x.re * y.re - x.im * y.im, x.re * y.im + x.im * y.re};
+}
+
+__device__ __forceinline__ double robust_cdiv2(double a, double b, double c, double d, double r,
+                                               double t) {
+    if (r != 0) {
+        const double br = b * r;
+        return (br != 0 ? (a + br) * t : a * t + (b * t) * r);
+    }
+    return (a + d * (b / c)) * t;
+}
+
+// Base.:/(::ComplexF64, ::ComplexF64): Baudin–Smith robust complex division.
+__device__ __forceinline__ c64 cdiv(c64 z, c64 w) {
+    double a = z.re, b = z.im, c = w.re, d = w.im;
+    const double absa = fabs(a), absb = fabs(b), ab = absa >= absb ? absa : absb;
+    const double absc = fabs(c), absd = fabs(d), cd = absc >= absd ? absc : absd;
+    const double halfov = 0.5 * 1.7976931348623157e308;
+    const double twouneps = 2.2250738585072014e-308 * 2.0 / 2.220446049250313e-16;
+    const double bs = 2.0 / (2.220446049250313e-16 * 2.220446049250313e-16);
+    double s = 1.0, p, q;
+    if (ab >= halfov) { a = 0.5 * a; b = 0.5 * b; s = 2.0; }
+    if (cd >= halfov) { c = 0.5 * c; d = 0.5 * d; s *= 0.5; }
+    if (ab <= twouneps) { a *= bs; b *= bs; s /= bs; }
+    if (cd <= twouneps) { c *= bs; d *= bs; s *= bs; }
+    if (absd <= absc) {
+        const double r = d / c, t = 1.0 / (c + d * r);
+        p = robust_cdiv2(a, b, c, d, r, t);
+        q = robust_cdiv2(b, -a, c, d, r, t);
+    } else {
+        const double r = c / d, t = 1.0 / (d + c * r);
+        p = robust_cdiv2(b, a, d, c, r, t);
+        q = -robust_cdiv2(a, -b, d, c, r, t);
+    }
+    return {p * s, q * s};
+}
+
+// exp(Complex(±0, x)) as Julia evaluates it: (cos x, sin x), or (1, x) when x == 0.
+__device__ __forceinline__ c64 cisj(double x) {
+    if (x == 0.0) return {1.0, x};
+    double s, c;
+    sincos(x, &s, &c);
+    return {c, s};
+}
+
+// ---------------------------------------------------------------------------------------
+// Bessel functions of the first kind J_0..J_{KP} at b (any sign) by Miller's backward
+// recurrence J_{n-1} = (2n/b) J_n − J_{n+1}, normalised with J_0 + 2 Σ_k J_{2k} = 1, with
+// rescaling against overflow.  Relative accuracy ~1e-16 for |b| ≤ KP/2.
+template <int KP>
+__host__ __device__ __forceinline__ void bessel_j(double b, double (&J)[KP + 1]) {
+    const double ab = fabs(b);
+    if (ab == 0.0) {
+        J[0] = 1.0;
+#pragma unroll
+        for (int n = 1; n <= KP; ++n) J[n] = 0.0;
+        return;
+    }
+    // start order: even, comfortably above max(KP, |b|)
+    int m = KP + 20 + (int)ab;
+    m += (m & 1);
+    const double inv = 2.0 / ab;
+    double jp1 = 0.0, jn = 1.0e-280, norm = 0.0;
+#pragma unroll
+    for (int n = 0; n <= KP; ++n) J[n] = 0.0;
+    for (int n = m; n >= 1; --n) {
+        const double jm1 = (double)n * inv * jn - jp1;  // J_{n-1}
+        jp1 = jn;
+        jn = jm1;
+        // J_n now stored in jp1; record orders ≤ KP
+        if (n <= KP) {
+#pragma unroll
+            for (int q = 1; q <= KP; ++q)
+                if (q == n) J[q] = jp1;
+        }
+        if ((n & 1) == 0) norm += 2.0 * jp1;  // even order n contributes 2 J_n
+        if (fabs(jn) > 1.0e250) {              // rescale everything accumulated so far
+            jn *= 1.0e-250;
+            jp1 *= 1.0e-250;
+            norm *= 1.0e-250;
+#pragma unroll
+            for (int q = 1; q <= KP; ++q) J[q] *= 1.0e-250;
+        }
+    }
+    J[0] = jn;
+    norm += jn;
+    const double s = 1.0 / norm;
+#pragma unroll
+    for (int n = 0; n <= KP; ++n) J[n] *= s;
+    if (b < 0.0) {
+#pragma unroll
+        for (int n = 1; n <= KP; n += 2) J[n] = -J[n];
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Deterministic sum over a workgroup of WG threads (WG multiple of 64) of NV doubles.
+// lds must hold (WG/64)*NV doubles.  On return every thread holds the same totals.
+template <int WG, int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double *lds) {
+    constexpr int NW = WG / 64;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k] = v[k] + __shfl_xor(v[k], off, 64);
+    }
+    if (NW == 1) return;
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) lds[wave * NV + k] = v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        double s = lds[k];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) s = s + lds[w * NV + k];
+        v[k] = s;
+    }
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------------------
+// Counter-based RNG (splitmix64), identical to tests/synth.py.
+__device__ __host__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    uint64_t z = x;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ double rng_uniform(uint64_t seed, uint64_t stream, uint64_t idx) {
+    const uint64_t key = splitmix64((seed * 0x100000001B3ull) ^ stream);
+    return (double)(splitmix64(idx ^ key) >> 11) * (1.0 / 9007199254740992.0);
+}
+__device__ __forceinline__ double rng_normal(uint64_t seed, uint64_t stream, uint64_t idx) {
+    const double u1 = rng_uniform(seed, 2 * stream, idx);
+    const double u2 = rng_uniform(seed, 2 * stream + 1, idx);
+    return sqrt(-2.0 * log1p(-u1)) * cos(6.283185307179586 * u2);
+}
+
+}  // namespace gpd

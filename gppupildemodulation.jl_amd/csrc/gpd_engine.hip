@@ -1,0 +1,599 @@
+// C-ABI implementation of include/gpdemod.h on top of the gfx950 kernels (gpd_kernels.hpp).
+//
+// Host runtime: per-device context (workspace arena, ordering event, kernel timing events)
+// created lazily under a mutex; gpd_fit_batch shards series over devices with one host thread
+// per device; gpd_fit_batch_dev enqueues the whole pipeline on the caller's stream without a
+// host round trip (the harmonic → exact fallback list is consumed on device).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/gpdemod.h"
+#include "gpd_kernels.hpp"
+
+using namespace gpd;
+
+static_assert(sizeof(Param) == sizeof(gpd_param), "gpd_param layout");
+static_assert(sizeof(c64) == sizeof(gpd_c64), "gpd_c64 layout");
+
+namespace {
+
+void set_err(char *buf, size_t len, const char *fmt, ...) {
+    if (!buf || len == 0) return;
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, len, fmt, ap);
+    va_end(ap);
+}
+
+#define HIP_TRY(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess) {                                                          \
+            set_err(errbuf, errlen, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                    __FILE__, __LINE__);                                                 \
+            return GPD_E_HIP;                                                            \
+        }                                                                                \
+    } while (0)
+
+constexpr int kMaxTimers = 12;
+
+struct DevCtx {
+    int dev = -1;
+    std::mutex mu;
+    char *ws = nullptr;
+    size_t ws_cap = 0;
+    hipEvent_t done = nullptr;  // orders successive calls that share the workspace
+    hipEvent_t ev[kMaxTimers + 1] = {};
+    const char *tname[kMaxTimers] = {};
+    int ntimers = 0;
+    bool have_timers = false;
+};
+
+std::mutex g_mu;
+std::vector<DevCtx *> g_ctx;
+
+DevCtx *ctx_for(int dev) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if ((int)g_ctx.size() <= dev) g_ctx.resize(dev + 1, nullptr);
+    if (!g_ctx[dev]) {
+        g_ctx[dev] = new DevCtx();
+        g_ctx[dev]->dev = dev;
+    }
+    return g_ctx[dev];
+}
+
+size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
+
+struct Layout {
+    size_t info, tab, part, mom, aux, fstat, raw, list, phbuf, total;
+    int nch;
+    long long chunk;
+};
+
+Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic, bool phbuf) {
+    Layout L{};
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        size_t o = off;
+        off += align_up(bytes);
+        return o;
+    };
+    const long long npg = (P + 63) / 64;
+    long long nch = harmonic ? std::max<long long>(1, 8192 / std::max<long long>(npg, 1)) : 1;
+    nch = std::min<long long>(nch, std::max<long long>(1, (N + 255) / 256));
+    long long chunk = (N + nch - 1) / nch;
+    chunk = (chunk + MOM_TS - 1) / MOM_TS * MOM_TS;
+    nch = (N + chunk - 1) / chunk;
+    L.nch = (int)nch;
+    L.chunk = chunk;
+    L.info = take(sizeof(Info));
+    L.tab = take(harmonic ? (size_t)N * 2 * KH * sizeof(double) : 0);
+    L.part = take(harmonic ? (size_t)nch * NMOM * P * sizeof(double) : 0);
+    L.mom = take(harmonic ? (size_t)NMOM * P * sizeof(double) : 0);
+    L.aux = take((size_t)P * 4 * sizeof(double));
+    L.fstat = take(faint ? (size_t)P * 16 * sizeof(double) : 0);
+    L.raw = take((size_t)P * 2 * sizeof(double));
+    L.list = take((size_t)(P + 64) * sizeof(int));
+    L.phbuf = take(phbuf ? (size_t)n_fc * N * sizeof(c64) : 0);
+    L.total = off;
+    return L;
+}
+
+const char *kErrStr[] = {"ok", "invalid argument", "HIP runtime error", "no HIP device",
+                         "out of device memory", "harmonic method unsafe for these timestamps"};
+
+}  // namespace
+
+extern "C" {
+
+int gpd_version(void) { return GPD_ABI_VERSION; }
+
+const char *gpd_strerror(int code) {
+    if (code > 0 || code < -5) return "unknown error";
+    return kErrStr[-code];
+}
+
+int gpd_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+}  // extern "C"
+
+// Whole device pipeline.  bphi == nullptr: fit (gpd_fit_batch_dev); else evaluate χ² at
+// (bphi[2k], bphi[2k+1]) for every series (gpd_chi2_batch_dev).
+static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, const gpd_c64 *d,
+                        int64_t ldd, const gpd_c64 *fc, int64_t n_fc, int64_t ldfc,
+                        const int32_t *fc_of_pixel, const int8_t *state, double omega,
+                        const double *xinit, uint32_t flags, int32_t maxfun,
+                        gpd_param *out_params, gpd_c64 *out_demod, int64_t ldo,
+                        const double *bphi, int device, void *stream_, char *errbuf,
+                        size_t errlen) {
+    if (n_samples < 2 || n_pixels < 1 || !t || !d || !fc || !fc_of_pixel || !out_params ||
+        ldd < n_samples || ldfc < n_samples || n_fc < 1 || (out_demod && ldo < n_samples)) {
+        set_err(errbuf, errlen, "gpd_fit_batch_dev: invalid shapes/pointers (N=%lld P=%lld)",
+                (long long)n_samples, (long long)n_pixels);
+        return GPD_E_ARG;
+    }
+    if (n_pixels > (int64_t)0x7fffff00) {
+        set_err(errbuf, errlen, "gpd_fit_batch_dev: too many series");
+        return GPD_E_ARG;
+    }
+    if ((flags & GPD_METHOD_EXACT) && (flags & GPD_METHOD_HARMONIC)) {
+        set_err(errbuf, errlen, "gpd_fit_batch_dev: both METHOD bits set");
+        return GPD_E_ARG;
+    }
+    int ndev = gpd_device_count();
+    if (ndev <= 0) {
+        set_err(errbuf, errlen, "gpd_fit_batch_dev: no HIP device visible");
+        return GPD_E_NODEV;
+    }
+    if (device < 0 || device >= ndev) {
+        set_err(errbuf, errlen, "gpd_fit_batch_dev: device %d out of range", device);
+        return GPD_E_ARG;
+    }
+    HIP_TRY(hipSetDevice(device));
+    hipStream_t stream = (hipStream_t)stream_;
+    const bool faint = state != nullptr;
+    const bool offs = (flags & GPD_FIT_OFFSETS) != 0;
+    // Harmonic moments cover the no-offsets χ²; offsets go to the exact evaluator.
+    const bool want_exact = (flags & GPD_METHOD_EXACT) || offs;
+    if ((flags & GPD_METHOD_HARMONIC) && offs) {
+        set_err(errbuf, errlen, "gpd_fit_batch_dev: harmonic method does not support fitoffsets yet");
+        return GPD_E_ARG;
+    }
+    const bool harmonic = !want_exact;
+    const long long N = n_samples, P = n_pixels;
+    const bool phbuf = want_exact && (size_t)n_fc * N * sizeof(c64) <= (size_t(4) << 30);
+
+    DevCtx *cx = ctx_for(device);
+    std::lock_guard<std::mutex> lk(cx->mu);
+    const Layout L = plan(N, P, n_fc, faint, harmonic, phbuf);
+    if (cx->ws_cap < L.total) {
+        if (cx->ws) {
+            HIP_TRY(hipDeviceSynchronize());
+            HIP_TRY(hipFree(cx->ws));
+            cx->ws = nullptr;
+            cx->ws_cap = 0;
+        }
+        hipError_t e = hipMalloc(&cx->ws, L.total);
+        if (e != hipSuccess) {
+            set_err(errbuf, errlen, "gpd_fit_batch_dev: workspace of %zu bytes: %s", L.total,
+                    hipGetErrorString(e));
+            (void)hipGetLastError();
+            return GPD_E_OOM;
+        }
+        cx->ws_cap = L.total;
+    }
+    if (!cx->done) {
+        HIP_TRY(hipEventCreateWithFlags(&cx->done, hipEventDisableTiming));
+        for (int i = 0; i <= kMaxTimers; ++i) HIP_TRY(hipEventCreate(&cx->ev[i]));
+    } else {
+        HIP_TRY(hipStreamWaitEvent(stream, cx->done, 0));
+    }
+    char *ws = cx->ws;
+    Info *info = (Info *)(ws + L.info);
+    double *tab = (double *)(ws + L.tab);
+    double *part = (double *)(ws + L.part);
+    double *mom = (double *)(ws + L.mom);
+    double *aux = (double *)(ws + L.aux);
+    double *fstat = (double *)(ws + L.fstat);
+    double *raw = (double *)(ws + L.raw);
+    int *list = (int *)(ws + L.list);
+    int *count = list + P;
+    c64 *ph = (c64 *)(ws + L.phbuf);
+
+    Problem pb;
+    pb.N = N;
+    pb.P = P;
+    pb.t = t;
+    pb.d = (const c64 *)d;
+    pb.ldd = ldd;
+    pb.fc = (const c64 *)fc;
+    pb.ldfc = ldfc;
+    pb.n_fc = n_fc;
+    pb.fcop = fc_of_pixel;
+    pb.state = state;
+    pb.omega = omega;
+    pb.flags = flags;
+    pb.maxfun = maxfun <= 0 ? 60 : std::max(maxfun, 6);
+    pb.has_xinit = xinit != nullptr;
+    pb.x0 = xinit ? xinit[0] : 0.0;
+    pb.x1 = xinit ? xinit[1] : 0.0;
+    Param *outp = (Param *)out_params;
+
+    int nt = 0;
+    auto mark = [&](const char *name) {
+        if (nt < kMaxTimers) {
+            cx->tname[nt] = name;
+            (void)hipEventRecord(cx->ev[nt + 1], stream);
+            ++nt;
+        }
+    };
+    HIP_TRY(hipEventRecord(cx->ev[0], stream));
+
+    k_prepare<<<1, 1024, 0, stream>>>(pb, info);
+    HIP_TRY(hipMemsetAsync(count, 0, sizeof(int), stream));
+    mark("prepare");
+    if (faint) {
+        k_faint_stats<<<(unsigned)P, 256, 0, stream>>>(pb, fstat);
+        mark("faint_stats");
+    }
+    const unsigned exact_grid = (unsigned)std::min<long long>(P, 1024);
+    if (harmonic) {
+        k_table<<<(unsigned)((N + 255) / 256), 256, 0, stream>>>(t, N, omega, tab);
+        mark("table");
+        dim3 g((unsigned)((P + 63) / 64), (unsigned)L.nch);
+        if (faint)
+            k_moments<true><<<g, 64, 0, stream>>>(pb, tab, fstat, L.chunk, part);
+        else
+            k_moments<false><<<g, 64, 0, stream>>>(pb, tab, fstat, L.chunk, part);
+        mark("moments");
+        dim3 gr((unsigned)((P + 255) / 256), (unsigned)NMOM);
+        k_reduce_moments<<<gr, 256, 0, stream>>>(part, L.nch, P, info, fstat, faint ? 1 : 0, mom, aux);
+        mark("reduce");
+        if (bphi) {
+            k_chi2_harmonic<<<(unsigned)((P + 63) / 64), 64, 0, stream>>>(pb, info, mom, aux, bphi, outp);
+            mark("chi2_harmonic");
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipEventRecord(cx->done, stream));
+            cx->ntimers = nt;
+            cx->have_timers = true;
+            return GPD_OK;
+        }
+        k_fit_harmonic<<<(unsigned)((P + 63) / 64), 64, 0, stream>>>(pb, info, mom, aux, outp, raw,
+                                                                   list, count);
+        mark("fit_harmonic");
+        // fallback: series whose fit left the expansion's safe range, re-fitted exactly
+        if (faint)
+            k_fit_exact<true, false, false><<<exact_grid, EXACT_WG, 0, stream>>>(
+                pb, info, nullptr, fstat, list, count, outp, raw, ST_FALLBACK);
+        else
+            k_fit_exact<false, false, false><<<exact_grid, EXACT_WG, 0, stream>>>(
+                pb, info, nullptr, fstat, list, count, outp, raw, ST_FALLBACK);
+        mark("fit_fallback");
+    } else {
+        if (phbuf) {
+            dim3 g((unsigned)std::min<long long>((N + 255) / 256, 256), (unsigned)n_fc);
+            k_phasor<<<g, 256, 0, stream>>>((const c64 *)fc, ldfc, n_fc, N, ph);
+            mark("phasor");
+        }
+#define GPD_LAUNCH_EXACT(FA, OF, PH)                                                                 \
+    do {                                                                                        \
+        if (bphi)                                                                               \
+            k_chi2_exact<FA, OF, PH><<<(unsigned)P, EXACT_WG, 0, stream>>>(pb, info, ph, fstat, \
+                                                                           bphi, outp);         \
+        else                                                                                    \
+            k_fit_exact<FA, OF, PH><<<exact_grid, EXACT_WG, 0, stream>>>(pb, info, ph, fstat,   \
+                                                                         nullptr, nullptr,      \
+                                                                         outp, raw, 0);         \
+    } while (0)
+        if (faint) {
+            if (offs) { if (phbuf) GPD_LAUNCH_EXACT(true, true, true); else GPD_LAUNCH_EXACT(true, true, false); }
+            else { if (phbuf) GPD_LAUNCH_EXACT(true, false, true); else GPD_LAUNCH_EXACT(true, false, false); }
+        } else {
+            if (offs) { if (phbuf) GPD_LAUNCH_EXACT(false, true, true); else GPD_LAUNCH_EXACT(false, true, false); }
+            else { if (phbuf) GPD_LAUNCH_EXACT(false, false, true); else GPD_LAUNCH_EXACT(false, false, false); }
+        }
+#undef GPD_LAUNCH_EXACT
+        mark(bphi ? "chi2_exact" : "fit_exact");
+    }
+    if (out_demod && !bphi) {
+        dim3 g((unsigned)std::min<long long>((N + 255) / 256, 64), (unsigned)P);
+        k_output<<<g, 256, 0, stream>>>(pb, outp, raw, (c64 *)out_demod, ldo);
+        mark("output");
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(cx->done, stream));
+    cx->ntimers = nt;
+    cx->have_timers = true;
+    return GPD_OK;
+}
+
+extern "C" {
+
+int gpd_fit_batch_dev(int64_t n_samples, int64_t n_pixels, const double *t, const gpd_c64 *d,
+                      int64_t ldd, const gpd_c64 *fc, int64_t n_fc, int64_t ldfc,
+                      const int32_t *fc_of_pixel, const int8_t *state, double omega,
+                      const double *xinit, uint32_t flags, int32_t maxfun, gpd_param *out_params,
+                      gpd_c64 *out_demod, int64_t ldo, int device, void *stream, char *errbuf,
+                      size_t errlen) {
+    return pipeline_dev(n_samples, n_pixels, t, d, ldd, fc, n_fc, ldfc, fc_of_pixel, state, omega,
+                        xinit, flags, maxfun, out_params, out_demod, ldo, nullptr, device, stream,
+                        errbuf, errlen);
+}
+
+int gpd_chi2_batch_dev(int64_t n_samples, int64_t n_pixels, const double *t, const gpd_c64 *d,
+                       int64_t ldd, const gpd_c64 *fc, int64_t n_fc, int64_t ldfc,
+                       const int32_t *fc_of_pixel, const int8_t *state, double omega,
+                       const double *bphi, uint32_t flags, gpd_param *out_params, int device,
+                       void *stream, char *errbuf, size_t errlen) {
+    if (!bphi) {
+        set_err(errbuf, errlen, "gpd_chi2_batch_dev: bphi is NULL");
+        return GPD_E_ARG;
+    }
+    return pipeline_dev(n_samples, n_pixels, t, d, ldd, fc, n_fc, ldfc, fc_of_pixel, state, omega,
+                        nullptr, flags, 0, out_params, nullptr, n_samples, bphi, device, stream,
+                        errbuf, errlen);
+}
+
+int gpd_last_timings(int device, const char **names, double *ms, int cap) {
+    if (device < 0 || device >= gpd_device_count()) return 0;
+    DevCtx *cx = ctx_for(device);
+    std::lock_guard<std::mutex> lk(cx->mu);
+    if (!cx->have_timers) return 0;
+    if (hipSetDevice(device) != hipSuccess) return 0;
+    if (hipEventSynchronize(cx->ev[cx->ntimers]) != hipSuccess) return 0;
+    int n = std::min(cap, cx->ntimers);
+    for (int i = 0; i < n; ++i) {
+        float f = 0.f;
+        (void)hipEventElapsedTime(&f, cx->ev[i], cx->ev[i + 1]);
+        if (names) names[i] = cx->tname[i];
+        if (ms) ms[i] = (double)f;
+    }
+    return n;
+}
+
+}  // extern "C"
+
+// Host-pointer driver: shard series over devices (one host thread per device), copy in, run the
+// device pipeline, copy out.  bphi (host, 2 per series) selects χ²-evaluation mode.
+static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, const gpd_c64 *d,
+                      int64_t ldd, const gpd_c64 *fc, int64_t n_fc, int64_t ldfc,
+                      const int32_t *fc_of_pixel, const int8_t *state, double omega,
+                      const double *xinit, uint32_t flags, int32_t maxfun, gpd_param *out_params,
+                      gpd_c64 *out_demod, int64_t ldo, const double *bphi, int32_t n_gpus,
+                      char *errbuf, size_t errlen) {
+    if (n_samples < 2 || n_pixels < 1 || !t || !d || !fc || !fc_of_pixel || !out_params ||
+        ldd < n_samples || ldfc < n_samples || n_fc < 1 || (out_demod && ldo < n_samples)) {
+        set_err(errbuf, errlen, "gpd_batch: invalid shapes/pointers");
+        return GPD_E_ARG;
+    }
+    for (int64_t k = 0; k < n_pixels; ++k) {
+        if (fc_of_pixel[k] < 0 || fc_of_pixel[k] >= n_fc) {
+            set_err(errbuf, errlen, "gpd_batch: fc_of_pixel[%lld]=%d outside [0,%lld)",
+                    (long long)k, fc_of_pixel[k], (long long)n_fc);
+            return GPD_E_ARG;
+        }
+    }
+    const int ndev = gpd_device_count();
+    if (ndev <= 0) {
+        set_err(errbuf, errlen, "gpd_batch: no HIP device visible");
+        return GPD_E_NODEV;
+    }
+    int G = n_gpus <= 0 ? 1 : std::min<int>(n_gpus, ndev);
+    G = (int)std::min<int64_t>(G, n_pixels);
+    const int64_t N = n_samples;
+    std::vector<int> rc(G, GPD_OK);
+    std::vector<std::string> msg(G);
+
+    auto worker = [&](int g) {
+        char eb[512] = {0};
+        const size_t errlen_l = sizeof eb;
+        char *errbuf_l = eb;
+        auto fail = [&](int code) {
+            rc[g] = code;
+            msg[g] = eb;
+        };
+        const int64_t p0 = n_pixels * g / G, p1 = n_pixels * (g + 1) / G, P = p1 - p0;
+        if (hipSetDevice(g) != hipSuccess) {
+            set_err(errbuf_l, errlen_l, "hipSetDevice(%d) failed", g);
+            return fail(GPD_E_HIP);
+        }
+        double *dt = nullptr;
+        c64 *dd = nullptr, *dfc = nullptr, *dout = nullptr;
+        int32_t *dfcop = nullptr;
+        int8_t *dst = nullptr;
+        Param *dpar = nullptr;
+        double *dbphi = nullptr;
+        hipStream_t s = nullptr;
+        auto cleanup = [&]() {
+            if (s) (void)hipStreamDestroy(s);
+            (void)hipFree(dt);
+            (void)hipFree(dd);
+            (void)hipFree(dfc);
+            (void)hipFree(dout);
+            (void)hipFree(dfcop);
+            (void)hipFree(dst);
+            (void)hipFree(dpar);
+            (void)hipFree(dbphi);
+        };
+        auto chk = [&](hipError_t e, const char *what) {
+            if (e != hipSuccess) {
+                set_err(errbuf_l, errlen_l, "%s: %s", what, hipGetErrorString(e));
+                return false;
+            }
+            return true;
+        };
+        bool ok = chk(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate") &&
+                  chk(hipMalloc(&dt, N * sizeof(double)), "hipMalloc t") &&
+                  chk(hipMalloc(&dd, (size_t)P * N * sizeof(c64)), "hipMalloc d") &&
+                  chk(hipMalloc(&dfc, (size_t)n_fc * N * sizeof(c64)), "hipMalloc fc") &&
+                  chk(hipMalloc(&dfcop, P * sizeof(int32_t)), "hipMalloc fcop") &&
+                  chk(hipMalloc(&dpar, P * sizeof(Param)), "hipMalloc params") &&
+                  (!state || chk(hipMalloc(&dst, N), "hipMalloc state")) &&
+                  (!bphi || chk(hipMalloc(&dbphi, 2 * P * sizeof(double)), "hipMalloc bphi")) &&
+                  (!out_demod || chk(hipMalloc(&dout, (size_t)P * N * sizeof(c64)), "hipMalloc out"));
+        if (!ok) {
+            cleanup();
+            (void)hipGetLastError();
+            return fail(GPD_E_OOM);
+        }
+        ok = chk(hipMemcpyAsync(dt, t, N * sizeof(double), hipMemcpyHostToDevice, s), "H2D t") &&
+             chk(hipMemcpy2DAsync(dd, N * sizeof(c64), d + p0 * ldd, ldd * sizeof(gpd_c64),
+                                  N * sizeof(c64), P, hipMemcpyHostToDevice, s), "H2D d") &&
+             chk(hipMemcpy2DAsync(dfc, N * sizeof(c64), fc, ldfc * sizeof(gpd_c64), N * sizeof(c64),
+                                  n_fc, hipMemcpyHostToDevice, s), "H2D fc") &&
+             chk(hipMemcpyAsync(dfcop, fc_of_pixel + p0, P * sizeof(int32_t), hipMemcpyHostToDevice, s),
+                 "H2D fcop") &&
+             (!state || chk(hipMemcpyAsync(dst, state, N, hipMemcpyHostToDevice, s), "H2D state")) &&
+             (!bphi || chk(hipMemcpyAsync(dbphi, bphi + 2 * p0, 2 * P * sizeof(double),
+                                          hipMemcpyHostToDevice, s), "H2D bphi"));
+        if (!ok) {
+            cleanup();
+            return fail(GPD_E_HIP);
+        }
+        int r = pipeline_dev(N, P, dt, (const gpd_c64 *)dd, N, (const gpd_c64 *)dfc, n_fc, N, dfcop,
+                             dst, omega, xinit, flags, maxfun, (gpd_param *)dpar, (gpd_c64 *)dout, N,
+                             dbphi, g, s, errbuf_l, errlen_l);
+        if (r != GPD_OK) {
+            cleanup();
+            return fail(r);
+        }
+        ok = chk(hipMemcpyAsync(out_params + p0, dpar, P * sizeof(Param), hipMemcpyDeviceToHost, s),
+                 "D2H params") &&
+             (!out_demod || chk(hipMemcpy2DAsync(out_demod + p0 * ldo, ldo * sizeof(gpd_c64), dout,
+                                                 N * sizeof(c64), N * sizeof(c64), P,
+                                                 hipMemcpyDeviceToHost, s), "D2H out")) &&
+             chk(hipStreamSynchronize(s), "hipStreamSynchronize");
+        cleanup();
+        if (!ok) return fail(GPD_E_HIP);
+    };
+    if (G == 1) {
+        worker(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int g = 0; g < G; ++g) th.emplace_back(worker, g);
+        for (auto &x : th) x.join();
+    }
+    for (int g = 0; g < G; ++g) {
+        if (rc[g] != GPD_OK) {
+            set_err(errbuf, errlen, "device %d: %s", g, msg[g].c_str());
+            return rc[g];
+        }
+    }
+    return GPD_OK;
+}
+
+extern "C" {
+
+int gpd_fit_batch(int64_t n_samples, int64_t n_pixels, const double *t, const gpd_c64 *d,
+                  int64_t ldd, const gpd_c64 *fc, int64_t n_fc, int64_t ldfc,
+                  const int32_t *fc_of_pixel, const int8_t *state, double omega,
+                  const double *xinit, uint32_t flags, int32_t maxfun, gpd_param *out_params,
+                  gpd_c64 *out_demod, int64_t ldo, int32_t n_gpus, char *errbuf, size_t errlen) {
+    return host_batch(n_samples, n_pixels, t, d, ldd, fc, n_fc, ldfc, fc_of_pixel, state, omega,
+                      xinit, flags, maxfun, out_params, out_demod, ldo, nullptr, n_gpus, errbuf,
+                      errlen);
+}
+
+int gpd_chi2_batch(int64_t n_samples, int64_t n_pixels, const double *t, const gpd_c64 *d,
+                   int64_t ldd, const gpd_c64 *fc, int64_t n_fc, int64_t ldfc,
+                   const int32_t *fc_of_pixel, const int8_t *state, double omega,
+                   const double *bphi, uint32_t flags, gpd_param *out_params, int32_t n_gpus,
+                   char *errbuf, size_t errlen) {
+    if (!bphi) {
+        set_err(errbuf, errlen, "gpd_chi2_batch: bphi is NULL");
+        return GPD_E_ARG;
+    }
+    return host_batch(n_samples, n_pixels, t, d, ldd, fc, n_fc, ldfc, fc_of_pixel, state, omega,
+                      nullptr, flags, 0, out_params, nullptr, n_samples, bphi, n_gpus, errbuf,
+                      errlen);
+}
+
+int gpd_synth_fill_dev(int64_t n_samples, int64_t n_pixels, int64_t pixel_offset, uint64_t seed,
+                       double t0, double dt, double sigma, int with_offsets, double omega,
+                       double *t, gpd_c64 *d, int64_t ldd, gpd_c64 *fc, int64_t ldfc,
+                       int32_t *fc_of_pixel, gpd_param *truth, int device, void *stream_) {
+    char *errbuf = nullptr;
+    size_t errlen = 0;
+    if (n_samples < 1 || n_pixels < 1 || pixel_offset % 4 != 0 || !t || !d || !fc ||
+        !fc_of_pixel || ldd < n_samples || ldfc < n_samples)
+        return GPD_E_ARG;
+    HIP_TRY(hipSetDevice(device));
+    hipStream_t s = (hipStream_t)stream_;
+    const long long N = n_samples, P = n_pixels, nfc = (P + 3) / 4;
+    Param *tr = (Param *)truth;
+    Param *tmp = nullptr;
+    if (!tr) {
+        HIP_TRY(hipMallocAsync((void **)&tmp, P * sizeof(Param), s));
+        tr = tmp;
+    }
+    k_synth_t<<<(unsigned)((N + 255) / 256), 256, 0, s>>>(N, t0, dt, t);
+    k_synth_truth<<<(unsigned)((P + 255) / 256), 256, 0, s>>>(P, pixel_offset, seed, with_offsets, tr);
+    k_synth_fc<<<(unsigned)((nfc + 63) / 64), 64, 0, s>>>(N, nfc, pixel_offset / 4, seed, (c64 *)fc, ldfc);
+    dim3 g((unsigned)std::min<long long>((N + 255) / 256, 64), (unsigned)P);
+    k_synth_d<<<g, 256, 0, s>>>(N, P, pixel_offset, seed, t0, dt, sigma, omega, tr, (const c64 *)fc,
+                               ldfc, (c64 *)d, ldd, fc_of_pixel);
+    HIP_TRY(hipGetLastError());
+    if (tmp) HIP_TRY(hipFreeAsync(tmp, s));
+    return GPD_OK;
+}
+
+int gpd_buildstates(int64_t n, const double *t, int64_t n1, const double *timer1, int64_t n2,
+                    const double *timer2, double preswitchdelay, double postwitchdelay,
+                    int8_t *states) {
+    // src/Faint.jl:21-73, sequential state machine (host; O(N) once per exposure).
+    if (n < 2 || n1 < 1 || n2 < 1 || !t || !timer1 || !timer2 || !states) return GPD_E_ARG;
+    const double timestep = t[1] - t[0];
+    const long long premax = (long long)std::ceil(preswitchdelay / timestep);
+    const long long postmax = (long long)std::ceil(postwitchdelay / timestep);
+    const int8_t HIGH = GPD_STATE_HIGH, LOW = GPD_STATE_LOW, NORMAL = GPD_STATE_NORMAL;
+    int8_t current = NORMAL;
+    int64_t i1 = 0, i2 = 0;
+    double first1 = timer1[i1++], first2 = timer2[i2++];
+    const double tlast = t[n - 1];
+    long long forget = 0;
+    for (int64_t k = 0; k < n; ++k) {
+        const double time = t[k];
+        if (time >= first1) {  // HIGH switch
+            current = HIGH;
+            forget = premax;
+            if (i1 >= n1) {
+                first1 = tlast;
+                if (first2 == tlast) current = NORMAL;
+            } else {
+                first1 = timer1[i1++];
+            }
+        }
+        if (time >= first2) {  // LOW switch
+            current = LOW;
+            forget = postmax;
+            if (i2 >= n2) {
+                first2 = tlast;
+                if (first1 == tlast) current = NORMAL;
+            } else {
+                first2 = timer2[i2++];
+            }
+        }
+        if (forget > 0) {
+            states[k] = GPD_STATE_TRANSIENT;
+            forget -= 1;
+        } else {
+            states[k] = current;
+        }
+    }
+    return GPD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,857 @@
+// gfx950 kernels of the demodulation engine.  See DESIGN.md for the data layout and rooflines.
+//
+// Reference hot path (FerreolS/GPPupilDemodulation.jl @ 2024-10-16): the per-diode body of
+// demodulateall (src/Modulation.jl:388-432) — χ²(b,ϕ) (Chi2CostFunction, :245-330) minimised by
+// NEWUOA (:332-342) from an 8-point ϕ grid, π-flip check, final χ², output column, sign
+// normalisation — plus the faint-mode weights (src/Faint.jl:89-100).
+//
+// Two evaluators of χ²(b,ϕ), both feeding the same device NEWUOA (gpd_newuoa.hpp):
+//   exact     one workgroup per series, every χ² evaluation is a full pass over the samples
+//             with the reference's arithmetic (model → a (or c,a) → residual norm);
+//   harmonic  one HBM pass computes Jacobi–Anger moments F_n = Σ_i q_i e^{-j n x_i}
+//             (q = w p̄ d, x = fl(ω t)); afterwards χ² costs O(K) per evaluation:
+//             S(b,ϕ) = Σ_n J_n(b) e^{-j n ϕ} F_n,  N χ² = Σ w|d|² − |S|²/Σ w|p|².
+#pragma once
+
+#include "gpd_device.hpp"
+#include "gpd_newuoa.hpp"
+
+namespace gpd {
+
+constexpr int KH = 24;               // harmonics kept (|b| ≤ ~4.3 at 1e-16 tail)
+constexpr int NMOM = 3 + 4 * KH;     // F0r, F0i, W2, then (A,B,C,D)_n for n = 1..K
+constexpr int MOM_TS = 8;            // samples per LDS tile in the moment kernel
+constexpr int EXACT_WG = 256;        // threads per series in the exact evaluator
+constexpr double PI_F64 = 3.141592653589793;
+
+// ϕrange = range(-π, π, 8) (src/Modulation.jl:360), bit-exact Float64 values.
+__device__ __constant__ const double c_phi_grid[8] = {
+    -0x1.921fb54442d18p+1, -0x1.1f3b3855544c8p+1, -0x1.58ad76cccb8f0p+0, -0x1.cb91f3bbba140p-2,
+    0x1.cb91f3bbba140p-2,  0x1.58ad76cccb8f0p+0,  0x1.1f3b3855544c8p+1,  0x1.921fb54442d18p+1};
+
+// status bits (mirror include/gpdemod.h)
+constexpr int ST_REFIT = 0x1, ST_MAXFUN = 0x2, ST_NAN = 0x4, ST_EXACT = 0x8, ST_FALLBACK = 0x10;
+constexpr uint32_t F_OFFSETS = 0x1u, F_RECENTER = 0x2u, F_ONLY_HIGH = 0x4u;
+
+struct Param {  // == gpd_param
+    double c_re, c_im, a_re, a_im, b, phi, chi2;
+    int32_t nfev, status;
+};
+
+// Per-launch facts computed on device (k_prepare).
+struct Info {
+    long long nvalid;  // valid samples (shared by every series)
+    int mode;          // 0: harmonic, plain ϕ; 1: harmonic, ϕ quantised to the ulp of fl(ωt); 2: exact only
+    int pad;
+    double qbase;      // mode 1: a multiple of that ulp inside the binade of fl(ωt)
+    double xmin, xmax; // range of |fl(ω t)| over valid samples
+};
+
+struct Problem {
+    long long N, P;
+    const double *__restrict__ t;
+    const c64 *__restrict__ d;
+    long long ldd;
+    const c64 *__restrict__ fc;
+    long long ldfc, n_fc;
+    const int32_t *__restrict__ fcop;
+    const int8_t *__restrict__ state;  // nullptr: non-faint
+    double omega;
+    uint32_t flags;
+    int maxfun;
+    int has_xinit;
+    double x0, x1;
+};
+
+__device__ __forceinline__ bool sample_valid(const Problem &pb, long long i, int &st) {
+    if (pb.state == nullptr) {
+        st = 0;
+        return true;
+    }
+    st = pb.state[i];
+    if (st == -1) return false;  // TRANSIENT always dropped (src/Modulation.jl:380-382)
+    if (pb.flags & F_ONLY_HIGH) return st == 3 || st == 2;  // HIGH ∪ NORMAL (:375-376)
+    return true;
+}
+
+// FC phasor exp(im·angle(fc)) (src/Modulation.jl:388), Julia arithmetic.
+__device__ __forceinline__ c64 fc_phasor(c64 z) { return cisj(atan2(z.im, z.re)); }
+
+// ---------------------------------------------------------------------------------------
+// Driver shared by both evaluators (src/Modulation.jl:402-416).  F: double operator()(double(&)[2])
+template <class F>
+__device__ __forceinline__ void drive_fit(F &f, const Problem &pb, double (&x)[2], int &status) {
+    if (pb.has_xinit) {
+        x[0] = pb.x0;
+        x[1] = pb.x1;
+    } else {
+        double fg[8];
+        for (int k = 0; k < 8; ++k) {
+            double xx[2] = {0.1, c_phi_grid[k]};
+            fg[k] = f(xx);
+        }
+        int best = 0;  // findmin: first NaN wins, else first minimum
+#pragma unroll
+        for (int k = 1; k < 8; ++k) {
+            const bool keep = (fg[best] != fg[best]);  // best is NaN → stays
+            if (!keep && ((fg[k] != fg[k]) || fg[best] > fg[k])) best = k;
+        }
+        double g = c_phi_grid[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) g = (best == k) ? c_phi_grid[k] : g;
+        x[0] = 0.1;
+        x[1] = g;
+    }
+    Newuoa<2, 5> nw;
+    double fx;
+    int nf = nw.run(x, 1.0, 1e-3, pb.maxfun, f, fx);
+    if (nf >= pb.maxfun) status |= ST_MAXFUN;
+    const double lklval = f(x);
+    const double php = x[1] + (x[1] < 0 ? PI_F64 : -PI_F64);
+    double xf[2] = {x[0], php};
+    if (lklval > f(xf)) {  // "bad minima" (src/Modulation.jl:411-414)
+        status |= ST_REFIT;
+        x[1] = php;
+        nf = nw.run(x, 1.0, 1e-3, pb.maxfun, f, fx);
+        if (nf >= pb.maxfun) status |= ST_MAXFUN;
+    }
+}
+
+__device__ __forceinline__ void store_param(Param *out, double *raw, long long k, double c_re,
+                                            double c_im, double a_re, double a_im, double b,
+                                            double phi, double chi2, int nfev, int status) {
+    raw[2 * k] = b;  // pre-normalisation (b, ϕ) feed the output pass (src/Modulation.jl:417-425)
+    raw[2 * k + 1] = phi;
+    if (b < 0) {  // src/Modulation.jl:427-430
+        b *= -1;
+        phi += (phi < 0 ? PI_F64 : -PI_F64);
+    }
+    if (chi2 != chi2) status |= ST_NAN;
+    Param p;
+    p.c_re = c_re;
+    p.c_im = c_im;
+    p.a_re = a_re;
+    p.a_im = a_im;
+    p.b = b;
+    p.phi = phi;
+    p.chi2 = chi2;
+    p.nfev = nfev;
+    p.status = status;
+    out[k] = p;
+}
+
+// ---------------------------------------------------------------------------------------
+// k_prepare: one workgroup.  Counts valid samples and classifies fl(ωt) for the harmonic path.
+__global__ __launch_bounds__(1024) void k_prepare(Problem pb, Info *info) {
+    __shared__ double red[16 * 3];
+    double cnt = 0.0, xmn = 1.0e308, xmx = 0.0;
+    for (long long i = threadIdx.x; i < pb.N; i += 1024) {
+        int st;
+        if (!sample_valid(pb, i, st)) continue;
+        const double x = fabs(pb.omega * pb.t[i]);
+        cnt += 1.0;
+        xmn = fmin(xmn, x);
+        xmx = fmax(xmx, x);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        cnt += __shfl_xor(cnt, off, 64);
+        xmn = fmin(xmn, __shfl_xor(xmn, off, 64));
+        xmx = fmax(xmx, __shfl_xor(xmx, off, 64));
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) {
+        red[wave * 3] = cnt;
+        red[wave * 3 + 1] = xmn;
+        red[wave * 3 + 2] = xmx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 16; ++w) {
+            cnt += red[w * 3];
+            xmn = fmin(xmn, red[w * 3 + 1]);
+            xmx = fmax(xmx, red[w * 3 + 2]);
+        }
+        Info in;
+        in.nvalid = (long long)cnt;
+        in.xmin = xmn;
+        in.xmax = xmx;
+        in.pad = 0;
+        in.qbase = 0.0;
+        // Rounding of θ = fl(fl(ωt) + ϕ) (src/Modulation.jl:137).  While every |fl(ωt)| ± π sits
+        // in one binade [2^e, 2^(e+1)), fl(x+ϕ) = x + round(ϕ to a multiple of ulp 2^(e-52)):
+        // the harmonic path reproduces it by quantising ϕ.  Small |x| (< 2^16): the per-sample
+        // rounding noise is below 2e-11 rad and uncorrelated, harmonic without quantisation.
+        const double lo = xmn - PI_F64, hi = xmx + PI_F64;
+        int elo, ehi;
+        frexp(lo > 0 ? lo : 0.0, &elo);
+        frexp(hi, &ehi);
+        if (hi < 65536.0) {
+            in.mode = 0;
+        } else if (lo > 64.0 && elo == ehi) {
+            in.mode = 1;
+            in.qbase = ldexp(0.75, ehi);  // 1.5·2^(e) — a multiple of the ulp in that binade
+        } else {
+            in.mode = 2;
+        }
+        if (in.nvalid == 0) in.mode = 2;
+        *info = in;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// k_table: c_n(i) = cos(n x_i), s_n(i) = sin(n x_i), n = 1..K, x_i = fl(ω t_i), by the
+// angle-addition recurrence from sincos(x_i) (exact range reduction of x_i; error ~n·eps).
+__global__ __launch_bounds__(256) void k_table(const double *__restrict__ t, long long N,
+                                               double omega, double *__restrict__ tab) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= N) return;
+    const double x = omega * t[i];
+    double s1, c1;
+    sincos(x, &s1, &c1);
+    double cn = c1, sn = s1;
+    double *row = tab + i * (2 * KH);
+#pragma unroll
+    for (int n = 1; n <= KH; ++n) {
+        row[2 * (n - 1)] = cn;
+        row[2 * (n - 1) + 1] = sn;
+        const double cn1 = cn * c1 - sn * s1;
+        const double sn1 = sn * c1 + cn * s1;
+        cn = cn1;
+        sn = sn1;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// k_faint_stats: per series and MetState, m = mean(|d|), w = 1/var(|d|) (src/Faint.jl:89-100)
+// over the valid samples, plus Σ|d|² per state.  One workgroup per series.
+// out[k*16 + ...]: m[5] | w[5] | W2 | DEN | Q2 (state index = code + 1).
+__global__ __launch_bounds__(256) void k_faint_stats(Problem pb, double *__restrict__ out) {
+    __shared__ double lds[4 * 15];
+    const long long k = blockIdx.x;
+    const c64 *d = pb.d + k * pb.ldd;
+    double v[15];
+#pragma unroll
+    for (int q = 0; q < 15; ++q) v[q] = 0.0;
+    for (long long i = threadIdx.x; i < pb.N; i += 256) {
+        int st;
+        if (!sample_valid(pb, i, st)) continue;
+        const c64 z = d[i];
+        const double ad = hypot(z.re, z.im);
+        const double d2 = z.re * z.re + z.im * z.im;
+#pragma unroll
+        for (int q = 0; q < 5; ++q)
+            if (st + 1 == q) {
+                v[q] += 1.0;
+                v[5 + q] += ad;
+                v[10 + q] += d2;
+            }
+    }
+    block_sum<256, 15>(v, lds);
+    double m[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) m[q] = v[5 + q] / v[q];
+    double s[5] = {0, 0, 0, 0, 0};
+    for (long long i = threadIdx.x; i < pb.N; i += 256) {
+        int st;
+        if (!sample_valid(pb, i, st)) continue;
+        const c64 z = d[i];
+        const double ad = hypot(z.re, z.im);
+#pragma unroll
+        for (int q = 0; q < 5; ++q)
+            if (st + 1 == q) {
+                const double dv = ad - m[q];
+                s[q] += dv * dv;
+            }
+    }
+    block_sum<256, 5>(s, lds);
+    if (threadIdx.x == 0) {
+        double *o = out + k * 16;
+        double W2 = 0.0, DEN = 0.0, Q2 = 0.0;
+        for (int q = 0; q < 5; ++q) {
+            const double w = 1.0 / (s[q] / (v[q] - 1.0));
+            o[q] = m[q];
+            o[5 + q] = w;
+            if (v[q] > 0) {
+                W2 += w * v[10 + q];
+                DEN += w * m[q] * m[q] * v[q];
+                Q2 += (w * m[q]) * (w * m[q]) * v[10 + q];
+            }
+        }
+        o[10] = W2;
+        o[11] = DEN;
+        o[12] = Q2;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// k_phasor: FC phasor buffer for the exact evaluator (only when it fits the workspace).
+__global__ __launch_bounds__(256) void k_phasor(const c64 *__restrict__ fc, long long ldfc,
+                                                long long n_fc, long long N, c64 *__restrict__ ph) {
+    const long long g = blockIdx.y;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < N; i += (long long)gridDim.x * 256)
+        ph[g * N + i] = fc_phasor(fc[g * ldfc + i]);
+}
+
+// ---------------------------------------------------------------------------------------
+// HARMONIC PATH — k_moments: the HBM-streaming pass (roofline kernel).
+// One wave per workgroup; lane = series (64 series per workgroup); blockIdx.y = sample chunk.
+// Series tiles of MOM_TS samples are staged through LDS transposed ([sample][series]) from
+// coalesced 128-B row loads; the cos/sin table row of each sample is wave-uniform (SMEM).
+// Writes partial moments part[chunk][m][P].
+template <bool FAINT>
+__global__ __launch_bounds__(64) void k_moments(Problem pb, const double *__restrict__ tab,
+                                                const double *__restrict__ fstat,
+                                                long long chunk_len, double *__restrict__ part) {
+    __shared__ c64 dtile[MOM_TS][65];
+    __shared__ c64 ptile[MOM_TS][65];
+    const int lane = threadIdx.x;
+    const long long p0 = (long long)blockIdx.x * 64;
+    const long long pix = p0 + lane;
+    const long long s_begin = (long long)blockIdx.y * chunk_len;
+    long long s_end = s_begin + chunk_len;
+    if (s_end > pb.N) s_end = pb.N;
+
+    double wm[5];  // faint: w_s · m_s for this series
+    if (FAINT) {
+#pragma unroll
+        for (int q = 0; q < 5; ++q) wm[q] = pix < pb.P ? fstat[pix * 16 + 5 + q] * fstat[pix * 16 + q] : 0.0;
+    }
+    double acc[NMOM];
+#pragma unroll
+    for (int q = 0; q < NMOM; ++q) acc[q] = 0.0;
+
+    const int ls = lane & (MOM_TS - 1);   // sample within tile this lane stages
+    const int lp = lane / MOM_TS;          // series sub-row this lane stages
+    for (long long s0 = s_begin; s0 < s_end; s0 += MOM_TS) {
+        const long long ss = s0 + ls;
+#pragma unroll
+        for (int r = 0; r < 64 / MOM_TS; ++r) {
+            const long long pp = p0 + lp + r * (64 / MOM_TS) * 1;
+            const int prow = lp + r * (64 / MOM_TS);
+            c64 dv = {0.0, 0.0}, pv = {0.0, 0.0};
+            if (pp < pb.P && ss < s_end) {
+                dv = pb.d[pp * pb.ldd + ss];
+                const c64 z = pb.fc[(long long)pb.fcop[pp] * pb.ldfc + ss];
+                const double r2 = z.re * z.re + z.im * z.im;
+                if (r2 > 0.0) {
+                    const double inv = 1.0 / sqrt(r2);
+                    pv = {z.re * inv, z.im * inv};
+                } else {
+                    pv = {1.0, 0.0};  // angle(0) = 0
+                }
+            }
+            dtile[ls][prow] = dv;
+            ptile[ls][prow] = pv;
+        }
+        __syncthreads();
+        const int nts = (int)((s_end - s0) < MOM_TS ? (s_end - s0) : MOM_TS);
+        for (int s = 0; s < nts; ++s) {
+            const long long i = s0 + s;
+            int st = 0;
+            if (FAINT) {
+                if (!sample_valid(pb, i, st)) continue;  // wave-uniform
+            }
+            const c64 dv = dtile[s][lane];
+            const c64 pv = ptile[s][lane];
+            double qr = fma(pv.re, dv.re, pv.im * dv.im);   // q = p̄ d  (× w m in faint mode)
+            double qi = fma(pv.re, dv.im, -(pv.im * dv.re));
+            if (FAINT) {
+                double f = wm[0];
+#pragma unroll
+                for (int q = 1; q < 5; ++q) f = (st + 1 == q) ? wm[q] : f;
+                qr *= f;
+                qi *= f;
+            } else {
+                acc[2] = fma(dv.re, dv.re, fma(dv.im, dv.im, acc[2]));
+            }
+            acc[0] += qr;
+            acc[1] += qi;
+            const double *row = tab + i * (2 * KH);
+#pragma unroll
+            for (int n = 0; n < KH; ++n) {
+                const double c = row[2 * n], sn = row[2 * n + 1];
+                acc[3 + 4 * n + 0] = fma(qr, c, acc[3 + 4 * n + 0]);
+                acc[3 + 4 * n + 1] = fma(qi, sn, acc[3 + 4 * n + 1]);
+                acc[3 + 4 * n + 2] = fma(qi, c, acc[3 + 4 * n + 2]);
+                acc[3 + 4 * n + 3] = fma(qr, sn, acc[3 + 4 * n + 3]);
+            }
+        }
+        __syncthreads();
+    }
+    if (pix < pb.P) {
+        double *o = part + (long long)blockIdx.y * NMOM * pb.P + pix;
+#pragma unroll
+        for (int q = 0; q < NMOM; ++q) o[(long long)q * pb.P] = acc[q];
+    }
+}
+
+// k_reduce_moments: mom[m][k] = Σ_chunk part[chunk][m][k] (fixed order), plus per-series
+// aux[k] = {W2, DEN, Q2, 0}.
+__global__ __launch_bounds__(256) void k_reduce_moments(const double *__restrict__ part, int nch,
+                                                        long long P, const Info *__restrict__ info,
+                                                        const double *__restrict__ fstat, int faint,
+                                                        double *__restrict__ mom,
+                                                        double *__restrict__ aux) {
+    const long long k = (long long)blockIdx.x * 256 + threadIdx.x;
+    const int m = blockIdx.y;
+    if (k >= P) return;
+    double s = 0.0;
+    for (int c = 0; c < nch; ++c) s += part[((long long)c * NMOM + m) * P + k];
+    mom[(long long)m * P + k] = s;
+    if (m == 2) {
+        if (faint) {
+            aux[4 * k + 0] = fstat[k * 16 + 10];
+            aux[4 * k + 1] = fstat[k * 16 + 11];
+            aux[4 * k + 2] = fstat[k * 16 + 12];
+        } else {
+            aux[4 * k + 0] = s;                    // Σ|d|²
+            aux[4 * k + 1] = (double)info->nvalid;  // Σ|p|² (|p| = 1)
+            aux[4 * k + 2] = s;                    // Σ|q|² = Σ|d|²
+        }
+        aux[4 * k + 3] = 0.0;
+    }
+}
+
+// χ²(b,ϕ) from the moments of one series (lane).
+struct HarmChi2 {
+    const double *__restrict__ mom;
+    long long P, k;
+    double nvalid, W2, DEN, tailref, qbase;
+    double a_re, a_im;
+    int nfev;
+    bool fallback;
+
+    __device__ double operator()(const double (&x)[2]) {
+        ++nfev;
+        if (fallback) return 0.0;
+        const double b = x[0];
+        double phi = x[1];
+        double J[KH + 2];
+        bessel_j<KH + 1>(b, J);
+        if (!(fabs(b) < 0.45 * KH) || fabs(J[KH + 1]) > tailref) {
+            fallback = true;  // truncated expansion not exact here → exact evaluator
+            return 0.0;
+        }
+        if (qbase != 0.0) phi = (qbase + phi) - qbase;  // θ = fl(x + ϕ) = x + ϕ_q (one binade)
+        double sph, cph;
+        sincos(phi, &sph, &cph);
+        double Sr = J[0] * mom[0 * P + k];
+        double Si = J[0] * mom[1 * P + k];
+        double cn = 1.0, sn = 0.0;
+#pragma unroll
+        for (int n = 1; n <= KH; ++n) {
+            const double c2 = cn * cph - sn * sph;
+            const double s2 = sn * cph + cn * sph;
+            cn = c2;
+            sn = s2;
+            const double A = mom[(long long)(3 + 4 * (n - 1) + 0) * P + k];
+            const double B = mom[(long long)(3 + 4 * (n - 1) + 1) * P + k];
+            const double C = mom[(long long)(3 + 4 * (n - 1) + 2) * P + k];
+            const double D = mom[(long long)(3 + 4 * (n - 1) + 3) * P + k];
+            double tr, ti;
+            if ((n & 1) == 0) {
+                tr = fma(A, cn, -(D * sn));
+                ti = fma(C, cn, -(B * sn));
+            } else {
+                tr = fma(B, cn, C * sn);
+                ti = -fma(D, cn, A * sn);
+            }
+            const double j2 = 2.0 * J[n];
+            Sr = fma(j2, tr, Sr);
+            Si = fma(j2, ti, Si);
+        }
+        a_re = Sr / DEN;  // a = Σ w m̄ d / Σ w|m|²  (src/Modulation.jl:144)
+        a_im = Si / DEN;
+        const double chi2n = W2 - (Sr * Sr + Si * Si) / DEN;
+        return chi2n / nvalid;
+    }
+};
+
+// k_fit_harmonic: lane = series.  Series whose NEWUOA probes leave the expansion's safe
+// range are appended to `list` for the exact evaluator.
+__global__ __launch_bounds__(64) void k_fit_harmonic(Problem pb, const Info *__restrict__ info,
+                                                     const double *__restrict__ mom,
+                                                     const double *__restrict__ aux,
+                                                     Param *__restrict__ out, double *__restrict__ raw,
+                                                     int *__restrict__ list, int *__restrict__ count) {
+    const long long k = (long long)blockIdx.x * 64 + threadIdx.x;
+    if (k >= pb.P) return;
+    const Info in = *info;
+    if (in.mode == 2) {  // harmonic path unusable for these timestamps
+        list[atomicAdd(count, 1)] = (int)k;
+        return;
+    }
+    HarmChi2 f;
+    f.mom = mom;
+    f.P = pb.P;
+    f.k = k;
+    f.nvalid = (double)in.nvalid;
+    f.W2 = aux[4 * k + 0];
+    f.DEN = aux[4 * k + 1];
+    const double Q2 = aux[4 * k + 2];
+    // tail bound: |Σ_{|n|>K} J_n e^{-jnϕ} F_n| ≤ 2|J_{K+1}| sqrt(N Σ|q|²) ≤ 1e-16 sqrt(W2·DEN)
+    f.tailref = 0.5e-16 * sqrt(f.W2 * f.DEN) / sqrt(f.nvalid * Q2);
+    f.qbase = in.mode == 1 ? in.qbase : 0.0;
+    f.a_re = f.a_im = 0.0;
+    f.nfev = 0;
+    f.fallback = false;
+    double x[2];
+    int status = 0;
+    drive_fit(f, pb, x, status);
+    const double chi2 = f(x);  // likelihood[idx] = lkl(x) (src/Modulation.jl:416)
+    if (f.fallback) {
+        list[atomicAdd(count, 1)] = (int)k;
+        return;
+    }
+    store_param(out, raw, k, 0.0, 0.0, f.a_re, f.a_im, x[0], x[1], chi2, f.nfev, status);
+}
+
+// ---------------------------------------------------------------------------------------
+// EXACT PATH — one workgroup per series, NEWUOA replicated on every thread (uniform control
+// flow), χ² as a cooperative pass with the reference arithmetic.
+template <bool FAINT, bool OFFS, bool PHBUF>
+struct ExactChi2 {
+    const Problem *pb;
+    const c64 *__restrict__ d;
+    const c64 *__restrict__ src;  // PHBUF: phasor column; else raw FC column
+    double *lds;
+    double m5[5], w5[5];
+    double nvalid;
+    double a_re, a_im, c_re, c_im;
+    int nfev;
+
+    __device__ __forceinline__ bool load(long long i, c64 &p, double &w) const {
+        int st;
+        if (!sample_valid(*pb, i, st)) return false;
+        const c64 ph = PHBUF ? src[i] : fc_phasor(src[i]);
+        if (FAINT) {
+            double m = m5[0], ww = w5[0];
+#pragma unroll
+            for (int q = 1; q < 5; ++q) {
+                m = (st + 1 == q) ? m5[q] : m;
+                ww = (st + 1 == q) ? w5[q] : ww;
+            }
+            p = {m * ph.re, m * ph.im};  // power .* FCphasor (src/Modulation.jl:396)
+            w = ww;
+        } else {
+            p = ph;
+            w = 1.0;
+        }
+        return true;
+    }
+    __device__ __forceinline__ c64 model(long long i, const c64 &p, double b, double phi) const {
+        double th = pb->omega * pb->t[i];
+        th = th + phi;
+        const double beta = b * sin(th);
+        return cmul(p, cisj(beta));  // power * exp(ȷ b sin(ωt+ϕ)) (src/Modulation.jl:137)
+    }
+
+    __device__ double operator()(const double (&x)[2]) {
+        ++nfev;
+        const double b = x[0], phi = x[1];
+        const long long N = pb->N;
+        if (OFFS) {
+            double v[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // a11, a12(2), a22, b1(2), b2(2)
+            for (long long i = threadIdx.x; i < N; i += EXACT_WG) {
+                c64 p;
+                double w;
+                if (!load(i, p, w)) continue;
+                const c64 m = model(i, p, b, phi);
+                const c64 dd = d[i];
+                v[0] += w;
+                v[1] += w * m.re;
+                v[2] += w * m.im;
+                v[3] += w * (m.re * m.re + m.im * m.im);
+                v[4] += w * dd.re;
+                v[5] += w * dd.im;
+                const c64 pr = cmul(c64{w * m.re, w * (-m.im)}, dd);
+                v[6] += pr.re;
+                v[7] += pr.im;
+            }
+            block_sum<EXACT_WG, 8>(v, lds);
+            // StaticArrays 2×2 Cramer solve (src/Modulation.jl:189-192)
+            const c64 A11 = {v[0], 0.0}, A12 = {v[1], v[2]}, A21 = {v[1], -v[2]}, A22 = {v[3], 0.0};
+            const c64 b1 = {v[4], v[5]}, b2 = {v[6], v[7]};
+            const c64 t1 = cmul(A11, A22), t2 = cmul(A12, A21);
+            const c64 det = {t1.re - t2.re, t1.im - t2.im};
+            const c64 u1 = cmul(A22, b1), u2 = cmul(A12, b2);
+            const c64 v1 = cmul(A11, b2), v2 = cmul(A21, b1);
+            const c64 cc = cdiv(c64{u1.re - u2.re, u1.im - u2.im}, det);
+            const c64 aa = cdiv(c64{v1.re - v2.re, v1.im - v2.im}, det);
+            c_re = cc.re;
+            c_im = cc.im;
+            a_re = aa.re;
+            a_im = aa.im;
+        } else {
+            double v[4] = {0, 0, 0, 0};  // num(2), den(2)
+            for (long long i = threadIdx.x; i < N; i += EXACT_WG) {
+                c64 p;
+                double w;
+                if (!load(i, p, w)) continue;
+                const c64 m = model(i, p, b, phi);
+                const c64 mwc = {m.re * w, -(m.im * w)};  // conj(model .* weight)
+                const c64 xx = cmul(mwc, d[i]);
+                const c64 yy = cmul(mwc, m);
+                v[0] += xx.re;
+                v[1] += xx.im;
+                v[2] += yy.re;
+                v[3] += yy.im;
+            }
+            block_sum<EXACT_WG, 4>(v, lds);
+            const c64 aa = cdiv(c64{v[0], v[1]}, c64{v[2], v[3]});  // (src/Modulation.jl:144)
+            c_re = c_im = 0.0;
+            a_re = aa.re;
+            a_im = aa.im;
+        }
+        // weighted_norm2(model .- data, weight) / N  (src/Modulation.jl:299-305, 325)
+        double s[1] = {0.0};
+        const c64 aa = {a_re, a_im};
+        for (long long i = threadIdx.x; i < N; i += EXACT_WG) {
+            c64 p;
+            double w;
+            if (!load(i, p, w)) continue;
+            c64 mm = cmul(aa, model(i, p, b, phi));
+            if (OFFS) {
+                mm.re = c_re + mm.re;
+                mm.im = c_im + mm.im;
+            }
+            const c64 dd = d[i];
+            const double rr = mm.re - dd.re, ri = mm.im - dd.im;
+            s[0] += w * (rr * rr + ri * ri);
+        }
+        block_sum<EXACT_WG, 1>(s, lds);
+        return s[0] / nvalid;
+    }
+};
+
+template <bool FAINT, bool OFFS, bool PHBUF>
+__global__ __launch_bounds__(EXACT_WG) void k_fit_exact(Problem pb, const Info *__restrict__ info,
+                                                        const c64 *__restrict__ phbuf,
+                                                        const double *__restrict__ fstat,
+                                                        const int *__restrict__ list,
+                                                        const int *__restrict__ count,
+                                                        Param *__restrict__ out,
+                                                        double *__restrict__ raw, int extra_status) {
+    __shared__ double lds[(EXACT_WG / 64) * 8];
+    const long long total = list ? (long long)(*count) : pb.P;
+    const double nvalid = (double)info->nvalid;
+    for (long long idx = blockIdx.x; idx < total; idx += gridDim.x) {
+        const long long k = list ? (long long)list[idx] : idx;
+        ExactChi2<FAINT, OFFS, PHBUF> f;
+        f.pb = &pb;
+        f.d = pb.d + k * pb.ldd;
+        const long long g = pb.fcop[k];
+        f.src = PHBUF ? phbuf + g * pb.N : pb.fc + g * pb.ldfc;
+        f.lds = lds;
+        f.nvalid = nvalid;
+        if (FAINT) {
+#pragma unroll
+            for (int q = 0; q < 5; ++q) {
+                f.m5[q] = fstat[k * 16 + q];
+                f.w5[q] = fstat[k * 16 + 5 + q];
+            }
+        }
+        f.a_re = f.a_im = f.c_re = f.c_im = 0.0;
+        f.nfev = 0;
+        double x[2];
+        int status = ST_EXACT | extra_status;
+        drive_fit(f, pb, x, status);
+        const double chi2 = f(x);
+        if (threadIdx.x == 0)
+            store_param(out, raw, k, f.c_re, f.c_im, f.a_re, f.a_im, x[0], x[1], chi2, f.nfev, status);
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// χ²(b_k, ϕ_k) for every series at a given point: the Chi2CostFunction functor
+// (src/Modulation.jl:318-330) as a batch operation (one evaluation, no optimisation).
+template <bool FAINT, bool OFFS, bool PHBUF>
+__global__ __launch_bounds__(EXACT_WG) void k_chi2_exact(Problem pb, const Info *__restrict__ info,
+                                                         const c64 *__restrict__ phbuf,
+                                                         const double *__restrict__ fstat,
+                                                         const double *__restrict__ bphi,
+                                                         Param *__restrict__ out) {
+    __shared__ double lds[(EXACT_WG / 64) * 8];
+    const long long k = blockIdx.x;
+    ExactChi2<FAINT, OFFS, PHBUF> f;
+    f.pb = &pb;
+    f.d = pb.d + k * pb.ldd;
+    const long long g = pb.fcop[k];
+    f.src = PHBUF ? phbuf + g * pb.N : pb.fc + g * pb.ldfc;
+    f.lds = lds;
+    f.nvalid = (double)info->nvalid;
+    if (FAINT) {
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            f.m5[q] = fstat[k * 16 + q];
+            f.w5[q] = fstat[k * 16 + 5 + q];
+        }
+    }
+    f.nfev = 0;
+    double x[2] = {bphi[2 * k], bphi[2 * k + 1]};
+    const double chi2 = f(x);
+    if (threadIdx.x == 0) {
+        Param p;
+        p.c_re = f.c_re;
+        p.c_im = f.c_im;
+        p.a_re = f.a_re;
+        p.a_im = f.a_im;
+        p.b = x[0];
+        p.phi = x[1];
+        p.chi2 = chi2;
+        p.nfev = 1;
+        p.status = ST_EXACT;
+        out[k] = p;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_chi2_harmonic(Problem pb, const Info *__restrict__ info,
+                                                      const double *__restrict__ mom,
+                                                      const double *__restrict__ aux,
+                                                      const double *__restrict__ bphi,
+                                                      Param *__restrict__ out) {
+    const long long k = (long long)blockIdx.x * 64 + threadIdx.x;
+    if (k >= pb.P) return;
+    const Info in = *info;
+    HarmChi2 f;
+    f.mom = mom;
+    f.P = pb.P;
+    f.k = k;
+    f.nvalid = (double)in.nvalid;
+    f.W2 = aux[4 * k + 0];
+    f.DEN = aux[4 * k + 1];
+    f.tailref = 0.5e-16 * sqrt(f.W2 * f.DEN) / sqrt(f.nvalid * aux[4 * k + 2]);
+    f.qbase = in.mode == 1 ? in.qbase : 0.0;
+    f.a_re = f.a_im = 0.0;
+    f.nfev = 0;
+    f.fallback = in.mode == 2;
+    double x[2] = {bphi[2 * k], bphi[2 * k + 1]};
+    const double chi2 = f(x);
+    Param p;
+    p.c_re = p.c_im = 0.0;
+    p.a_re = f.a_re;
+    p.a_im = f.a_im;
+    p.b = x[0];
+    p.phi = x[1];
+    p.chi2 = f.fallback ? __builtin_nan("") : chi2;
+    p.nfev = 1;
+    p.status = f.fallback ? ST_FALLBACK : 0;
+    out[k] = p;
+}
+
+// ---------------------------------------------------------------------------------------
+// k_output: demodulated column over ALL samples (src/Modulation.jl:417-425).
+__global__ __launch_bounds__(256) void k_output(Problem pb, const Param *__restrict__ par,
+                                                const double *__restrict__ raw,
+                                                c64 *__restrict__ outd, long long ldo) {
+    const long long k = blockIdx.y;
+    const Param pk = par[k];
+    const double b = raw[2 * k], phi = raw[2 * k + 1];
+    const double arga = atan2(pk.a_im, pk.a_re);
+    const c64 aa = {pk.a_re, pk.a_im};
+    const bool offs = (pb.flags & F_OFFSETS) != 0;
+    const c64 *d = pb.d + k * pb.ldd;
+    c64 *o = outd + k * ldo;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < pb.N; i += (long long)gridDim.x * 256) {
+        double th = pb.omega * pb.t[i];
+        th = th + phi;
+        c64 dd = d[i];
+        if (pb.flags & F_RECENTER) {
+            double ph = b * sin(th);  // getphase (src/Modulation.jl:66-69)
+            ph = ph + arga;
+            const double psi = ph - arga;
+            if (offs) {
+                dd.re = dd.re - pk.c_re;
+                dd.im = dd.im - pk.c_im;
+            }
+            o[i] = cmul(dd, cisj(-psi));
+        } else {
+            c64 mv = cmul(aa, cisj(b * sin(th)));
+            if (offs) {
+                mv.re = pk.c_re + mv.re;
+                mv.im = pk.c_im + mv.im;
+            }
+            o[i] = cmul(dd, cisj(-atan2(mv.im, mv.re)));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Synthetic data (benchmarks).  Same counter-based RNG streams as tests/synth.py.
+__global__ __launch_bounds__(256) void k_synth_truth(long long P, long long pixel_offset,
+                                                     uint64_t seed, int with_offsets, Param *truth) {
+    const long long k = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (k >= P) return;
+    const uint64_t gk = (uint64_t)(pixel_offset + k);
+    Param p;
+    p.b = 0.3 + 2.2 * rng_uniform(seed, 1, gk);
+    p.phi = -PI_F64 + 2 * PI_F64 * rng_uniform(seed, 2, gk);
+    const double amp = 0.5 + rng_uniform(seed, 3, gk);
+    const double arga = -PI_F64 + 2 * PI_F64 * rng_uniform(seed, 4, gk);
+    double s, c;
+    sincos(arga, &s, &c);
+    p.a_re = amp * c;
+    p.a_im = amp * s;
+    if (with_offsets) {
+        p.c_re = 0.1 * rng_normal(seed, 5, gk) / sqrt(2.0);
+        p.c_im = 0.1 * rng_normal(seed, 6, gk) / sqrt(2.0);
+    } else {
+        p.c_re = p.c_im = 0.0;
+    }
+    p.chi2 = 0.0;
+    p.nfev = 0;
+    p.status = 0;
+    truth[k] = p;
+}
+
+__global__ __launch_bounds__(64) void k_synth_fc(long long N, long long n_fc, long long fc_offset,
+                                                 uint64_t seed, c64 *fc, long long ldfc) {
+    const long long g = (long long)blockIdx.x * 64 + threadIdx.x;
+    if (g >= n_fc) return;
+    const uint64_t gg = (uint64_t)(fc_offset + g);
+    double Phi = 2 * PI_F64 * rng_uniform(seed, 7, gg);
+    c64 *col = fc + g * ldfc;
+    for (long long i = 0; i < N; ++i) {
+        Phi += 1e-3 * rng_normal(seed, 100 + gg, (uint64_t)i);
+        double s, c;
+        sincos(Phi, &s, &c);
+        col[i] = {1.3 * c, 1.3 * s};
+    }
+}
+
+__global__ __launch_bounds__(256) void k_synth_d(long long N, long long P, long long pixel_offset,
+                                                 uint64_t seed, double t0, double dt, double sigma,
+                                                 double omega, const Param *__restrict__ truth,
+                                                 const c64 *__restrict__ fc, long long ldfc,
+                                                 c64 *__restrict__ d, long long ldd,
+                                                 int32_t *__restrict__ fcop) {
+    const long long k = blockIdx.y;
+    const Param tr = truth[k];
+    const uint64_t gk = (uint64_t)(pixel_offset + k);
+    const long long g = k / 4;
+    if (blockIdx.x == 0 && threadIdx.x == 0) fcop[k] = (int32_t)g;
+    const c64 *fcol = fc + g * ldfc;
+    c64 *col = d + k * ldd;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < N; i += (long long)gridDim.x * 256) {
+        const double t = t0 + (double)i * dt;
+        const c64 z = fcol[i];
+        const double r = sqrt(z.re * z.re + z.im * z.im);
+        const c64 p = {z.re / r, z.im / r};
+        const c64 e = cisj(tr.b * sin(omega * t + tr.phi));
+        const c64 ae = cmul(c64{tr.a_re, tr.a_im}, e);
+        const c64 mdl = {tr.c_re + ae.re, tr.c_im + ae.im};
+        const c64 pm = cmul(p, mdl);
+        const double n1 = rng_normal(seed, 1000 + 2 * gk, (uint64_t)i);
+        const double n2 = rng_normal(seed, 1001 + 2 * gk, (uint64_t)i);
+        col[i] = {pm.re + sigma * n1 / sqrt(2.0), pm.im + sigma * n2 / sqrt(2.0)};
+    }
+}
+
+__global__ __launch_bounds__(256) void k_synth_t(long long N, double t0, double dt, double *t) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i < N) t[i] = t0 + (double)i * dt;
+}
+
+}  // namespace gpd

@@ -1,0 +1,1283 @@
+// Device-side Powell NEWUOA for the per-series (b, ϕ) fit.
+//
+// Replaces OptimPackNextGen.Powell.Newuoa.newuoa as called by minimize!
+// (src/Modulation.jl:332-342: newuoa(f, xinit, 1, 1e-3; check=false), npt = 2n+1 = 5,
+// maxfun = 30n = 60 by default).  Algorithm: M.J.D. Powell, "The NEWUOA software for
+// unconstrained optimization without derivatives" (DAMTP 2004/NA05) — NEWUOB, TRSAPP,
+// BIGLAG, BIGDEN, UPDATE.  This is a structured re-implementation for GPU threads: fixed
+// N/NPT known at compile time so every array lives in registers, runtime interpolation-point
+// indices go through branch-free select helpers, and the objective is a device functor so the
+// same code serves the wave-cooperative exact evaluator and the lane-per-series harmonic one.
+// Every floating-point expression keeps the operation order of the published algorithm
+// (compile with -ffp-contract=off) so trajectories agree with the CPU oracle to rounding.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+namespace gpd {
+
+#define GPD_HD __host__ __device__ __forceinline__
+#define GPD_HDN __host__ __device__
+
+// ---------------------------------------------------------------- select helpers ------
+template <int L>
+GPD_HD double rd(const double (&a)[L], int k) {  // a[k], k runtime (0-based)
+    double v = a[0];
+#pragma unroll
+    for (int j = 1; j < L; ++j) v = (k == j) ? a[j] : v;
+    return v;
+}
+template <int L>
+GPD_HD void wr(double (&a)[L], int k, double v) {
+#pragma unroll
+    for (int j = 0; j < L; ++j)
+        if (k == j) a[j] = v;
+}
+template <int R, int C>
+GPD_HD double rd2(const double (&a)[R][C], int r, int c) {  // a[r][c], r runtime, c static
+    double v = a[0][c];
+#pragma unroll
+    for (int j = 1; j < R; ++j) v = (r == j) ? a[j][c] : v;
+    return v;
+}
+template <int R, int C>
+GPD_HD void wr2(double (&a)[R][C], int r, int c, double v) {
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+        if (r == j) a[j][c] = v;
+}
+// column c runtime, row static
+template <int R, int C>
+GPD_HD double rdc(const double (&a)[R][C], int r, int c) {
+    double v = a[r][0];
+#pragma unroll
+    for (int j = 1; j < C; ++j) v = (c == j) ? a[r][j] : v;
+    return v;
+}
+template <int R, int C>
+GPD_HD void wrc(double (&a)[R][C], int r, int c, double v) {
+#pragma unroll
+    for (int j = 0; j < C; ++j)
+        if (c == j) a[r][j] = v;
+}
+
+constexpr double kTwoPi = 6.283185307179586476925286766559;  // 8·atan(1)
+
+template <int N, int NPT>
+struct Newuoa {
+    static constexpr int NDIM = NPT + N;
+    static constexpr int NPTM = NPT - N - 1;
+    static constexpr int NH = N * (N + 1) / 2;
+
+    // persistent state (NEWUOB)
+    double xbase[N], xopt[N], xnew[N], xpt[NPT][N], fval[NPT], gq[N], hq[NH], pq[NPT];
+    double bmat[NDIM][N], zmat[NPT][NPTM], d[N], vlag[NDIM], w[NDIM];
+
+    // ---------------------------------------------------- hd = ∇²Q · v (TRSAPP label 170)
+    GPD_HD void hess_mul(const double (&v)[N], double (&hd)[N]) const {
+#pragma unroll
+        for (int i = 0; i < N; ++i) hd[i] = 0.0;
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            double temp = 0.0;
+#pragma unroll
+            for (int j = 0; j < N; ++j) temp = temp + xpt[k][j] * v[j];
+            temp = temp * pq[k];
+#pragma unroll
+            for (int i = 0; i < N; ++i) hd[i] = hd[i] + temp * xpt[k][i];
+        }
+        int ih = 0;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+#pragma unroll
+            for (int i = 0; i <= j; ++i) {
+                if (i < j) hd[j] = hd[j] + hq[ih] * v[i];
+                hd[i] = hd[i] + hq[ih] * v[j];
+                ++ih;
+            }
+        }
+    }
+
+    // ------------------------------------------------------------------------- TRSAPP
+    // Truncated CG + 2-D boundary search for the trust-region step.  Writes step, crvmin.
+    GPD_HDN void trsapp(double delta, double (&step)[N], double &crvmin) const {
+        double dv[N], g[N], hd[N], hs[N];
+        const double delsq = delta * delta;
+        int iterc = 0;
+        const int itermax = N;
+        double dd, ds, ss, gg, ggbeg, qred, bstep, alpha, dhd, temp;
+        double sg = 0, shs = 0;
+        hess_mul(xopt, hd);
+        qred = 0.0;
+        dd = 0.0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            step[i] = 0.0;
+            hs[i] = 0.0;
+            g[i] = gq[i] + hd[i];
+            dv[i] = -g[i];
+            dd = dd + dv[i] * dv[i];
+        }
+        crvmin = 0.0;
+        if (dd == 0.0) return;
+        ds = 0.0;
+        ss = 0.0;
+        gg = dd;
+        ggbeg = gg;
+        // ---- conjugate-gradient phase
+        for (;;) {
+            ++iterc;
+            temp = delsq - ss;
+            bstep = temp / (ds + sqrt(ds * ds + dd * temp));
+            hess_mul(dv, hd);
+            dhd = 0.0;
+#pragma unroll
+            for (int j = 0; j < N; ++j) dhd = dhd + dv[j] * hd[j];
+            alpha = bstep;
+            if (dhd > 0.0) {
+                temp = dhd / dd;
+                if (iterc == 1) crvmin = temp;
+                crvmin = fmin(crvmin, temp);
+                alpha = fmin(alpha, gg / dhd);
+            }
+            const double qadd = alpha * (gg - 0.5 * alpha * dhd);
+            qred = qred + qadd;
+            const double ggsav = gg;
+            gg = 0.0;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                step[i] = step[i] + alpha * dv[i];
+                hs[i] = hs[i] + alpha * hd[i];
+                gg = gg + (g[i] + hs[i]) * (g[i] + hs[i]);
+            }
+            if (!(alpha < bstep)) break;  // reached the boundary
+            if (qadd <= 0.01 * qred) return;
+            if (gg <= 1.0e-4 * ggbeg) return;
+            if (iterc == itermax) return;
+            temp = gg / ggsav;
+            dd = 0.0;
+            ds = 0.0;
+            ss = 0.0;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                dv[i] = temp * dv[i] - g[i] - hs[i];
+                dd = dd + dv[i] * dv[i];
+                ds = ds + dv[i] * step[i];
+                ss = ss + step[i] * step[i];
+            }
+            if (ds <= 0.0) return;
+            if (!(ss < delsq)) break;
+        }
+        crvmin = 0.0;
+        // ---- alternative iterations on the boundary
+        for (;;) {
+            if (gg <= 1.0e-4 * ggbeg) return;
+            sg = 0.0;
+            shs = 0.0;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                sg = sg + step[i] * g[i];
+                shs = shs + step[i] * hs[i];
+            }
+            const double sgk = sg + shs;
+            const double angtest = sgk / sqrt(gg * delsq);
+            if (angtest <= -0.99) return;
+            ++iterc;
+            temp = sqrt(delsq * gg - sgk * sgk);
+            const double ta = delsq / temp, tb = sgk / temp;
+#pragma unroll
+            for (int i = 0; i < N; ++i) dv[i] = ta * (g[i] + hs[i]) - tb * step[i];
+            hess_mul(dv, hd);
+            double dg = 0.0, dhs = 0.0;
+            dhd = 0.0;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                dg = dg + dv[i] * g[i];
+                dhd = dhd + hd[i] * dv[i];
+                dhs = dhs + hd[i] * step[i];
+            }
+            const double cf = 0.5 * (shs - dhd);
+            const double qbeg = sg + cf;
+            double qsav = qbeg, qmin = qbeg, qnew = qbeg, tempa = 0.0, tempb = 0.0;
+            int isave = 0;
+            const int iu = 49;
+            const double dang = kTwoPi / (double)(iu + 1);
+            for (int i = 1; i <= iu; ++i) {
+                const double ang = (double)i * dang;
+                const double cth = cos(ang), sth = sin(ang);
+                qnew = (sg + cf * cth) * cth + (dg + dhs * cth) * sth;
+                if (qnew < qmin) {
+                    qmin = qnew;
+                    isave = i;
+                    tempa = qsav;
+                } else if (i == isave + 1) {
+                    tempb = qnew;
+                }
+                qsav = qnew;
+            }
+            if (isave == 0) tempa = qnew;
+            if (isave == iu) tempb = qbeg;
+            double ang = 0.0;
+            if (tempa != tempb) {
+                tempa = tempa - qmin;
+                tempb = tempb - qmin;
+                ang = 0.5 * (tempa - tempb) / (tempa + tempb);
+            }
+            ang = dang * ((double)isave + ang);
+            const double cth = cos(ang), sth = sin(ang);
+            const double reduc = qbeg - (sg + cf * cth) * cth - (dg + dhs * cth) * sth;
+            gg = 0.0;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                step[i] = cth * step[i] + sth * dv[i];
+                hs[i] = cth * hs[i] + sth * hd[i];
+                gg = gg + (g[i] + hs[i]) * (g[i] + hs[i]);
+            }
+            qred = qred + reduc;
+            const double ratio = reduc / qred;
+            if (!(iterc < itermax && ratio > 0.01)) return;
+        }
+    }
+
+    // H column of point knew (1-based): hcol[k] = Σ_j ±zmat[knew][j] zmat[k][j]
+    GPD_HD void h_column(int knew, int idz, double (&hcol)[NPT]) const {
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) hcol[k] = 0.0;
+#pragma unroll
+        for (int j = 0; j < NPTM; ++j) {
+            double temp = rd2(zmat, knew - 1, j);
+            if (j + 1 < idz) temp = -temp;
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) hcol[k] = hcol[k] + temp * zmat[k][j];
+        }
+    }
+
+    // ------------------------------------------------------------------------- BIGLAG
+    // Step that (approximately) maximises |Lagrange function knew| within radius delta.
+    GPD_HDN void biglag(int idz, int knew, double delta, double &alpha) {
+        double hcol[NPT], gc[N], gd[N], s[N], wv[N];
+        const double delsq = delta * delta;
+        h_column(knew, idz, hcol);
+        alpha = rd(hcol, knew - 1);
+        double dd = 0.0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            d[i] = rd2(xpt, knew - 1, i) - xopt[i];
+            gc[i] = rd2(bmat, knew - 1, i);
+            gd[i] = 0.0;
+            dd = dd + d[i] * d[i];
+        }
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            double temp = 0.0, sum = 0.0;
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                temp = temp + xpt[k][j] * xopt[j];
+                sum = sum + xpt[k][j] * d[j];
+            }
+            temp = hcol[k] * temp;
+            sum = hcol[k] * sum;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                gc[i] = gc[i] + temp * xpt[k][i];
+                gd[i] = gd[i] + sum * xpt[k][i];
+            }
+        }
+        double gg = 0.0, sp = 0.0, dhd = 0.0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            gg = gg + gc[i] * gc[i];
+            sp = sp + d[i] * gc[i];
+            dhd = dhd + d[i] * gd[i];
+        }
+        double scale = delta / sqrt(dd);
+        if (sp * dhd < 0.0) scale = -scale;
+        double temp = 0.0;
+        if (sp * sp > 0.99 * dd * gg) temp = 1.0;
+        double tau = scale * (fabs(sp) + 0.5 * scale * fabs(dhd));
+        if (gg * delsq < 0.01 * tau * tau) temp = 1.0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            d[i] = scale * d[i];
+            gd[i] = scale * gd[i];
+            s[i] = gc[i] + temp * gd[i];
+        }
+        for (int iterc = 1;; ++iterc) {
+            double ss = 0.0;
+            dd = 0.0;
+            sp = 0.0;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                dd = dd + d[i] * d[i];
+                sp = sp + d[i] * s[i];
+                ss = ss + s[i] * s[i];
+            }
+            temp = dd * ss - sp * sp;
+            if (temp <= 1.0e-8 * dd * ss) return;
+            const double denom = sqrt(temp);
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                s[i] = (dd * s[i] - sp * d[i]) / denom;
+                wv[i] = 0.0;
+            }
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) {
+                double sum = 0.0;
+#pragma unroll
+                for (int j = 0; j < N; ++j) sum = sum + xpt[k][j] * s[j];
+                sum = hcol[k] * sum;
+#pragma unroll
+                for (int i = 0; i < N; ++i) wv[i] = wv[i] + sum * xpt[k][i];
+            }
+            double cf1 = 0.0, cf2 = 0.0, cf3 = 0.0, cf4 = 0.0, cf5 = 0.0;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                cf1 = cf1 + s[i] * wv[i];
+                cf2 = cf2 + d[i] * gc[i];
+                cf3 = cf3 + s[i] * gc[i];
+                cf4 = cf4 + d[i] * gd[i];
+                cf5 = cf5 + s[i] * gd[i];
+            }
+            cf1 = 0.5 * cf1;
+            cf4 = 0.5 * cf4 - cf1;
+            const double taubeg = cf1 + cf2 + cf4;
+            double taumax = taubeg, tauold = taubeg, tempa = 0.0, tempb = 0.0;
+            tau = taubeg;
+            int isave = 0;
+            const int iu = 49;
+            const double dang = kTwoPi / (double)(iu + 1);
+            for (int i = 1; i <= iu; ++i) {
+                const double ang = (double)i * dang;
+                const double cth = cos(ang), sth = sin(ang);
+                tau = cf1 + (cf2 + cf4 * cth) * cth + (cf3 + cf5 * cth) * sth;
+                if (fabs(tau) > fabs(taumax)) {
+                    taumax = tau;
+                    isave = i;
+                    tempa = tauold;
+                } else if (i == isave + 1) {
+                    tempb = tau;
+                }
+                tauold = tau;
+            }
+            if (isave == 0) tempa = tau;
+            if (isave == iu) tempb = taubeg;
+            double stp = 0.0;
+            if (tempa != tempb) {
+                tempa = tempa - taumax;
+                tempb = tempb - taumax;
+                stp = 0.5 * (tempa - tempb) / (tempa + tempb);
+            }
+            const double ang = dang * ((double)isave + stp);
+            const double cth = cos(ang), sth = sin(ang);
+            tau = cf1 + (cf2 + cf4 * cth) * cth + (cf3 + cf5 * cth) * sth;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                d[i] = cth * d[i] + sth * s[i];
+                gd[i] = cth * gd[i] + sth * wv[i];
+                s[i] = gc[i] + gd[i];
+            }
+            if (fabs(tau) <= 1.1 * fabs(taubeg)) return;
+            if (!(iterc < N)) return;
+        }
+    }
+
+    // ------------------------------------------------------------------------- BIGDEN
+    // Alternative step maximising |denominator| of the update; sets w (Wcheck), vlag, beta.
+    GPD_HDN void bigden(int idz, int kopt, int knew, double &beta) {
+        double hw[N + NPT];                    // W(1..N+NPT) of the published routine
+        double s[N], den[9], denex[9], par[9];
+        double wvec[NDIM][5], prod[NDIM][5];
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) hw[N + k] = 0.0;
+#pragma unroll
+        for (int j = 0; j < NPTM; ++j) {
+            double temp = rd2(zmat, knew - 1, j);
+            if (j + 1 < idz) temp = -temp;
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) hw[N + k] = hw[N + k] + temp * zmat[k][j];
+        }
+        double alpha = hw[N];
+#pragma unroll
+        for (int k = 1; k < NPT; ++k) alpha = (knew - 1 == k) ? hw[N + k] : alpha;
+
+        double dd = 0.0, ds = 0.0, ss = 0.0, xoptsq = 0.0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            dd = dd + d[i] * d[i];
+            s[i] = rd2(xpt, knew - 1, i) - xopt[i];
+            ds = ds + d[i] * s[i];
+            ss = ss + s[i] * s[i];
+            xoptsq = xoptsq + xopt[i] * xopt[i];
+        }
+        if (ds * ds > 0.99 * dd * ss) {
+            int ksav = knew;
+            double dtest = ds * ds / ss;
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) {
+                if (k + 1 != kopt) {
+                    double dstemp = 0.0, sstemp = 0.0;
+#pragma unroll
+                    for (int i = 0; i < N; ++i) {
+                        const double diff = xpt[k][i] - xopt[i];
+                        dstemp = dstemp + d[i] * diff;
+                        sstemp = sstemp + diff * diff;
+                    }
+                    if (dstemp * dstemp / sstemp < dtest) {
+                        ksav = k + 1;
+                        dtest = dstemp * dstemp / sstemp;
+                        ds = dstemp;
+                        ss = sstemp;
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < N; ++i) s[i] = rd2(xpt, ksav - 1, i) - xopt[i];
+        }
+        double ssden = dd * ss - ds * ds;
+        double densav = 0.0;
+        double tau = 0.0, tempa = 0.0, tempb = 0.0, tempc, sum, denold = 0.0, denmax = 0.0;
+        for (int iterc = 1;; ++iterc) {
+            double temp = 1.0 / sqrt(ssden);
+            double xoptd = 0.0, xopts = 0.0;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                s[i] = temp * (dd * s[i] - ds * d[i]);
+                xoptd = xoptd + xopt[i] * d[i];
+                xopts = xopts + xopt[i] * s[i];
+            }
+            tempa = 0.5 * xoptd * xoptd;
+            tempb = 0.5 * xopts * xopts;
+            den[0] = dd * (xoptsq + 0.5 * dd) + tempa + tempb;
+            den[1] = 2.0 * xoptd * dd;
+            den[2] = 2.0 * xopts * dd;
+            den[3] = tempa - tempb;
+            den[4] = xoptd * xopts;
+#pragma unroll
+            for (int i = 5; i < 9; ++i) den[i] = 0.0;
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) {
+                double ta = 0.0, tb = 0.0, tc = 0.0;
+#pragma unroll
+                for (int i = 0; i < N; ++i) {
+                    ta = ta + xpt[k][i] * d[i];
+                    tb = tb + xpt[k][i] * s[i];
+                    tc = tc + xpt[k][i] * xopt[i];
+                }
+                wvec[k][0] = 0.25 * (ta * ta + tb * tb);
+                wvec[k][1] = ta * tc;
+                wvec[k][2] = tb * tc;
+                wvec[k][3] = 0.25 * (ta * ta - tb * tb);
+                wvec[k][4] = 0.5 * ta * tb;
+            }
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                wvec[NPT + i][0] = 0.0;
+                wvec[NPT + i][1] = d[i];
+                wvec[NPT + i][2] = s[i];
+                wvec[NPT + i][3] = 0.0;
+                wvec[NPT + i][4] = 0.0;
+            }
+#pragma unroll
+            for (int jc = 0; jc < 5; ++jc) {
+                const bool full = (jc == 1 || jc == 2);
+#pragma unroll
+                for (int k = 0; k < NPT; ++k) prod[k][jc] = 0.0;
+#pragma unroll
+                for (int j = 0; j < NPTM; ++j) {
+                    sum = 0.0;
+#pragma unroll
+                    for (int k = 0; k < NPT; ++k) sum = sum + zmat[k][j] * wvec[k][jc];
+                    if (j + 1 < idz) sum = -sum;
+#pragma unroll
+                    for (int k = 0; k < NPT; ++k) prod[k][jc] = prod[k][jc] + sum * zmat[k][j];
+                }
+                if (full) {
+#pragma unroll
+                    for (int k = 0; k < NPT; ++k) {
+                        sum = 0.0;
+#pragma unroll
+                        for (int j = 0; j < N; ++j) sum = sum + bmat[k][j] * wvec[NPT + j][jc];
+                        prod[k][jc] = prod[k][jc] + sum;
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < N; ++j) {
+                    sum = 0.0;
+                    const int nw = full ? NDIM : NPT;
+#pragma unroll
+                    for (int i = 0; i < NDIM; ++i)
+                        if (i < nw) sum = sum + bmat[i][j] * wvec[i][jc];
+                    prod[NPT + j][jc] = sum;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < NDIM; ++k) {
+                sum = 0.0;
+#pragma unroll
+                for (int i = 0; i < 5; ++i) {
+                    par[i] = 0.5 * prod[k][i] * wvec[k][i];
+                    sum = sum + par[i];
+                }
+                den[0] = den[0] - par[0] - sum;
+                tempa = prod[k][0] * wvec[k][1] + prod[k][1] * wvec[k][0];
+                tempb = prod[k][1] * wvec[k][3] + prod[k][3] * wvec[k][1];
+                tempc = prod[k][2] * wvec[k][4] + prod[k][4] * wvec[k][2];
+                den[1] = den[1] - tempa - 0.5 * (tempb + tempc);
+                den[5] = den[5] - 0.5 * (tempb - tempc);
+                tempa = prod[k][0] * wvec[k][2] + prod[k][2] * wvec[k][0];
+                tempb = prod[k][1] * wvec[k][4] + prod[k][4] * wvec[k][1];
+                tempc = prod[k][2] * wvec[k][3] + prod[k][3] * wvec[k][2];
+                den[2] = den[2] - tempa - 0.5 * (tempb - tempc);
+                den[6] = den[6] - 0.5 * (tempb + tempc);
+                tempa = prod[k][0] * wvec[k][3] + prod[k][3] * wvec[k][0];
+                den[3] = den[3] - tempa - par[1] + par[2];
+                tempa = prod[k][0] * wvec[k][4] + prod[k][4] * wvec[k][0];
+                tempb = prod[k][1] * wvec[k][2] + prod[k][2] * wvec[k][1];
+                den[4] = den[4] - tempa - 0.5 * tempb;
+                den[7] = den[7] - par[3] + par[4];
+                tempa = prod[k][3] * wvec[k][4] + prod[k][4] * wvec[k][3];
+                den[8] = den[8] - 0.5 * tempa;
+            }
+            double pk[5];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) pk[i] = rd2(prod, knew - 1, i);
+            sum = 0.0;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                par[i] = 0.5 * pk[i] * pk[i];
+                sum = sum + par[i];
+            }
+            denex[0] = alpha * den[0] + par[0] + sum;
+            tempa = 2.0 * pk[0] * pk[1];
+            tempb = pk[1] * pk[3];
+            tempc = pk[2] * pk[4];
+            denex[1] = alpha * den[1] + tempa + tempb + tempc;
+            denex[5] = alpha * den[5] + tempb - tempc;
+            tempa = 2.0 * pk[0] * pk[2];
+            tempb = pk[1] * pk[4];
+            tempc = pk[2] * pk[3];
+            denex[2] = alpha * den[2] + tempa + tempb - tempc;
+            denex[6] = alpha * den[6] + tempb + tempc;
+            tempa = 2.0 * pk[0] * pk[3];
+            denex[3] = alpha * den[3] + tempa + par[1] - par[2];
+            tempa = 2.0 * pk[0] * pk[4];
+            denex[4] = alpha * den[4] + tempa + pk[1] * pk[2];
+            denex[7] = alpha * den[7] + par[3] - par[4];
+            denex[8] = alpha * den[8] + pk[3] * pk[4];
+
+            sum = denex[0] + denex[1] + denex[3] + denex[5] + denex[7];
+            denold = sum;
+            denmax = sum;
+            int isave = 0;
+            const int iu = 49;
+            const double dang = kTwoPi / (double)(iu + 1);
+            par[0] = 1.0;
+            for (int i = 1; i <= iu; ++i) {
+                const double ang = (double)i * dang;
+                par[1] = cos(ang);
+                par[2] = sin(ang);
+#pragma unroll
+                for (int j = 3; j <= 7; j += 2) {
+                    par[j] = par[1] * par[j - 2] - par[2] * par[j - 1];
+                    par[j + 1] = par[1] * par[j - 1] + par[2] * par[j - 2];
+                }
+                const double sumold = sum;
+                sum = 0.0;
+#pragma unroll
+                for (int j = 0; j < 9; ++j) sum = sum + denex[j] * par[j];
+                if (fabs(sum) > fabs(denmax)) {
+                    denmax = sum;
+                    isave = i;
+                    tempa = sumold;
+                } else if (i == isave + 1) {
+                    tempb = sum;
+                }
+            }
+            if (isave == 0) tempa = sum;
+            if (isave == iu) tempb = denold;
+            double stp = 0.0;
+            if (tempa != tempb) {
+                tempa = tempa - denmax;
+                tempb = tempb - denmax;
+                stp = 0.5 * (tempa - tempb) / (tempa + tempb);
+            }
+            const double ang = dang * ((double)isave + stp);
+            par[1] = cos(ang);
+            par[2] = sin(ang);
+#pragma unroll
+            for (int j = 3; j <= 7; j += 2) {
+                par[j] = par[1] * par[j - 2] - par[2] * par[j - 1];
+                par[j + 1] = par[1] * par[j - 1] + par[2] * par[j - 2];
+            }
+            beta = 0.0;
+            denmax = 0.0;
+#pragma unroll
+            for (int j = 0; j < 9; ++j) {
+                beta = beta + den[j] * par[j];
+                denmax = denmax + denex[j] * par[j];
+            }
+#pragma unroll
+            for (int k = 0; k < NDIM; ++k) {
+                vlag[k] = 0.0;
+#pragma unroll
+                for (int j = 0; j < 5; ++j) vlag[k] = vlag[k] + prod[k][j] * par[j];
+            }
+            tau = rd(vlag, knew - 1);
+            dd = 0.0;
+            tempa = 0.0;
+            tempb = 0.0;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                d[i] = par[1] * d[i] + par[2] * s[i];
+                hw[i] = xopt[i] + d[i];
+                dd = dd + d[i] * d[i];
+                tempa = tempa + d[i] * hw[i];
+                tempb = tempb + hw[i] * hw[i];
+            }
+            if (iterc >= N) break;
+            if (iterc > 1) densav = fmax(densav, denold);
+            if (fabs(denmax) <= 1.1 * fabs(densav)) break;
+            densav = denmax;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                temp = tempa * xopt[i] + tempb * d[i] - vlag[NPT + i];
+                s[i] = tau * rd2(bmat, knew - 1, i) + alpha * temp;
+            }
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) {
+                sum = 0.0;
+#pragma unroll
+                for (int j = 0; j < N; ++j) sum = sum + xpt[k][j] * hw[j];
+                temp = (tau * hw[N + k] - alpha * vlag[k]) * sum;
+#pragma unroll
+                for (int i = 0; i < N; ++i) s[i] = s[i] + temp * xpt[k][i];
+            }
+            ss = 0.0;
+            ds = 0.0;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                ss = ss + s[i] * s[i];
+                ds = ds + d[i] * s[i];
+            }
+            ssden = dd * ss - ds * ds;
+            if (!(ssden >= 1.0e-8 * dd * ss)) break;
+        }
+#pragma unroll
+        for (int k = 0; k < NDIM; ++k) {
+            w[k] = 0.0;
+#pragma unroll
+            for (int j = 0; j < 5; ++j) w[k] = w[k] + wvec[k][j] * par[j];
+        }
+        wr(vlag, kopt - 1, rd(vlag, kopt - 1) + 1.0);
+    }
+
+    // ------------------------------------------------------------------------- UPDATE
+    // Shift interpolation point knew: update BMAT, ZMAT, IDZ (vlag, beta from the step).
+    GPD_HDN void update(int &idz, double beta, int knew) {
+        double wk[NDIM];
+        int jl = 1;  // 1-based column index into zmat
+#pragma unroll
+        for (int j = 2; j <= NPTM; ++j) {
+            if (j == idz) {
+                jl = idz;
+            } else if (rd2(zmat, knew - 1, j - 1) != 0.0) {
+                const double zl = rdc(zmat, knew - 1, jl - 1);  // zmat[knew][jl]
+                const double zj = rd2(zmat, knew - 1, j - 1);
+                double temp = sqrt(zl * zl + zj * zj);
+                const double ta = zl / temp, tb = zj / temp;
+#pragma unroll
+                for (int i = 0; i < NPT; ++i) {
+                    const double zil = rdc(zmat, i, jl - 1);
+                    temp = ta * zil + tb * zmat[i][j - 1];
+                    zmat[i][j - 1] = ta * zmat[i][j - 1] - tb * zil;
+                    wrc(zmat, i, jl - 1, temp);
+                }
+                wr2(zmat, knew - 1, j - 1, 0.0);
+            }
+        }
+        double tempa = rd2(zmat, knew - 1, 0);
+        if (idz >= 2) tempa = -tempa;
+        double tempb = 0.0;
+        if (jl > 1) tempb = rdc(zmat, knew - 1, jl - 1);
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {
+            wk[i] = tempa * zmat[i][0];
+            if (jl > 1) wk[i] = wk[i] + tempb * rdc(zmat, i, jl - 1);
+        }
+        const double alpha = rd(wk, knew - 1);  // only wk[0..NPT) are set; knew <= NPT
+        const double tau = rd(vlag, knew - 1);
+        const double tausq = tau * tau;
+        const double denom = alpha * beta + tausq;
+        wr(vlag, knew - 1, tau - 1.0);
+        int iflag = 0;
+        if (jl == 1) {
+            const double temp = sqrt(fabs(denom));
+            tempb = tempa / temp;
+            tempa = tau / temp;
+#pragma unroll
+            for (int i = 0; i < NPT; ++i) zmat[i][0] = tempa * zmat[i][0] - tempb * vlag[i];
+            if (idz == 1 && temp < 0.0) idz = 2;
+            if (idz >= 2 && temp >= 0.0) iflag = 1;
+        } else {
+            int ja = 1;
+            if (beta >= 0.0) ja = jl;
+            const int jb = jl + 1 - ja;
+            double temp = rdc(zmat, knew - 1, jb - 1) / denom;
+            tempa = temp * beta;
+            tempb = temp * tau;
+            temp = rdc(zmat, knew - 1, ja - 1);
+            const double scala = 1.0 / sqrt(fabs(beta) * temp * temp + tausq);
+            const double scalb = scala * sqrt(fabs(denom));
+#pragma unroll
+            for (int i = 0; i < NPT; ++i) {
+                const double za = rdc(zmat, i, ja - 1), zb = rdc(zmat, i, jb - 1);
+                wrc(zmat, i, ja - 1, scala * (tau * za - temp * vlag[i]));
+                wrc(zmat, i, jb - 1, scalb * (zb - tempa * wk[i] - tempb * vlag[i]));
+            }
+            if (denom <= 0.0) {
+                if (beta < 0.0) idz = idz + 1;
+                if (beta >= 0.0) iflag = 1;
+            }
+        }
+        if (iflag == 1) {
+            idz = idz - 1;
+#pragma unroll
+            for (int i = 0; i < NPT; ++i) {
+                const double temp = zmat[i][0];
+                zmat[i][0] = rdc(zmat, i, idz - 1);
+                wrc(zmat, i, idz - 1, temp);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const int jp = NPT + j;  // 0-based row of BMAT / entry of VLAG, W
+            wk[jp] = rd2(bmat, knew - 1, j);
+            const double ta = (alpha * vlag[jp] - tau * wk[jp]) / denom;
+            const double tb = (-beta * wk[jp] - tau * vlag[jp]) / denom;
+#pragma unroll
+            for (int i = 0; i <= jp; ++i) {
+                bmat[i][j] = bmat[i][j] + ta * vlag[i] + tb * wk[i];
+                if (i >= NPT) bmat[jp][i - NPT] = bmat[i][j];
+            }
+        }
+    }
+
+    // ------------------------------------------------------------------------- NEWUOB
+    // Minimise f from x (in/out).  Returns the number of evaluations; *fx = f(x).
+    template <class F>
+    GPD_HDN int run(double (&x)[N], double rhobeg, double rhoend, int maxfun, F &fun,
+                   double &fx) {
+        const int nftest = maxfun > 1 ? maxfun : 1;
+        const int np = N + 1;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            xbase[j] = x[j];
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) xpt[k][j] = 0.0;
+#pragma unroll
+            for (int i = 0; i < NDIM; ++i) bmat[i][j] = 0.0;
+        }
+#pragma unroll
+        for (int ih = 0; ih < NH; ++ih) hq[ih] = 0.0;
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            pq[k] = 0.0;
+#pragma unroll
+            for (int j = 0; j < NPTM; ++j) zmat[k][j] = 0.0;
+        }
+        double rhosq = rhobeg * rhobeg;
+        const double recip = 1.0 / rhosq;
+        const double reciq = sqrt(0.5) / rhosq;
+        double f = 0.0, fbeg = 0.0, fopt = 0.0;
+        int kopt = 1;
+
+        // ---------------------------------------- initial interpolation set (NPT points)
+        for (int nf = 1; nf <= NPT; ++nf) {
+            const int nfm = nf - 1, nfmm = nf - 1 - N;
+            int ipt = 0, jpt = 0;
+            double xipt = 0.0, xjpt = 0.0;
+            if (nfm <= 2 * N) {
+                if (nfm >= 1 && nfm <= N) {
+                    wr2(xpt, nf - 1, nfm - 1, rhobeg);
+                } else if (nfm > N) {
+#pragma unroll
+                    for (int j = 0; j < N; ++j)
+                        if (j == nfmm - 1) wr2(xpt, nf - 1, j, -rhobeg);
+                }
+            } else {
+                int itemp = (nfmm - 1) / N;
+                jpt = nfm - itemp * N - N;
+                ipt = jpt + itemp;
+                if (ipt > N) {
+                    itemp = jpt;
+                    jpt = ipt - N;
+                    ipt = itemp;
+                }
+                xipt = rhobeg;
+                if (rd(fval, ipt + np - 1) < rd(fval, ipt)) xipt = -xipt;
+                xjpt = rhobeg;
+                if (rd(fval, jpt + np - 1) < rd(fval, jpt)) xjpt = -xjpt;
+#pragma unroll
+                for (int j = 0; j < N; ++j) {
+                    if (j == ipt - 1) wr2(xpt, nf - 1, j, xipt);
+                    if (j == jpt - 1) wr2(xpt, nf - 1, j, xjpt);
+                }
+            }
+            double xe[N];
+#pragma unroll
+            for (int j = 0; j < N; ++j) xe[j] = rd2(xpt, nf - 1, j) + xbase[j];
+#pragma unroll
+            for (int j = 0; j < N; ++j) x[j] = xe[j];
+            if (nf > nftest) {  // maxfun < NPT: stop during initialisation
+                fx = f;
+                finish(x, fopt, f);
+                fx = f;
+                return nf - 1;
+            }
+            f = fun(x);
+            wr(fval, nf - 1, f);
+            if (nf == 1) {
+                fbeg = f;
+                fopt = f;
+                kopt = 1;
+            } else if (f < fopt) {
+                fopt = f;
+                kopt = nf;
+            }
+            if (nfm <= 2 * N) {
+                if (nfm >= 1 && nfm <= N) {
+                    wr(gq, nfm - 1, (f - fbeg) / rhobeg);
+                    if (NPT < nf + N) {
+#pragma unroll
+                        for (int j = 0; j < N; ++j)
+                            if (j == nfm - 1) {
+                                bmat[0][j] = -1.0 / rhobeg;
+                                wr2(bmat, nf - 1, j, 1.0 / rhobeg);
+                                wr2(bmat, NPT + nfm - 1, j, -0.5 * rhosq);
+                            }
+                    }
+                } else if (nfm > N) {
+#pragma unroll
+                    for (int j = 0; j < N; ++j) {
+                        if (j == nfmm - 1) {
+                            wr2(bmat, nf - N - 1, j, 0.5 / rhobeg);
+                            wr2(bmat, nf - 1, j, -0.5 / rhobeg);
+                        }
+                    }
+#pragma unroll
+                    for (int j = 0; j < NPTM; ++j) {
+                        if (j == nfmm - 1) {
+                            zmat[0][j] = -reciq - reciq;
+                            wr2(zmat, nf - N - 1, j, reciq);
+                            wr2(zmat, nf - 1, j, reciq);
+                        }
+                    }
+                    const int ih = (nfmm * (nfmm + 1)) / 2;
+                    const double temp = (fbeg - f) / rhobeg;
+                    const double g = rd(gq, nfmm - 1);
+                    wr(hq, ih - 1, (g - temp) / rhobeg);
+                    wr(gq, nfmm - 1, 0.5 * (g + temp));
+                }
+            } else {
+                const int ih = (ipt * (ipt - 1)) / 2 + jpt;
+                if (xipt < 0.0) ipt = ipt + N;
+                if (xjpt < 0.0) jpt = jpt + N;
+#pragma unroll
+                for (int j = 0; j < NPTM; ++j) {
+                    if (j == nfmm - 1) {
+                        zmat[0][j] = recip;
+                        wr2(zmat, nf - 1, j, recip);
+                        wr2(zmat, ipt, j, -recip);
+                        wr2(zmat, jpt, j, -recip);
+                    }
+                }
+                wr(hq, ih - 1, (fbeg - rd(fval, ipt) - rd(fval, jpt) + f) / (xipt * xjpt));
+            }
+        }
+        int nf = NPT;
+
+        // ---------------------------------------- iterations
+        double rho = rhobeg, delta = rho;
+        int idz = 1;
+        double diffa = 0.0, diffb = 0.0, diffc = 0.0, ratio = 0.0, crvmin = 0.0;
+        double dnorm = 0.0, dsq = 0.0, dstep = 0.0, alpha = 0.0, beta = 0.0, vquad = 0.0;
+        double diff = 0.0;
+        int itest = 0, knew = 0, nfsav;
+        double xoptsq = 0.0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            xopt[i] = rd2(xpt, kopt - 1, i);
+            xoptsq = xoptsq + xopt[i] * xopt[i];
+        }
+    L90:
+        nfsav = nf;
+    L100:
+        knew = 0;
+        trsapp(delta, d, crvmin);
+        dsq = 0.0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) dsq = dsq + d[i] * d[i];
+        dnorm = fmin(delta, sqrt(dsq));
+        if (dnorm < 0.5 * rho) {
+            knew = -1;
+            delta = 0.1 * delta;
+            ratio = -1.0;
+            if (delta <= 1.5 * rho) delta = rho;
+            if (nf <= nfsav + 2) goto L460;
+            const double temp = 0.125 * crvmin * rho * rho;
+            if (temp <= fmax(fmax(diffa, diffb), diffc)) goto L460;
+            goto L490;
+        }
+    L120:
+        if (dsq <= 1.0e-3 * xoptsq) shift_base(xoptsq, idz);
+        if (knew > 0) biglag(idz, knew, dstep, alpha);
+        // VLAG and BETA for the current D; W(1..NPT) = Wcheck
+        {
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) {
+                double suma = 0.0, sumb = 0.0, sum = 0.0;
+#pragma unroll
+                for (int j = 0; j < N; ++j) {
+                    suma = suma + xpt[k][j] * d[j];
+                    sumb = sumb + xpt[k][j] * xopt[j];
+                    sum = sum + bmat[k][j] * d[j];
+                }
+                w[k] = suma * (0.5 * suma + sumb);
+                vlag[k] = sum;
+            }
+            beta = 0.0;
+#pragma unroll
+            for (int k = 0; k < NPTM; ++k) {
+                double sum = 0.0;
+#pragma unroll
+                for (int i = 0; i < NPT; ++i) sum = sum + zmat[i][k] * w[i];
+                if (k + 1 < idz) {
+                    beta = beta + sum * sum;
+                    sum = -sum;
+                } else {
+                    beta = beta - sum * sum;
+                }
+#pragma unroll
+                for (int i = 0; i < NPT; ++i) vlag[i] = vlag[i] + sum * zmat[i][k];
+            }
+            double bsum = 0.0, dx = 0.0;
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                double sum = 0.0;
+#pragma unroll
+                for (int i = 0; i < NPT; ++i) sum = sum + w[i] * bmat[i][j];
+                bsum = bsum + sum * d[j];
+                const int jp = NPT + j;
+#pragma unroll
+                for (int k = 0; k < N; ++k) sum = sum + bmat[jp][k] * d[k];
+                vlag[jp] = sum;
+                bsum = bsum + sum * d[j];
+                dx = dx + d[j] * xopt[j];
+            }
+            beta = dx * dx + dsq * (xoptsq + dx + dx + 0.5 * dsq) + beta - bsum;
+            wr(vlag, kopt - 1, rd(vlag, kopt - 1) + 1.0);
+        }
+        if (knew > 0) {
+            const double vk = rd(vlag, knew - 1);
+            const double temp = 1.0 + alpha * beta / (vk * vk);
+            if (fabs(temp) <= 0.8) bigden(idz, kopt, knew, beta);
+        }
+    L290:
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            xnew[i] = xopt[i] + d[i];
+            x[i] = xbase[i] + xnew[i];
+        }
+        nf = nf + 1;
+        if (nf > nftest) {
+            nf = nf - 1;
+            goto L530;
+        }
+        f = fun(x);
+        if (knew == -1) goto L530;
+        {
+            vquad = 0.0;
+            int ih = 0;
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                vquad = vquad + d[j] * gq[j];
+#pragma unroll
+                for (int i = 0; i <= j; ++i) {
+                    double temp = d[i] * xnew[j] + d[j] * xopt[i];
+                    if (i == j) temp = 0.5 * temp;
+                    vquad = vquad + temp * hq[ih];
+                    ++ih;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) vquad = vquad + pq[k] * w[k];
+        }
+        diff = f - fopt - vquad;
+        diffc = diffb;
+        diffb = diffa;
+        diffa = fabs(diff);
+        if (dnorm > rho) nfsav = nf;
+        {
+            const double fsave = fopt;
+            if (f < fopt) {
+                fopt = f;
+                xoptsq = 0.0;
+#pragma unroll
+                for (int i = 0; i < N; ++i) {
+                    xopt[i] = xnew[i];
+                    xoptsq = xoptsq + xopt[i] * xopt[i];
+                }
+            }
+            const int ksave = knew;
+            if (knew <= 0) {
+                if (vquad >= 0.0) goto L530;  // trust-region step failed to reduce Q
+                ratio = (f - fsave) / vquad;
+                if (ratio <= 0.1) {
+                    delta = 0.5 * dnorm;
+                } else if (ratio <= 0.7) {
+                    delta = fmax(0.5 * delta, dnorm);
+                } else {
+                    delta = fmax(0.5 * delta, dnorm + dnorm);
+                }
+                if (delta <= 1.5 * rho) delta = rho;
+                // point to drop
+                double rs = fmax(0.1 * delta, rho);
+                rs = rs * rs;
+                int ktemp = 0;
+                double detrat = 0.0;
+                if (f >= fsave) {
+                    ktemp = kopt;
+                    detrat = 1.0;
+                }
+#pragma unroll
+                for (int k = 0; k < NPT; ++k) {
+                    double hdiag = 0.0;
+#pragma unroll
+                    for (int j = 0; j < NPTM; ++j) {
+                        double temp = 1.0;
+                        if (j + 1 < idz) temp = -1.0;
+                        hdiag = hdiag + temp * zmat[k][j] * zmat[k][j];
+                    }
+                    double temp = fabs(beta * hdiag + vlag[k] * vlag[k]);
+                    double distsq = 0.0;
+#pragma unroll
+                    for (int j = 0; j < N; ++j)
+                        distsq = distsq + (xpt[k][j] - xopt[j]) * (xpt[k][j] - xopt[j]);
+                    if (distsq > rs) {
+                        const double r = distsq / rs;
+                        temp = temp * (r * r * r);
+                    }
+                    if (temp > detrat && k + 1 != ktemp) {
+                        detrat = temp;
+                        knew = k + 1;
+                    }
+                }
+                if (knew == 0) goto L460;
+            }
+            // L410: move point knew to xnew and update the model
+            update(idz, beta, knew);
+            wr(fval, knew - 1, f);
+            {
+                const double pqk = rd(pq, knew - 1);
+                int ih = 0;
+#pragma unroll
+                for (int i = 0; i < N; ++i) {
+                    const double temp = pqk * rd2(xpt, knew - 1, i);
+#pragma unroll
+                    for (int j = 0; j <= i; ++j) {
+                        hq[ih] = hq[ih] + temp * rd2(xpt, knew - 1, j);
+                        ++ih;
+                    }
+                }
+                wr(pq, knew - 1, 0.0);
+#pragma unroll
+                for (int j = 0; j < NPTM; ++j) {
+                    double temp = diff * rd2(zmat, knew - 1, j);
+                    if (j + 1 < idz) temp = -temp;
+#pragma unroll
+                    for (int k = 0; k < NPT; ++k) pq[k] = pq[k] + temp * zmat[k][j];
+                }
+                double gqsq = 0.0;
+#pragma unroll
+                for (int i = 0; i < N; ++i) {
+                    gq[i] = gq[i] + diff * rd2(bmat, knew - 1, i);
+                    gqsq = gqsq + gq[i] * gq[i];
+                    wr2(xpt, knew - 1, i, xnew[i]);
+                }
+                if (ksave == 0 && delta == rho) {
+                    if (fabs(ratio) > 1.0e-2) {
+                        itest = 0;
+                    } else {
+                        const double fk = rd(fval, kopt - 1);
+#pragma unroll
+                        for (int k = 0; k < NPT; ++k) vlag[k] = fval[k] - fk;
+                        double gisq = 0.0;
+#pragma unroll
+                        for (int i = 0; i < N; ++i) {
+                            double sum = 0.0;
+#pragma unroll
+                            for (int k = 0; k < NPT; ++k) sum = sum + bmat[k][i] * vlag[k];
+                            gisq = gisq + sum * sum;
+                            w[i] = sum;
+                        }
+                        itest = itest + 1;
+                        if (gqsq < 1.0e2 * gisq) itest = 0;
+                        if (itest >= 3) {
+#pragma unroll
+                            for (int i = 0; i < N; ++i) gq[i] = w[i];
+#pragma unroll
+                            for (int ih2 = 0; ih2 < NH; ++ih2) hq[ih2] = 0.0;
+                            double wz[NPTM];
+#pragma unroll
+                            for (int j = 0; j < NPTM; ++j) {
+                                wz[j] = 0.0;
+#pragma unroll
+                                for (int k = 0; k < NPT; ++k) wz[j] = wz[j] + vlag[k] * zmat[k][j];
+                                if (j + 1 < idz) wz[j] = -wz[j];
+                            }
+#pragma unroll
+                            for (int j = 0; j < NPTM; ++j) w[j] = wz[j];
+#pragma unroll
+                            for (int k = 0; k < NPT; ++k) {
+                                pq[k] = 0.0;
+#pragma unroll
+                                for (int j = 0; j < NPTM; ++j) pq[k] = pq[k] + zmat[k][j] * w[j];
+                            }
+                            itest = 0;
+                        }
+                    }
+                }
+            }
+            if (f < fsave) kopt = knew;
+            if (f <= fsave + 0.1 * vquad) goto L100;
+            if (ksave > 0) goto L100;
+        }
+        knew = 0;
+    L460 : {
+        double distsq = 4.0 * delta * delta;
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            double sum = 0.0;
+#pragma unroll
+            for (int j = 0; j < N; ++j) sum = sum + (xpt[k][j] - xopt[j]) * (xpt[k][j] - xopt[j]);
+            if (sum > distsq) {
+                knew = k + 1;
+                distsq = sum;
+            }
+        }
+        if (knew > 0) {
+            dstep = fmax(fmin(0.1 * sqrt(distsq), 0.5 * delta), rho);
+            dsq = dstep * dstep;
+            goto L120;
+        }
+    }
+        if (ratio > 0.0) goto L100;
+        if (fmax(delta, dnorm) > rho) goto L100;
+    L490:
+        if (rho > rhoend) {
+            delta = 0.5 * rho;
+            ratio = rho / rhoend;
+            if (ratio <= 16.0) {
+                rho = rhoend;
+            } else if (ratio <= 250.0) {
+                rho = sqrt(ratio) * rhoend;
+            } else {
+                rho = 0.1 * rho;
+            }
+            delta = fmax(delta, rho);
+            goto L90;
+        }
+        if (knew == -1) goto L290;
+    L530:
+        finish(x, fopt, f);
+        fx = f;
+        return nf;
+    }
+
+    GPD_HD void finish(double (&x)[N], double fopt, double &f) const {
+        if (fopt <= f) {
+#pragma unroll
+            for (int i = 0; i < N; ++i) x[i] = xbase[i] + xopt[i];
+            f = fopt;
+        }
+    }
+
+    // Move XBASE to XBASE+XOPT (NEWUOB label 120 block).
+    GPD_HDN void shift_base(double &xoptsq, int idz) {
+        const double tempq = 0.25 * xoptsq;
+        double wt[NPT], v[N], wi[N];
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            double sum = 0.0;
+#pragma unroll
+            for (int i = 0; i < N; ++i) sum = sum + xpt[k][i] * xopt[i];
+            const double temp = pq[k] * sum;
+            sum = sum - 0.5 * xoptsq;
+            wt[k] = sum;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                gq[i] = gq[i] + temp * xpt[k][i];
+                xpt[k][i] = xpt[k][i] - 0.5 * xopt[i];
+                v[i] = bmat[k][i];
+                wi[i] = sum * xpt[k][i] + tempq * xopt[i];
+                const int ip = NPT + i;
+#pragma unroll
+                for (int j = 0; j <= i; ++j) bmat[ip][j] = bmat[ip][j] + v[i] * wi[j] + wi[i] * v[j];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NPTM; ++k) {
+            double sumz = 0.0, wz[NPT];
+#pragma unroll
+            for (int i = 0; i < NPT; ++i) {
+                sumz = sumz + zmat[i][k];
+                wz[i] = wt[i] * zmat[i][k];
+            }
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                double sum = tempq * sumz * xopt[j];
+#pragma unroll
+                for (int i = 0; i < NPT; ++i) sum = sum + wz[i] * xpt[i][j];
+                v[j] = sum;
+                if (k + 1 < idz) sum = -sum;
+#pragma unroll
+                for (int i = 0; i < NPT; ++i) bmat[i][j] = bmat[i][j] + sum * zmat[i][k];
+            }
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                const int ip = i + NPT;
+                double temp = v[i];
+                if (k + 1 < idz) temp = -temp;
+#pragma unroll
+                for (int j = 0; j <= i; ++j) bmat[ip][j] = bmat[ip][j] + temp * v[j];
+            }
+        }
+        int ih = 0;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            wi[j] = 0.0;
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) {
+                wi[j] = wi[j] + pq[k] * xpt[k][j];
+                xpt[k][j] = xpt[k][j] - 0.5 * xopt[j];
+            }
+#pragma unroll
+            for (int i = 0; i <= j; ++i) {
+                if (i < j) gq[j] = gq[j] + hq[ih] * xopt[i];
+                gq[i] = gq[i] + hq[ih] * xopt[j];
+                hq[ih] = hq[ih] + wi[i] * xopt[j] + xopt[i] * wi[j];
+                bmat[NPT + i][j] = bmat[NPT + j][i];
+                ++ih;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            xbase[j] = xbase[j] + xopt[j];
+            xopt[j] = 0.0;
+        }
+        xoptsq = 0.0;
+    }
+};
+
+}  // namespace gpd

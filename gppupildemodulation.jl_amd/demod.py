@@ -1,0 +1,245 @@
+"""Host-side mirror of the reference API for the demodulation hot path.
+
+Mirrors FerreolS/GPPupilDemodulation.jl @ 2024-10-16:
+  * enums Side {FT=0, SC=16}, Diode {D1..D4, FC}, MetState, idx()   (src/Modulation.jl:9-22, src/Faint.jl:1)
+  * ModulationWithOffsets / ModulationNoOffsets records              (src/Modulation.jl:24-55)
+  * FaintStates + buildstates                                        (src/Faint.jl:3-73)
+  * demodulateall(timestamp, data; init, recenter, faintparam, onlyhigh, fitoffsets,
+                  preswitchdelay, postwitchdelay) -> (output, param, likelihood)
+                                                                     (src/Modulation.jl:344-435)
+The diode loop runs on the GPU through ONE gpd_fit_batch call (include/gpdemod.h); there is no
+CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import (GPD_FIT_OFFSETS, GPD_METHOD_EXACT, GPD_METHOD_HARMONIC, GPD_ONLY_HIGH,
+                   GPD_RECENTER, PARAM_DTYPE, check, load, ptr)
+
+M_2PI = 6.283185  # src/Modulation.jl:11 (not 2π)
+
+
+class Side(enum.IntEnum):  # src/Modulation.jl:9
+    FT = 0
+    SC = 16
+
+
+class Diode(enum.IntEnum):  # src/Modulation.jl:10
+    D1 = 1
+    D2 = 2
+    D3 = 3
+    D4 = 4
+    FC = 5
+
+
+class MetState(enum.IntEnum):  # src/Faint.jl:1
+    OFF = 0
+    LOW = 1
+    NORMAL = 2
+    HIGH = 3
+    TRANSIENT = -1
+
+
+def idx(side: Side, telescope: int, diode: Diode) -> int:
+    """1-based column of (side, telescope, diode) in the N×40 matrix (src/Modulation.jl:17-22)."""
+    if diode == Diode.FC:
+        return 32 + int(side) // 4 + (telescope - 1) + 1
+    return int(side) + (int(diode) - 1) + (telescope - 1) * 4 + 1
+
+
+def fc_column_of(col: int) -> int:
+    """1-based FC column used by the 1-based diode column `col` ∈ 1..32 (src/Modulation.jl:388)."""
+    side = Side.FT if col <= 16 else Side.SC
+    tel = ((col - 1) % 16) // 4 + 1
+    return idx(side, tel, Diode.FC)
+
+
+@dataclass
+class ModulationNoOffsets:  # src/Modulation.jl:34-39
+    a: complex
+    b: float
+    ϕ: float
+    ω: float = M_2PI
+
+
+@dataclass
+class ModulationWithOffsets:  # src/Modulation.jl:26-32
+    c: complex
+    a: complex
+    b: float
+    ϕ: float
+    ω: float = M_2PI
+
+
+@dataclass
+class FaintStates:  # src/Faint.jl:3-19
+    timer1: np.ndarray
+    timer2: np.ndarray
+    voltage1: float
+    voltage2: float
+    state1: MetState = MetState.HIGH
+    state2: MetState = MetState.LOW
+
+    @classmethod
+    def make(cls, timer1, timer2, voltage1, voltage2):
+        """Outer constructor: the higher-voltage timer is the LOW one (src/Faint.jl:12-19)."""
+        t1 = np.asarray(timer1, dtype=np.float64)
+        t2 = np.asarray(timer2, dtype=np.float64)
+        if voltage1 > voltage2:
+            return cls(t2, t1, voltage2, voltage1, MetState.HIGH, MetState.LOW)
+        return cls(t1, t2, voltage1, voltage2, MetState.HIGH, MetState.LOW)
+
+
+def buildstates(faintstates: FaintStates, timestamp, lag: int = 0, preswitchdelay=0.0,
+                postwitchdelay=0.0) -> np.ndarray:
+    """src/Faint.jl:21-73 → int8 MetState codes (host C++ in libgpdemod)."""
+    t = np.ascontiguousarray(timestamp, dtype=np.float64)
+    if t.size < 2:
+        raise ValueError("buildstates needs at least 2 timestamps")
+    step = t[1] - t[0]
+    t1 = np.ascontiguousarray(faintstates.timer1 + lag * step, dtype=np.float64)
+    t2 = np.ascontiguousarray(faintstates.timer2 + lag * step, dtype=np.float64)
+    if t1.size < 1 or t2.size < 1:
+        raise ValueError("popfirst! on an empty timer list")  # src/Faint.jl:33-34
+    out = np.empty(t.size, dtype=np.int8)
+    rc = load().gpd_buildstates(t.size, ptr(t), t1.size, ptr(t1), t2.size, ptr(t2),
+                                float(preswitchdelay), float(postwitchdelay), ptr(out))
+    check(rc)
+    return out
+
+
+def _method_flags(method: str) -> int:
+    if method == "auto":
+        return 0
+    if method == "exact":
+        return GPD_METHOD_EXACT
+    if method == "harmonic":
+        return GPD_METHOD_HARMONIC
+    raise ValueError(f"method must be auto|exact|harmonic, got {method!r}")
+
+
+def fit_batch(t, d, fc, fc_of_pixel, *, state=None, omega=M_2PI, xinit=None, recenter=True,
+              fitoffsets=False, onlyhigh=False, maxfun=60, want_output=False, method="auto",
+              n_gpus=1):
+    """Batch fit of P series on the GPU.
+
+    t: (N,) float64; d: (P, N) complex128 (row k = series k); fc: (G, N) complex128 raw FC
+    columns; fc_of_pixel: (P,) int (0-based row of fc).  Returns a PARAM_DTYPE record array
+    (and the (P, N) demodulated series when want_output).
+    """
+    L = load()
+    t = np.ascontiguousarray(t, dtype=np.float64)
+    d = np.ascontiguousarray(d, dtype=np.complex128)
+    fc = np.ascontiguousarray(fc, dtype=np.complex128)
+    fop = np.ascontiguousarray(fc_of_pixel, dtype=np.int32)
+    if d.ndim != 2 or fc.ndim != 2 or d.shape[1] != t.size or fc.shape[1] != t.size:
+        raise ValueError("voltage and time must have the same number of lines")  # src/Modulation.jl:258
+    P, N = d.shape
+    if fop.shape != (P,):
+        raise ValueError("fc_of_pixel must have one entry per series")
+    st = None
+    if state is not None:
+        st = np.ascontiguousarray(state, dtype=np.int8)
+        if st.shape != (N,):
+            raise ValueError("state and time must have the same number of lines")
+    xi = None
+    if xinit is not None:
+        xi = np.ascontiguousarray(xinit, dtype=np.float64)
+        if xi.shape != (2,):
+            raise ValueError("init must be a 2-vector [b, ϕ]")
+    flags = _method_flags(method)
+    if recenter:
+        flags |= GPD_RECENTER
+    if fitoffsets:
+        flags |= GPD_FIT_OFFSETS
+    if onlyhigh:
+        flags |= GPD_ONLY_HIGH
+    params = np.zeros(P, dtype=PARAM_DTYPE)
+    out = np.zeros((P, N), dtype=np.complex128) if want_output else None
+    err = ctypes.create_string_buffer(512)
+    rc = L.gpd_fit_batch(N, P, ptr(t), ptr(d), N, ptr(fc), fc.shape[0], N, ptr(fop), ptr(st),
+                         float(omega), ptr(xi), flags, int(maxfun), ptr(params), ptr(out), N,
+                         int(n_gpus), err, len(err))
+    check(rc, err)
+    return (params, out) if want_output else params
+
+
+def chi2_batch(t, d, fc, fc_of_pixel, bphi, *, state=None, omega=M_2PI, fitoffsets=False,
+               onlyhigh=False, method="auto", n_gpus=1):
+    """χ²(b_k, ϕ_k) per series — the Chi2CostFunction functor lkl(b, ϕ) (src/Modulation.jl:318-330)
+    evaluated on the GPU for a batch.  bphi: (P, 2).  Returns a PARAM_DTYPE record array with chi2
+    and the closed-form a (and c) at each point."""
+    L = load()
+    t = np.ascontiguousarray(t, dtype=np.float64)
+    d = np.ascontiguousarray(d, dtype=np.complex128)
+    fc = np.ascontiguousarray(fc, dtype=np.complex128)
+    fop = np.ascontiguousarray(fc_of_pixel, dtype=np.int32)
+    P, N = d.shape
+    bp = np.ascontiguousarray(bphi, dtype=np.float64).reshape(P, 2)
+    st = None if state is None else np.ascontiguousarray(state, dtype=np.int8)
+    flags = _method_flags(method)
+    if fitoffsets:
+        flags |= GPD_FIT_OFFSETS
+    if onlyhigh:
+        flags |= GPD_ONLY_HIGH
+    params = np.zeros(P, dtype=PARAM_DTYPE)
+    err = ctypes.create_string_buffer(512)
+    rc = L.gpd_chi2_batch(N, P, ptr(t), ptr(d), N, ptr(fc), fc.shape[0], N, ptr(fop), ptr(st),
+                          float(omega), ptr(bp), flags, ptr(params), int(n_gpus), err, len(err))
+    check(rc, err)
+    return params
+
+
+def demodulateall(timestamp, data, *, init="auto", recenter=True, faintparam=None,
+                  onlyhigh=False, fitoffsets=False, preswitchdelay=0.01, postwitchdelay=0.3,
+                  method="auto", n_gpus=1):
+    """GPU drop-in for demodulateall (src/Modulation.jl:344-435).
+
+    timestamp: (N,) float; data: (N, 40) complex (columns in idx() order, 1..32 diodes,
+    33..40 FC).  Returns (output (N, 40) complex, param: list of 32 Modulation records,
+    likelihood: (32,) float).
+    """
+    t = np.asarray(timestamp, dtype=np.float64)
+    data = np.asarray(data)
+    if not np.iscomplexobj(data):
+        raise TypeError("data must be a complex matrix (AbstractMatrix{Complex{T}})")
+    data = data.astype(np.complex128, copy=False)
+    if data.ndim != 2 or data.shape[1] != 40:
+        raise ValueError("data must be N×40 (32 diodes + 8 FC columns)")
+    N = data.shape[0]
+    if t.shape != (N,):
+        raise ValueError("voltage and time must have the same number of lines")
+    cols = np.ascontiguousarray(data.T)  # (40, N): column k contiguous, like Julia's Matrix
+    state = None
+    if faintparam is not None:
+        if isinstance(faintparam, FaintStates):
+            state = buildstates(faintparam, t, preswitchdelay=preswitchdelay,
+                                postwitchdelay=postwitchdelay)  # src/Modulation.jl:366-367
+        else:
+            state = np.asarray(faintparam, dtype=np.int8)
+            if state.shape != (N,):
+                raise ValueError("faintparam must have one MetState per sample")
+    xinit = None
+    if not (isinstance(init, str) and init == "auto"):
+        xinit = np.asarray(init, dtype=np.float64)
+    fop = np.array([fc_column_of(c) - 1 for c in range(1, 33)], dtype=np.int32)
+    params, out = fit_batch(t, cols[:32], cols, fop, state=state, xinit=xinit, recenter=recenter,
+                            fitoffsets=fitoffsets, onlyhigh=onlyhigh, want_output=True,
+                            method=method, n_gpus=n_gpus)
+    output = data.copy()  # output = copy(data): FC columns pass through (src/Modulation.jl:353)
+    output[:, :32] = out.T
+    param = []
+    for p in params:
+        if fitoffsets:
+            param.append(ModulationWithOffsets(complex(p["c"]), complex(p["a"]), float(p["b"]),
+                                               float(p["phi"])))
+        else:
+            param.append(ModulationNoOffsets(complex(p["a"]), float(p["b"]), float(p["phi"])))
+    likelihood = params["chi2"].copy()
+    return output, param, likelihood

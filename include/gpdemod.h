@@ -1,0 +1,171 @@
+/*
+ * gpdemod — MI355X (gfx950) per-pixel complex demodulation engine, C ABI.
+ *
+ * Drop-in boundary for FerreolS/GPPupilDemodulation.jl @ 2024-10-16:
+ *   demodulateall(timestamp, data; init, recenter, faintparam, onlyhigh, fitoffsets,
+ *                 preswitchdelay, postwitchdelay) -> (output, param, likelihood)
+ *   (src/Modulation.jl:344-435).  The Julia side keeps that signature and replaces the
+ *   `Threads.@threads` diode loop (src/Modulation.jl:387-433) by ONE call of
+ *   gpd_fit_batch covering all 32 diodes (or all windows); see INTEGRATION.md for the
+ *   `ccall` stub.  The calling convention mirrors the reference's only native call,
+ *   `ccall((:ffcrimll, libcfitsio), Cint, …)` + `fits_assert_ok` (src/FitsUtils.jl:40-59):
+ *   integer status return, 0 = ok, message in a caller-owned buffer.
+ *
+ * Plain C types only (no torch / HIP types in signatures).  All entry points are reentrant;
+ * per-device contexts (streams, workspaces) are created lazily under a mutex.
+ */
+#ifndef GPDEMOD_H
+#define GPDEMOD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPD_ABI_VERSION 1
+
+/* Julia ComplexF64 / Complex{Float64}: interleaved (re, im), 16 bytes. */
+typedef struct {
+    double re, im;
+} gpd_c64;
+
+/* One fitted series = the reference's Modulation record (src/Modulation.jl:24-39:
+ * ModulationWithOffsets{c,a,b,ϕ,ω} / ModulationNoOffsets{a,b,ϕ,ω}) plus the likelihood
+ * (src/Modulation.jl:359,416) and bookkeeping.  64 bytes.  c == 0 without GPD_FIT_OFFSETS.
+ * b, phi are sign-normalised (b >= 0) exactly as src/Modulation.jl:427-430. */
+typedef struct {
+    gpd_c64 c;
+    gpd_c64 a;
+    double b;
+    double phi;
+    double chi2;    /* likelihood = χ²(b,ϕ) = Σ w|r|² / N_valid (src/Modulation.jl:320,416) */
+    int32_t nfev;   /* χ² evaluations spent on this series (grid + NEWUOA + checks)          */
+    int32_t status; /* GPD_ST_* bits                                                         */
+} gpd_param;
+
+/* flags — demodulateall keywords (src/Modulation.jl:345-351) */
+#define GPD_FIT_OFFSETS 0x1u      /* fitoffsets=true → ModulationWithOffsets               */
+#define GPD_RECENTER 0x2u         /* recenter=true (default in the reference)              */
+#define GPD_ONLY_HIGH 0x4u        /* onlyhigh=true (faint mode only)                        */
+#define GPD_METHOD_EXACT 0x10u    /* force the per-sample (reference-arithmetic) evaluator  */
+#define GPD_METHOD_HARMONIC 0x20u /* force the one-pass harmonic-moment evaluator           */
+/* neither METHOD bit: automatic (harmonic when the timestamps allow it, else exact)          */
+
+/* per-series status bits (the reference ignores NEWUOA's status: check=false) */
+#define GPD_ST_REFIT 0x1    /* "bad minima" π-flip re-fit ran (src/Modulation.jl:411-414)    */
+#define GPD_ST_MAXFUN 0x2   /* a NEWUOA call stopped at maxfun                               */
+#define GPD_ST_NAN 0x4      /* final χ² is NaN (e.g. a 1-sample faint state, src/Faint.jl:97)*/
+#define GPD_ST_EXACT 0x8    /* fitted with the exact per-sample evaluator                    */
+#define GPD_ST_FALLBACK 0x10 /* harmonic evaluator left its safe |b| range → exact re-fit     */
+
+/* error codes (negative) */
+#define GPD_OK 0
+#define GPD_E_ARG -1
+#define GPD_E_HIP -2
+#define GPD_E_NODEV -3
+#define GPD_E_OOM -4
+#define GPD_E_UNSAFE -5 /* GPD_METHOD_HARMONIC requested on timestamps it cannot represent */
+
+/* MetState codes (src/Faint.jl:1) for the `state` arrays. */
+#define GPD_STATE_TRANSIENT (-1)
+#define GPD_STATE_OFF 0
+#define GPD_STATE_LOW 1
+#define GPD_STATE_NORMAL 2
+#define GPD_STATE_HIGH 3
+
+int gpd_version(void);                /* = GPD_ABI_VERSION                            */
+const char *gpd_strerror(int code);   /* static string                                */
+int gpd_device_count(void);           /* visible HIP devices (0 if none)              */
+
+/*
+ * Fit (and optionally demodulate) a batch of series.  Replaces the diode loop of
+ * demodulateall (src/Modulation.jl:387-433): per series, the FC phasor
+ * exp(im·angle(fc)) (:388), faint power/weight (:391-396, src/Faint.jl:89-100), the 8-point
+ * ϕ grid at b = 0.1 (:402-405), NEWUOA(rhobeg 1, rhoend 1e-3) (:407, :332-342), the π-flip
+ * check and re-fit (:408-414), the final χ² (:416), the output column (:417-425) and the sign
+ * normalisation (:426-431).
+ *
+ *   n_samples, t[n_samples]     timestamps (s), shared by every series (Float64)
+ *   d, ldd                      series, column-major complex, column k = series k
+ *                               (Julia Matrix{ComplexF64} column, idx() order)
+ *   fc, n_fc, ldfc              raw fibre-coupler columns (complex); the phasor is formed here
+ *   fc_of_pixel[n_pixels]       FC column index (0-based) used by series k
+ *   state[n_samples]            MetState per sample (faint mode), or NULL (non-faint: w≡1, p=phasor)
+ *   omega                       modulation pulsation (reference: M_2PI = 6.283185)
+ *   xinit                       NULL → init=:auto grid; else {b, ϕ} start for every series
+ *   flags                       GPD_* above
+ *   maxfun                      NEWUOA evaluation cap per call (<=0 → 60 = 30·n)
+ *   out_params[n_pixels]        fitted records
+ *   out_demod, ldo              NULL → fit only; else demodulated columns (all n_samples)
+ *   n_gpus                      <=0 → 1; series are sharded over that many devices
+ *   errbuf, errlen              optional message buffer
+ * Host pointers; synchronous.  Returns GPD_OK or a negative GPD_E_*.
+ */
+int gpd_fit_batch(int64_t n_samples, int64_t n_pixels, const double *t, const gpd_c64 *d,
+                  int64_t ldd, const gpd_c64 *fc, int64_t n_fc, int64_t ldfc,
+                  const int32_t *fc_of_pixel, const int8_t *state, double omega,
+                  const double *xinit, uint32_t flags, int32_t maxfun, gpd_param *out_params,
+                  gpd_c64 *out_demod, int64_t ldo, int32_t n_gpus, char *errbuf, size_t errlen);
+
+/*
+ * Same computation on device-resident buffers of device `device` (all pointers are device
+ * pointers, params included), enqueued on `stream` (hipStream_t, NULL = default stream).
+ * Asynchronous: returns once enqueued.  Workspace is owned by the library (per device,
+ * grown on demand, reused across calls); concurrent calls on one device serialise on it.
+ */
+int gpd_fit_batch_dev(int64_t n_samples, int64_t n_pixels, const double *t, const gpd_c64 *d,
+                      int64_t ldd, const gpd_c64 *fc, int64_t n_fc, int64_t ldfc,
+                      const int32_t *fc_of_pixel, const int8_t *state, double omega,
+                      const double *xinit, uint32_t flags, int32_t maxfun, gpd_param *out_params,
+                      gpd_c64 *out_demod, int64_t ldo, int device, void *stream, char *errbuf,
+                      size_t errlen);
+
+/*
+ * χ²(b_k, ϕ_k) of every series at a caller-given point, no optimisation: the Chi2CostFunction
+ * functor lkl(b, ϕ) (src/Modulation.jl:318-330) as a batch.  bphi[2k], bphi[2k+1] = (b, ϕ) of
+ * series k.  out_params[k] receives chi2 and the closed-form a (and c) at that point; b, phi echo
+ * the input.  Same data arguments and flags as gpd_fit_batch (METHOD bits select the evaluator).
+ */
+int gpd_chi2_batch(int64_t n_samples, int64_t n_pixels, const double *t, const gpd_c64 *d,
+                   int64_t ldd, const gpd_c64 *fc, int64_t n_fc, int64_t ldfc,
+                   const int32_t *fc_of_pixel, const int8_t *state, double omega,
+                   const double *bphi, uint32_t flags, gpd_param *out_params, int32_t n_gpus,
+                   char *errbuf, size_t errlen);
+
+int gpd_chi2_batch_dev(int64_t n_samples, int64_t n_pixels, const double *t, const gpd_c64 *d,
+                       int64_t ldd, const gpd_c64 *fc, int64_t n_fc, int64_t ldfc,
+                       const int32_t *fc_of_pixel, const int8_t *state, double omega,
+                       const double *bphi, uint32_t flags, gpd_param *out_params, int device,
+                       void *stream, char *errbuf, size_t errlen);
+
+/*
+ * buildstates (src/Faint.jl:21-73): two-timer faint state machine on the host.
+ * timer1 = HIGH switch times, timer2 = LOW switch times (FaintStates already orders them by
+ * voltage, src/Faint.jl:12-19), both already shifted by lag·timestep.  Writes MetState codes.
+ */
+int gpd_buildstates(int64_t n_samples, const double *t, int64_t n1, const double *timer1,
+                    int64_t n2, const double *timer2, double preswitchdelay,
+                    double postwitchdelay, int8_t *states);
+
+/*
+ * Synthetic GRAVITY-like metrology batch generated ON DEVICE (benchmarks):
+ * d[k][i] = p_i(c_k + a_k exp(j b_k sin(ω t_i + ϕ_k))) + σ CN(0,1), FC column g = 1.3 exp(jΦ_g),
+ * Φ a random walk (σ 1e-3 rad/step), 4 series per FC column, counter-based RNG keyed by
+ * (seed, global series index, sample) so that shards generate identical data.
+ * t[i] = t0 + i·dt.  truth (optional, device) receives {c, a, b, ϕ} per series as gpd_param.
+ */
+int gpd_synth_fill_dev(int64_t n_samples, int64_t n_pixels, int64_t pixel_offset, uint64_t seed,
+                       double t0, double dt, double sigma, int with_offsets, double omega,
+                       double *t, gpd_c64 *d, int64_t ldd, gpd_c64 *fc, int64_t ldfc,
+                       int32_t *fc_of_pixel, gpd_param *truth, int device, void *stream);
+
+/* Per-kernel timing of the last gpd_fit_batch_dev call on `device` (ms, HIP events on the
+ * launch stream).  names/ms arrays of length cap; returns the number of entries. */
+int gpd_last_timings(int device, const char **names, double *ms, int cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPDEMOD_H */

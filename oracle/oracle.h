@@ -1,0 +1,63 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY (see newuoa_oracle.c header).  CPU restatement of the
+ * reference demodulation path of FerreolS/GPPupilDemodulation.jl @ 2024-10-16.
+ * PARITY UNPINNED: the reference (Julia + OptimPackNextGen) cannot run in this container and
+ * ships no fixtures; this restatement follows the cited source lines as text.
+ */
+#ifndef GPD_ORACLE_H
+#define GPD_ORACLE_H
+#include <stdint.h>
+
+#define ORACLE_NEWUOA_NMAX 4
+
+typedef double (*oracle_objfun)(void *ctx, int n, const double *x);
+
+/* Powell NEWUOA (src/Modulation.jl:335 → OptimPackNextGen newuoa). Returns nfev. */
+int oracle_newuoa(int n, int npt, double *x, double rhobeg, double rhoend, int maxfun,
+                  oracle_objfun f, void *ctx, double *fx);
+
+/* Parameter record: mirrors ModulationNoOffsets/ModulationWithOffsets (src/Modulation.jl:24-39)
+ * plus the likelihood and bookkeeping.  Layout identical to the product's gpd_param. */
+typedef struct {
+    double c_re, c_im, a_re, a_im, b, phi, chi2;
+    int32_t nfev, status;
+} oracle_param;
+
+/* flags (same bit values as the product C-ABI, include/gpdemod.h) */
+#define ORACLE_FIT_OFFSETS 1u
+#define ORACLE_RECENTER 2u
+#define ORACLE_ONLY_HIGH 4u
+
+/* χ²(b,ϕ) for one series, reference arithmetic (src/Modulation.jl:122-148,174-195,299-326).
+ * w == NULL means w ≡ 1.  On return *mod holds a (and c) at (b,ϕ). */
+double oracle_chi2(int64_t n, const double *t, const double *d, const double *w,
+                   const double *p, double omega, int offsets, double b, double phi,
+                   oracle_param *mod);
+
+/* Batch fit over pixels (the per-diode body of demodulateall, src/Modulation.jl:388-432).
+ *   t[n_samples]; d column-major complex (interleaved re,im), column k = pixel k, ld = ldd
+ *   fc: raw FC columns (complex), fc_of_pixel[k] = FC column used by pixel k
+ *   state: NULL (non-faint) or MetState codes per sample (OFF=0 LOW=1 NORMAL=2 HIGH=3 TRANSIENT=-1)
+ *   xinit: NULL (:auto grid) or 2 doubles
+ *   out (optional, may be NULL): demodulated columns, column-major complex, ld = ldo
+ * Returns 0.  nthreads <= 0 → all available.  perturb_seed != 0 multiplies every χ² value by
+ * 1 ± 2^-52 (pseudo-random sign): probes how NEWUOA's tie-breaks react to 1-ulp differences. */
+int oracle_fit_batch(int64_t n_samples, int64_t n_pixels, const double *t, const double *d,
+                     int64_t ldd, const double *fc, int64_t ldfc, const int32_t *fc_of_pixel,
+                     const int8_t *state, double omega, const double *xinit, uint32_t flags,
+                     int maxfun, oracle_param *params, double *out, int64_t ldo, int nthreads,
+                     uint64_t perturb_seed);
+
+/* src/Faint.jl:21-73 buildstates (timers already lag-shifted by the caller when lag≠0). */
+int oracle_buildstates(int64_t n, const double *t, int64_t n1, const double *timer1, int64_t n2,
+                       const double *timer2, int8_t state1, int8_t state2, double preswitchdelay,
+                       double postwitchdelay, int8_t *states);
+
+/* src/Faint.jl:89-100 compute_mean_var_power on an already-masked series. */
+void oracle_mean_var_power(int64_t n, const int8_t *states, const double *d, double *m,
+                           double *w);
+
+/* src/Modulation.jl:360 ϕrange = range(-π, π, 8), as Float64 values. */
+void oracle_phi_grid(double *out8);
+
+#endif

@@ -1,0 +1,146 @@
+"""ctypes binding of the CPU oracle (oracle/liboracle.so).
+
+ORACLE — TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may import this module, and only as the checker.  The product library never
+loads it.  PARITY UNPINNED (see oracle/oracle.h).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "liboracle.so")
+
+PARAM_DTYPE = np.dtype(
+    [("c", np.complex128), ("a", np.complex128), ("b", np.float64), ("phi", np.float64),
+     ("chi2", np.float64), ("nfev", np.int32), ("status", np.int32)], align=True)
+assert PARAM_DTYPE.itemsize == 64
+
+FIT_OFFSETS, RECENTER, ONLY_HIGH = 1, 2, 4
+M_2PI = 6.283185  # src/Modulation.jl:11
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(_LIB):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_LIB)
+        P = ctypes.c_void_p
+        L.oracle_fit_batch.argtypes = [ctypes.c_int64, ctypes.c_int64, P, P, ctypes.c_int64, P,
+                                       ctypes.c_int64, P, P, ctypes.c_double, P, ctypes.c_uint32,
+                                       ctypes.c_int, P, P, ctypes.c_int64, ctypes.c_int,
+                                       ctypes.c_uint64]
+        L.oracle_fit_batch.restype = ctypes.c_int
+        L.oracle_chi2.argtypes = [ctypes.c_int64, P, P, P, P, ctypes.c_double, ctypes.c_int,
+                                  ctypes.c_double, ctypes.c_double, P]
+        L.oracle_chi2.restype = ctypes.c_double
+        L.oracle_buildstates.argtypes = [ctypes.c_int64, P, ctypes.c_int64, P, ctypes.c_int64, P,
+                                         ctypes.c_int8, ctypes.c_int8, ctypes.c_double,
+                                         ctypes.c_double, P]
+        L.oracle_buildstates.restype = ctypes.c_int
+        L.oracle_mean_var_power.argtypes = [ctypes.c_int64, P, P, P, P]
+        L.oracle_mean_var_power.restype = None
+        L.oracle_phi_grid.argtypes = [P]
+        L.oracle_phi_grid.restype = None
+        OBJ = ctypes.CFUNCTYPE(ctypes.c_double, ctypes.c_void_p, ctypes.c_int,
+                               ctypes.POINTER(ctypes.c_double))
+        L.oracle_newuoa.argtypes = [ctypes.c_int, ctypes.c_int, P, ctypes.c_double,
+                                    ctypes.c_double, ctypes.c_int, OBJ, P, P]
+        L.oracle_newuoa.restype = ctypes.c_int
+        L._OBJ = OBJ
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def newuoa(f, x0, rhobeg, rhoend, maxfun=None, npt=None):
+    """Powell NEWUOA on a Python callable (test helper). Returns (x, fx, nfev)."""
+    L = lib()
+    x = np.ascontiguousarray(x0, dtype=np.float64).copy()
+    n = x.size
+    npt = 2 * n + 1 if npt is None else npt
+    maxfun = 30 * n if maxfun is None else maxfun
+    cb = L._OBJ(lambda ctx, nn, xp: float(f(np.ctypeslib.as_array(xp, shape=(nn,)).copy())))
+    fx = np.zeros(1)
+    nf = L.oracle_newuoa(n, npt, _ptr(x), rhobeg, rhoend, maxfun, cb, None, _ptr(fx))
+    if nf < 0:
+        raise ValueError("bad NEWUOA arguments")
+    return x, float(fx[0]), nf
+
+
+def fit_batch(t, d, fc, fc_of_pixel, state=None, omega=M_2PI, xinit=None, flags=RECENTER,
+              maxfun=60, want_output=False, nthreads=0, perturb_seed=0):
+    """Oracle batch fit.  d: (n_pixels, n_samples) complex128 (row k = pixel column k),
+    fc: (n_fc, n_samples) complex128, fc_of_pixel: (n_pixels,) int32."""
+    L = lib()
+    t = np.ascontiguousarray(t, dtype=np.float64)
+    d = np.ascontiguousarray(d, dtype=np.complex128)
+    fc = np.ascontiguousarray(fc, dtype=np.complex128)
+    fop = np.ascontiguousarray(fc_of_pixel, dtype=np.int32)
+    P, N = d.shape
+    st = None if state is None else np.ascontiguousarray(state, dtype=np.int8)
+    xi = None if xinit is None else np.ascontiguousarray(xinit, dtype=np.float64)
+    params = np.zeros(P, dtype=PARAM_DTYPE)
+    out = np.zeros_like(d) if want_output else None
+    rc = L.oracle_fit_batch(N, P, _ptr(t), _ptr(d), N, _ptr(fc), N, _ptr(fop), _ptr(st),
+                            float(omega), _ptr(xi), int(flags), int(maxfun), _ptr(params),
+                            _ptr(out), N, int(nthreads), int(perturb_seed))
+    if rc != 0:
+        raise RuntimeError(f"oracle_fit_batch failed: {rc}")
+    return (params, out) if want_output else params
+
+
+def chi2(t, d, p, b, phi, w=None, omega=M_2PI, offsets=False):
+    L = lib()
+    t = np.ascontiguousarray(t, dtype=np.float64)
+    d = np.ascontiguousarray(d, dtype=np.complex128)
+    p = np.ascontiguousarray(p, dtype=np.complex128)
+    w = None if w is None else np.ascontiguousarray(w, dtype=np.float64)
+    rec = np.zeros(1, dtype=PARAM_DTYPE)
+    v = L.oracle_chi2(t.size, _ptr(t), _ptr(d), _ptr(w), _ptr(p), float(omega), int(offsets),
+                      float(b), float(phi), _ptr(rec))
+    return v, rec[0]
+
+
+def buildstates(t, timer1, timer2, state1=3, state2=1, preswitchdelay=0.0, postwitchdelay=0.0):
+    L = lib()
+    t = np.ascontiguousarray(t, dtype=np.float64)
+    t1 = np.ascontiguousarray(timer1, dtype=np.float64)
+    t2 = np.ascontiguousarray(timer2, dtype=np.float64)
+    out = np.zeros(t.size, dtype=np.int8)
+    rc = L.oracle_buildstates(t.size, _ptr(t), t1.size, _ptr(t1), t2.size, _ptr(t2), state1,
+                              state2, preswitchdelay, postwitchdelay, _ptr(out))
+    if rc != 0:
+        raise ValueError("buildstates: need ≥2 samples and ≥1 timer each")
+    return out
+
+
+def mean_var_power(states, d):
+    L = lib()
+    s = np.ascontiguousarray(states, dtype=np.int8)
+    d = np.ascontiguousarray(d, dtype=np.complex128)
+    m = np.zeros(d.size)
+    w = np.zeros(d.size)
+    L.oracle_mean_var_power(d.size, _ptr(s), _ptr(d), _ptr(m), _ptr(w))
+    return m, w
+
+
+def phi_grid():
+    out = np.zeros(8)
+    lib().oracle_phi_grid(_ptr(out))
+    return out

@@ -1,0 +1,232 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle on identical inputs.
+
+Tolerance (BASELINE.json north_star): fitted parameters within 1e-10 relative of the CPU
+reference; ϕ compared modulo 2π with absolute tolerance 1e-10·max(1,|ϕ|).  The oracle is a
+restatement (parity unpinned against the Julia reference itself).
+"""
+import numpy as np
+import pytest
+
+import synth
+from conftest import rel_err, wrap_diff
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-10
+NPERTURB = 12  # oracle runs with χ² *= 1 ± 2^-52 (tie-sensitivity envelope)
+
+
+def _dev(x, r, key):
+    if key == "phi":
+        return wrap_diff(x["phi"], r["phi"]) / np.maximum(1.0, np.abs(r["phi"]))
+    if key == "a":
+        return np.abs(x["a"] - r["a"]) / np.abs(r["a"])
+    return rel_err(x[key], r[key])
+
+
+def assert_params_close(got, ref, tol=TOL, check_c=False, label=""):
+    """Strict form: every series within tol (used where NEWUOA ties cannot occur)."""
+    rb, ra, rp, rc = (_dev(got, ref, k) for k in ("b", "a", "phi", "chi2"))
+    msg = (f"{label}: max rel b {rb.max():.2e}  a {ra.max():.2e}  phi {rp.max():.2e}  "
+           f"chi2 {rc.max():.2e}")
+    assert rb.max() <= tol and ra.max() <= tol and rp.max() <= tol and rc.max() <= tol, msg
+    if check_c:
+        dc = np.abs(got["c"] - ref["c"]) / np.maximum(np.abs(ref["c"]), np.abs(ref["a"]))
+        assert dc.max() <= tol, f"{label}: c {dc.max():.2e}"
+    return msg
+
+
+def assert_fit_parity(got, ref, perturbed, label="", min_match=0.7, tol=TOL):
+    """Parity of NEWUOA fits.  NEWUOA breaks exact ties of its symmetric interpolation set by
+    index order, so a 1-ulp change of χ² (any other libm, summation order, or the harmonic
+    evaluator's ~1e-15) re-routes ~10 % of series to another point within its rhoend
+    resolution — the reference itself is not reproducible there.
+    Each series must either match the oracle within tol, or lie within 1.5× the spread the
+    oracle itself shows under ±1-ulp χ² perturbations."""
+    keys = ("b", "phi", "a", "chi2")
+    err = np.max([_dev(got, ref, k) for k in keys], axis=0)
+    env = np.max([[_dev(p, ref, k) for k in keys] for p in perturbed], axis=(0, 1))
+    match = err <= tol
+    explained = err <= 1.5 * env + tol
+    msg = (f"{label}: {match.sum()}/{len(err)} series within {tol:g} (median {np.median(err):.1e}); "
+           f"{(~match).sum()} tie-flips, max dev {err.max():.1e}, oracle ulp-envelope max "
+           f"{env.max():.1e}; unexplained {(~explained).sum()}")
+    assert explained.all(), msg + f" — unexplained series {np.nonzero(~explained)[0]}"
+    assert match.mean() >= min_match, msg
+    assert err.max() < 1e-3, msg  # below NEWUOA's rhoend
+    return msg
+
+
+def perturbed_runs(oracle, B, n=NPERTURB, **kw):
+    return [oracle_fit(oracle, B, perturb_seed=s, **dict(kw)) for s in range(1, n + 1)]
+
+
+def oracle_fit(oracle, B, **kw):
+    kw = dict(kw)
+    flags = oracle.RECENTER if kw.pop("recenter", True) else 0
+    if kw.pop("fitoffsets", False):
+        flags |= oracle.FIT_OFFSETS
+    if kw.pop("onlyhigh", False):
+        flags |= oracle.ONLY_HIGH
+    return oracle.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], flags=flags, **kw)
+
+
+def fit(gpu, B, **kw):
+    return gpu.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], **kw)
+
+
+# ---------------------------------------------------------------- χ² evaluation parity
+@pytest.mark.parametrize("offsets", [False, True])
+def test_chi2_evaluation_parity(gpu, oracle, offsets):
+    """lkl(b, ϕ) (src/Modulation.jl:318-330) at random points: the exact evaluator reproduces
+    the oracle's χ² to ≤ 2 ulp and a to 1e-14; the harmonic evaluator to 1e-13."""
+    B = synth.make_batch(6000, 16, seed=3, offsets=offsets)
+    rng = np.random.default_rng(7)
+    bphi = np.stack([rng.uniform(-3.5, 3.5, 16), rng.uniform(-4, 4, 16)], 1)
+    ge = gpu.chi2_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], bphi, method="exact",
+                        fitoffsets=offsets)
+    gh = None if offsets else gpu.chi2_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], bphi,
+                                             method="harmonic")
+    for k in range(16):
+        p = np.exp(1j * np.angle(B["fc"][B["fc_of_pixel"][k]]))
+        v, rec = oracle.chi2(B["t"], B["d"][k], p, bphi[k, 0], bphi[k, 1], offsets=offsets)
+        assert abs(ge["chi2"][k] - v) <= 2 * np.spacing(v), (k, ge["chi2"][k], v)
+        assert abs(ge["a"][k] - rec["a"]) <= 1e-14 * abs(rec["a"]) + 1e-15
+        if offsets:
+            assert abs(ge["c"][k] - rec["c"]) <= 1e-13
+        else:
+            assert abs(gh["chi2"][k] - v) <= 1e-13 * v, (k, gh["chi2"][k], v)
+            assert abs(gh["a"][k] - rec["a"]) <= 1e-12 * abs(rec["a"])
+
+
+# ---------------------------------------------------------------- fit parity
+@pytest.mark.parametrize("method", ["exact", "harmonic"])
+def test_batch_fit_matches_oracle(gpu, oracle, method):
+    B = synth.make_batch(6000, 64, seed=1)
+    ref, refout = oracle_fit(oracle, B, want_output=True)
+    got, out = fit(gpu, B, method=method, want_output=True)
+    print(assert_fit_parity(got, ref, perturbed_runs(oracle, B), label=method))
+    same = np.max([_dev(got, ref, k) for k in ("b", "phi", "a")], axis=0) <= TOL
+    np.testing.assert_array_equal(got["nfev"][same], ref["nfev"][same])
+    np.testing.assert_array_equal((got["status"] & 0x7)[same], (ref["status"] & 0x7)[same])
+    # demodulated output (src/Modulation.jl:417-425) on series whose fit matched
+    scale = np.abs(B["d"]).max()
+    assert np.max(np.abs(out[same] - refout[same])) <= 1e-9 * scale
+
+
+def test_offsets_fit(gpu, oracle):
+    B = synth.make_batch(5000, 32, seed=9, offsets=True)
+    ref = oracle_fit(oracle, B, fitoffsets=True)
+    got = fit(gpu, B, fitoffsets=True)
+    assert np.all(got["status"] & gpu.GPD_ST_EXACT)
+    print(assert_fit_parity(got, ref, perturbed_runs(oracle, B, fitoffsets=True), label="offsets"))
+    ok = np.abs(got["b"] - ref["b"]) <= TOL * ref["b"]
+    assert np.max(np.abs(got["c"][ok] - ref["c"][ok])) <= 1e-10
+
+
+@pytest.mark.parametrize("method", ["exact", "harmonic"])
+def test_recenter_false_and_xinit(gpu, oracle, method):
+    B = synth.make_batch(4000, 16, seed=13)
+    xinit = np.array([0.7, -0.4])
+    ref, refout = oracle_fit(oracle, B, recenter=False, xinit=xinit, want_output=True)
+    got, out = fit(gpu, B, recenter=False, xinit=xinit, method=method, want_output=True)
+    print(assert_fit_parity(got, ref, perturbed_runs(oracle, B, recenter=False, xinit=xinit),
+                            label=f"xinit/{method}"))
+    same = np.abs(got["b"] - ref["b"]) <= TOL * ref["b"]
+    assert np.max(np.abs(out[same] - refout[same])) <= 1e-9 * np.abs(B["d"]).max()
+
+
+def faint_states(N, dt=0.002, seed=0):
+    """NORMAL, then alternating HIGH/LOW windows with TRANSIENT gaps (tex/figs/FaintStates)."""
+    rng = np.random.default_rng(seed)
+    st = np.full(N, 2, dtype=np.int8)
+    i = N // 10
+    while i < N - N // 10:
+        hi = int(rng.integers(N // 40, N // 20))
+        st[i:i + hi] = 3
+        st[i:i + 5] = -1
+        lo = int(rng.integers(N // 20, N // 8))
+        st[i + hi:i + hi + lo] = 1
+        st[i + hi:i + hi + 15] = -1
+        i += hi + lo
+    return st
+
+
+def faint_batch(N, P, seed):
+    B = synth.make_batch(N, P, seed=seed)
+    st = faint_states(N, seed=seed)
+    power = np.where(st == 3, 1.1, np.where(st == 1, 0.3, 0.6))  # state-dependent amplitude
+    B["d"] = B["d"] * power[None, :]
+    return B, st
+
+
+@pytest.mark.parametrize("method", ["exact", "harmonic"])
+@pytest.mark.parametrize("onlyhigh", [False, True])
+def test_faint_matches_oracle(gpu, oracle, method, onlyhigh):
+    B, st = faint_batch(6000, 32, seed=21)
+    ref = oracle_fit(oracle, B, state=st, onlyhigh=onlyhigh)
+    got = fit(gpu, B, state=st, method=method, onlyhigh=onlyhigh)
+    pert = perturbed_runs(oracle, B, state=st, onlyhigh=onlyhigh)
+    print(assert_fit_parity(got, ref, pert, label=f"faint/{method}/onlyhigh={onlyhigh}"))
+
+
+def test_faint_single_sample_state_gives_nan(gpu, oracle):
+    """var of a 1-sample state is NaN → NaN weights → NaN fit (src/Faint.jl:97)."""
+    B = synth.make_batch(2000, 4, seed=2)
+    st = np.full(2000, 2, dtype=np.int8)
+    st[100] = 0  # a single OFF sample
+    ref = oracle_fit(oracle, B, state=st)
+    for method in ("exact", "auto"):
+        got = fit(gpu, B, state=st, method=method)
+        assert np.all(np.isnan(ref["chi2"]))
+        assert np.all(np.isnan(got["chi2"]))
+        assert np.all(got["status"] & gpu.GPD_ST_NAN)
+
+
+def test_mjd_timestamps_quantised_harmonic(gpu, oracle):
+    """Real exposures use t ≈ 86400·MJD ≈ 5.2e9 s (src/GPPupilDemodulation.jl:139): θ = fl(fl(ωt)+ϕ)
+    is quantised at ~3.8e-6 rad; the harmonic path reproduces it by quantising ϕ."""
+    B = synth.make_batch(5000, 32, seed=31, t0=86400.0 * 60000.0)
+    ref = oracle_fit(oracle, B)
+    pert = perturbed_runs(oracle, B)
+    for method in ("exact", "harmonic"):
+        got = fit(gpu, B, method=method)
+        print(assert_fit_parity(got, ref, pert, label=f"mjd/{method}"))
+
+
+def test_large_b_falls_back_to_exact(gpu, oracle):
+    """NEWUOA probing |b| beyond the expansion's safe range (~4.5) → that series is re-fitted
+    by the exact evaluator on device (status FALLBACK), with the same parity."""
+    B = synth.make_batch(4000, 16, seed=41, b_range=(4.6, 5.5))
+    xinit = np.array([5.0, 0.3])
+    ref = oracle_fit(oracle, B, xinit=xinit)
+    got = fit(gpu, B, method="auto", xinit=xinit)
+    assert np.all(got["status"] & gpu.GPD_ST_FALLBACK)
+    assert np.all(got["status"] & gpu.GPD_ST_EXACT)
+    print(assert_fit_parity(got, ref, perturbed_runs(oracle, B, xinit=xinit), label="fallback"))
+
+
+def test_demodulateall_one_exposure_full_size(gpu, oracle):
+    """C2: one GRAVITY exposure, N×40 (32 diodes + 8 FC), N = 1e5, through the API mirror."""
+    N = 100_000
+    B = synth.make_batch(N, 32, seed=42)
+    data = np.empty((N, 40), dtype=np.complex128)
+    data[:, :32] = B["d"].T
+    fop = np.array([gpu.fc_column_of(c) - 1 for c in range(1, 33)])
+    for g in range(8):  # the synthetic FC group of each diode column is its idx() FC column
+        cols = np.nonzero(fop == 32 + g)[0]
+        assert np.all(B["fc_of_pixel"][cols] == B["fc_of_pixel"][cols[0]])
+        data[:, 32 + g] = B["fc"][B["fc_of_pixel"][cols[0]]]
+    output, param, likelihood = gpu.demodulateall(B["t"], data)
+    ref, refout = oracle.fit_batch(B["t"], data[:, :32].T, data.T, fop, want_output=True)
+    pert = [oracle.fit_batch(B["t"], data[:, :32].T, data.T, fop, perturb_seed=s)
+            for s in range(1, 7)]
+    got = np.zeros(32, dtype=gpu.PARAM_DTYPE)
+    got["a"] = [p.a for p in param]
+    got["b"] = [p.b for p in param]
+    got["phi"] = [p.ϕ for p in param]
+    got["chi2"] = likelihood
+    print(assert_fit_parity(got, ref, pert, label="C2 demodulateall"))
+    np.testing.assert_array_equal(output[:, 32:], data[:, 32:])  # FC columns pass through
+    same = np.abs(got["b"] - ref["b"]) <= TOL * ref["b"]
+    assert np.max(np.abs(output[:, :32][:, same] - refout[same].T)) <= 1e-9 * np.abs(data).max()
