@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""Throughput of the per-pixel demodulation fit on MI355X (BASELINE.json metric).
+
+One step = one full `demodulateall`-equivalent fit (grid + NEWUOA + π-flip check + final χ²,
+src/Modulation.jl:388-432) of every series of the batch, inputs resident in HBM, parameter
+records gathered to rank 0 (RCCL) — the demodulated-output pass is not part of the C3 workload
+(160 GB of output cannot coexist with the 200 GB input).
+
+Default workload (N=1): C3 = 1e5 synthetic series × 1e5 samples, fp64 complex, generated on
+device (seeded counter RNG).  Multi-GPU: one process per GPU (torch.distributed.run), weak
+scaling — every rank fits its own 1e5-series shard (global series ids rank·1e5 …).
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "complex samples/sec through demodulate fit (fp64), 1/2/4/8 MI355X + CPU ref"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pixels", type=int, default=100_000, help="series per GPU")
+    ap.add_argument("--samples", type=int, default=100_000)
+    ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--t0", type=float, default=0.0)
+    ap.add_argument("--method", default="auto", choices=["auto", "exact", "harmonic"])
+    ap.add_argument("--cpu-pixels", type=int, default=256,
+                    help="series in the CPU-oracle baseline sample (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+
+    import gpdemod_loader
+
+    gpd = gpdemod_loader.load()
+    L = gpd.load()
+    from gpdemod import shard  # noqa: E402  (package loaded by path as `gpdemod`)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    stream = torch.cuda.current_stream(dev)
+    sptr = ctypes.c_void_p(stream.cuda_stream)
+
+    P, N = args.pixels, args.samples
+    P -= P % 4
+    G = P // 4
+    offset = shard.weak_offset(P, rank)
+    # --- device-resident synthetic batch (untimed setup) -----------------------------------
+    t = torch.empty(N, dtype=torch.float64, device=dev)
+    d = torch.empty((P, N, 2), dtype=torch.float64, device=dev)
+    fc = torch.empty((G, N, 2), dtype=torch.float64, device=dev)
+    fcop = torch.empty(P, dtype=torch.int32, device=dev)
+    truth = torch.empty((P, 64), dtype=torch.uint8, device=dev)
+    params = torch.empty((P, 64), dtype=torch.uint8, device=dev)
+    rc = L.gpd_synth_fill_dev(N, P, offset, args.seed, args.t0, 0.002, 0.1, 0, gpd.M_2PI,
+                              t.data_ptr(), d.data_ptr(), N, fc.data_ptr(), N, fcop.data_ptr(),
+                              truth.data_ptr(), local, sptr)
+    gpd._lib.check(rc)
+    torch.cuda.synchronize(dev)
+
+    flags = gpd.GPD_RECENTER | {"auto": 0, "exact": gpd.GPD_METHOD_EXACT,
+                                "harmonic": gpd.GPD_METHOD_HARMONIC}[args.method]
+    err = ctypes.create_string_buffer(512)
+
+    def step():
+        r = L.gpd_fit_batch_dev(N, P, t.data_ptr(), d.data_ptr(), N, fc.data_ptr(), G, N,
+                                fcop.data_ptr(), None, gpd.M_2PI, None, flags, 60,
+                                params.data_ptr(), None, N, local, sptr, err, len(err))
+        gpd._lib.check(r, err)
+        return shard.gather_records(params, world, rank)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    kern = {}
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        gathered = step()
+        for name, ms in gpd.timings(local).items():  # HIP events on the launch stream
+            kern.setdefault(name, []).append(ms)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t_start
+    if dist:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    samples_total = float(world) * P * N * args.steps
+    value = samples_total / elapsed
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    # --- roofline of the dominant kernel (harmonic moment pass) ---------------------------
+    rec = gpd.PARAM_DTYPE
+    par = gathered[:P].cpu().numpy().reshape(-1).view(rec) if world > 1 else \
+        params.cpu().numpy().reshape(-1).view(rec)
+    roofline = None
+    algo_bytes = P * N * (16 + 16 / 4) + 8 * N  # d + FC phasor shared by 4 + t
+    mom = kern.get("moments")
+    if mom:
+        avg_ms = float(np.mean(mom))
+        achieved = algo_bytes / (avg_ms * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "kernel": "k_moments", "achieved": round(achieved, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": traffic_from_profiles(P, N), "algorithmic_bytes": algo_bytes,
+                    "avg_ms": round(avg_ms, 3)}
+    kernels = {k: round(float(np.mean(v)), 3) for k, v in kern.items()}
+    status = par["status"]
+    fits = {"fallback_exact": int(np.count_nonzero(status & gpd.GPD_ST_FALLBACK)),
+            "maxfun": int(np.count_nonzero(status & gpd.GPD_ST_MAXFUN)),
+            "nan": int(np.count_nonzero(status & gpd.GPD_ST_NAN)),
+            "mean_nfev": round(float(par["nfev"].mean()), 2)}
+    tr = truth.cpu().numpy().reshape(-1).view(rec)
+    fits["median_abs_b_err_vs_truth"] = float(np.median(np.abs(par["b"] - tr["b"])))
+
+    cpu = None
+    if not args.no_cpu and args.cpu_pixels > 0:
+        cpu = cpu_baseline(gpd, t, d, fc, fcop, par, args, N)
+
+    out = {
+        "metric": METRIC, "value": value, "unit": "complex samples/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (device-generated, seeded counter RNG; SURVEY §8d model)",
+        "config": {"workload": "C3" if (P, N) == (100_000, 100_000) else f"{P}x{N}",
+                   "series_per_gpu": P, "samples": N, "total_series": world * P,
+                   "method": args.method, "t0": args.t0, "parallelism": f"series-shard x{world}",
+                   "gather": "RCCL gather of 64-B records to rank 0" if world > 1 else "none"},
+        "roofline": roofline, "cpu_baseline": cpu, "kernels_ms": kernels, "fits": fits,
+    }
+    print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+def traffic_from_profiles(P, N):
+    """HBM bytes per moment-kernel launch from the committed rocprofv3 PMC summary (FETCH_SIZE
+    doubled per MI355X_MICROARCH.md §HBM + WRITE_SIZE), when it was taken on this shape."""
+    path = os.path.join(ROOT, "profiles", "pmc_moments.json")
+    try:
+        with open(path) as f:
+            j = json.load(f)
+        if j.get("pixels") == P and j.get("samples") == N:
+            return j.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_baseline(gpd, t, d, fc, fcop, par, args, N):
+    """Oracle restatement (oracle/, C + OpenMP) on a bounded sample of the same device-resident
+    series, timed on the host; also a full-size parity spot check of those series."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # checker / CPU baseline only
+
+    k = min(args.cpu_pixels, d.shape[0]) // 4 * 4
+    th = t.cpu().numpy()
+    dd = d[:k].cpu().numpy().view(np.complex128).reshape(k, N)
+    ff = fc[: k // 4].cpu().numpy().view(np.complex128).reshape(k // 4, N)
+    fo = fcop[:k].cpu().numpy()
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    t0 = time.perf_counter()
+    ref = oracle.fit_batch(th, dd, ff, fo, flags=oracle.RECENTER, nthreads=threads)
+    dt = time.perf_counter() - t0
+    err = np.abs(par["b"][:k] - ref["b"]) / ref["b"]
+    return {"value": k * N / dt, "unit": "complex samples/s", "cores": threads, "kind": "port",
+            "sample": f"{k} of the device-generated series x {N} samples (first FC groups), "
+                      f"oracle/ C restatement, OpenMP over series, {dt:.1f} s wall",
+            "parity_b_within_1e-10": f"{int((err <= 1e-10).sum())}/{k}",
+            "parity_b_max_rel": float(err.max())}
+
+
+if __name__ == "__main__":
+    main()
