@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile.sh run into profiles/<tag>/ (committed evidence).
+
+HBM bytes per k_moments launch = FETCH_SIZE·1024·2 (gfx950 reports ½ of a wide coalesced
+stream, MI355X_MICROARCH.md §HBM) + WRITE_SIZE·1024, averaged over dispatches."""
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def pmc(path, name):
+    vals = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] == name and "k_moments" in r["Kernel_Name"]:
+                vals.append(float(r["Counter_Value"]))
+    return sum(vals) / len(vals) if vals else None
+
+
+def main(tag, src=None):
+    src = src or os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    bench = json.load(open(os.path.join(src, "bench_trace.json")))
+    stats = {}
+    with open(os.path.join(dst, "kernel_stats.csv")) as f:
+        for r in csv.DictReader(f):
+            stats[r["Name"]] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6}
+    mom = next(v for k, v in stats.items() if "k_moments" in k)
+    fetch_kb = pmc(os.path.join(src, "pmc_fetch", "pmc_counter_collection.csv"), "FETCH_SIZE")
+    write_kb = pmc(os.path.join(src, "pmc_write", "pmc_counter_collection.csv"), "WRITE_SIZE")
+    cfg = bench["config"]
+    hbm = fetch_kb * 1024 * 2 + write_kb * 1024
+    summary = {
+        "tag": tag, "pixels": cfg["series_per_gpu"], "samples": cfg["samples"],
+        "k_moments_avg_ms_rocprof": mom["avg_ms"],
+        "k_moments_avg_ms_hip_events": bench["roofline"]["avg_ms"],
+        "FETCH_SIZE_kB": fetch_kb, "WRITE_SIZE_kB": write_kb,
+        "hbm_bytes_per_launch": hbm,
+        "algorithmic_bytes_per_launch": bench["roofline"]["algorithmic_bytes"],
+        "traffic_over_algorithmic": hbm / bench["roofline"]["algorithmic_bytes"],
+        "bench": bench,
+    }
+    json.dump(summary, open(os.path.join(dst, "summary.json"), "w"), indent=1)
+    json.dump({k: summary[k] for k in ("tag", "pixels", "samples", "hbm_bytes_per_launch",
+                                       "FETCH_SIZE_kB", "WRITE_SIZE_kB")},
+              open(os.path.join(ROOT, "profiles", "pmc_moments.json"), "w"), indent=1)
+    print(json.dumps({k: v for k, v in summary.items() if k != "bench"}, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
