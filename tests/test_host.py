@@ -1,0 +1,59 @@
+"""CPU checks of the host-side mirror (idx/Side/Diode/MetState, FaintStates, argument handling)
+and of the multi-GPU sharding helpers."""
+import numpy as np
+import pytest
+
+
+def test_idx_matches_reference_layout(gpd):
+    """src/Modulation.jl:17-22: FT T1..T4 D1..D4 → 1..16, SC → 17..32, FC FT → 33..36, FC SC → 37..40."""
+    S, D = gpd.Side, gpd.Diode
+    assert gpd.idx(S.FT, 1, D.D1) == 1
+    assert gpd.idx(S.FT, 4, D.D4) == 16
+    assert gpd.idx(S.SC, 1, D.D1) == 17
+    assert gpd.idx(S.SC, 4, D.D4) == 32
+    assert [gpd.idx(S.FT, t, D.FC) for t in range(1, 5)] == [33, 34, 35, 36]
+    assert [gpd.idx(S.SC, t, D.FC) for t in range(1, 5)] == [37, 38, 39, 40]
+    cols = sorted(gpd.idx(s, t, d) for s in S for t in range(1, 5) for d in D)
+    assert cols == list(range(1, 41))
+    for c in range(1, 33):
+        side = S.FT if c <= 16 else S.SC
+        tel = (c - 1) % 16 // 4 + 1
+        assert gpd.fc_column_of(c) == gpd.idx(side, tel, D.FC)
+
+
+def test_metstate_codes(gpd):
+    M = gpd.MetState
+    assert (M.OFF, M.LOW, M.NORMAL, M.HIGH, M.TRANSIENT) == (0, 1, 2, 3, -1)
+
+
+def test_faintstates_orders_by_voltage(gpd):
+    fs = gpd.FaintStates.make([1.0, 2.0], [1.5], 5.0, 1.0)  # voltage1 > voltage2 → swap
+    np.testing.assert_array_equal(fs.timer1, [1.5])
+    np.testing.assert_array_equal(fs.timer2, [1.0, 2.0])
+    assert (fs.state1, fs.state2) == (gpd.MetState.HIGH, gpd.MetState.LOW)
+
+
+def test_demodulateall_validates_like_reference(gpd):
+    t = np.arange(100) * 0.002
+    with pytest.raises(TypeError):
+        gpd.demodulateall(t, np.zeros((100, 40)))            # not complex
+    with pytest.raises(ValueError):
+        gpd.demodulateall(t, np.zeros((100, 39), complex))   # not N×40
+    with pytest.raises(ValueError):
+        gpd.demodulateall(t[:99], np.zeros((100, 40), complex))
+    with pytest.raises(ValueError):
+        gpd.demodulateall(t, np.zeros((100, 40), complex), faintparam=np.zeros(7, np.int8))
+
+
+def test_shard_range_partitions_whole_groups(gpd):
+    from gpdemod import shard
+
+    for n, w in [(100_000, 8), (32, 8), (40, 3), (7, 2), (1, 4)]:
+        spans = [shard.shard_range(n, w, r) for r in range(w)]
+        assert spans[0][0] == 0 and spans[-1][1] == n
+        for (a, b), (c, _) in zip(spans, spans[1:]):
+            assert b == c and a <= b
+        assert all(a % 4 == 0 for a, _ in spans)
+    assert shard.weak_offset(100_000, 3) == 300_000
+    with pytest.raises(ValueError):
+        shard.weak_offset(10, 1)

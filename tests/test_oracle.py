@@ -1,0 +1,167 @@
+"""CPU checks of the oracle (test infrastructure) against known answers and the reference's
+stated properties.  PARITY UNPINNED: the reference ships no tests/fixtures and cannot run here,
+so these pin the restatement with (a) bit-exact Julia constants, (b) published NEWUOA behaviour
+on standard problems, (c) mathematical identities of the model, (d) truth recovery."""
+import json
+import math
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_phi_grid_is_julia_range(oracle):
+    sys.path.insert(0, os.path.join(ROOT, "oracle", "tools"))
+    import phi_grid
+
+    ref = phi_grid.julia_range(-math.pi, math.pi, 8)
+    np.testing.assert_array_equal(oracle.phi_grid(), np.array(ref))
+    assert oracle.phi_grid()[0] == -math.pi and oracle.phi_grid()[-1] == math.pi
+
+
+def test_newuoa_rosenbrock(oracle):
+    f = lambda x: (1 - x[0]) ** 2 + 100 * (x[1] - x[0] ** 2) ** 2
+    x, fx, nf = oracle.newuoa(f, [-1.2, 1.0], 0.5, 1e-8, maxfun=2000)
+    np.testing.assert_allclose(x, [1.0, 1.0], atol=1e-6)
+    assert fx < 1e-12 and nf < 400
+
+
+def test_newuoa_quadratic_exact_minimum(oracle):
+    f = lambda x: (x[0] - 3) ** 2 + 2 * (x[1] + 1) ** 2 + x[0] * x[1]
+    x, fx, nf = oracle.newuoa(f, [0.0, 0.0], 1.0, 1e-7, maxfun=500)
+    np.testing.assert_allclose(x, [4.0, -2.0], atol=1e-6)
+    assert abs(fx + 5.0) < 1e-12
+
+
+def test_newuoa_respects_maxfun(oracle):
+    f = lambda x: (1 - x[0]) ** 2 + 100 * (x[1] - x[0] ** 2) ** 2
+    _, _, nf = oracle.newuoa(f, [-1.2, 1.0], 0.5, 1e-8, maxfun=60)
+    assert nf == 60
+
+
+def _series(seed=4, N=4000, offsets=False):
+    B = synth.make_batch(N, 4, seed=seed, offsets=offsets)
+    p = np.exp(1j * np.angle(B["fc"][0]))
+    return B, p
+
+
+def test_chi2_symmetry_b_phi(oracle):
+    """f(b, ϕ) = f(−b, ϕ + π) (tex/GPPupilDemodulation.tex:189)."""
+    B, p = _series()
+    for b, phi in [(0.7, 0.3), (1.9, -2.0), (2.6, 3.0)]:
+        f1, _ = oracle.chi2(B["t"], B["d"][0], p, b, phi)
+        f2, _ = oracle.chi2(B["t"], B["d"][0], p, -b, phi + math.pi)
+        assert abs(f1 - f2) <= 1e-12 * f1
+
+
+@pytest.mark.parametrize("offsets", [False, True])
+def test_chi2_closed_form_is_least_squares(oracle, offsets):
+    """a (and c) from the closed form (src/Modulation.jl:140-146) are the LS solution; χ² is the
+    weighted residual norm / N (src/Modulation.jl:320)."""
+    B, p = _series(offsets=offsets)
+    t, d = B["t"], B["d"][0]
+    b, phi = 1.3, 0.4
+    f, rec = oracle.chi2(t, d, p, b, phi, offsets=offsets)
+    m = p * np.exp(1j * b * np.sin(6.283185 * t + phi))
+    A = np.stack([np.ones_like(m), m], 1) if offsets else m[:, None]
+    sol, *_ = np.linalg.lstsq(A, d, rcond=None)
+    if offsets:
+        np.testing.assert_allclose([rec["c"], rec["a"]], sol, rtol=1e-10, atol=1e-12)
+    else:
+        np.testing.assert_allclose(rec["a"], sol[0], rtol=1e-12)
+    r = A @ sol - d
+    assert abs(f - np.sum(np.abs(r) ** 2) / len(d)) <= 1e-12 * f
+
+
+def test_fit_recovers_truth(oracle):
+    B = synth.make_batch(20000, 16, seed=11)
+    par = oracle.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"])
+    tr = B["truth"]
+    # noise-limited: σ=0.1 complex noise, 2e4 samples → parameter errors ~1e-3
+    assert np.max(np.abs(par["b"] - tr["b"])) < 1e-2
+    assert np.max(synth.wrap(par["phi"] - tr["phi"]).__abs__()) < 1e-2
+    assert np.max(np.abs(np.abs(par["a"]) - np.abs(tr["a"]))) < 1e-2
+    assert np.all(np.abs(par["chi2"] - 0.01) < 1e-3)  # E|noise|² = σ²
+    assert np.all(par["b"] >= 0)  # sign normalisation
+
+
+def test_mean_var_power_matches_numpy(oracle):
+    rng = np.random.default_rng(0)
+    d = rng.standard_normal(3000) + 1j * rng.standard_normal(3000)
+    st = rng.choice(np.array([0, 1, 2, 3], dtype=np.int8), size=3000)
+    m, w = oracle.mean_var_power(st, d)
+    for s in range(4):
+        sel = st == s
+        a = np.abs(d[sel])
+        np.testing.assert_allclose(m[sel], a.mean(), rtol=1e-13)
+        np.testing.assert_allclose(w[sel], 1 / a.var(ddof=1), rtol=1e-12)
+
+
+def test_mean_var_power_single_sample_state_is_nan(oracle):
+    d = np.ones(10, dtype=np.complex128) * (1 + 1j)
+    st = np.full(10, 2, dtype=np.int8)
+    st[3] = 0
+    m, w = oracle.mean_var_power(st, d)
+    assert np.isnan(w[3]) and np.isfinite(w[0])
+
+
+def py_buildstates(t, t1, t2, pre, post, s1=3, s2=1):
+    """Line-by-line Python transcription of src/Faint.jl:21-73 (lag = 0)."""
+    step = t[1] - t[0]
+    premax, postmax = math.ceil(pre / step), math.ceil(post / step)
+    t1, t2 = list(t1), list(t2)
+    cur, f1, f2, forget, out = 2, t1.pop(0), t2.pop(0), 0, []
+    for time in t:
+        if time >= f1:
+            cur, forget = s1, premax
+            if not t1:
+                f1 = t[-1]
+                if f2 == t[-1]:
+                    cur = 2
+            else:
+                f1 = t1.pop(0)
+        if time >= f2:
+            cur, forget = s2, postmax
+            if not t2:
+                f2 = t[-1]
+                if f1 == t[-1]:
+                    cur = 2
+            else:
+                f2 = t2.pop(0)
+        if forget > 0:
+            out.append(-1)
+            forget -= 1
+        else:
+            out.append(cur)
+    return np.array(out, dtype=np.int8)
+
+
+@pytest.mark.parametrize("pre,post", [(0.0, 0.0), (0.01, 0.3), (0.004, 0.02)])
+def test_buildstates(oracle, pre, post):
+    t = np.arange(3000) * 0.002 + 1.0
+    t1 = 1.0 + np.arange(5) * 1.1 + 0.3    # HIGH switches
+    t2 = t1 + 0.35                          # LOW switches
+    got = oracle.buildstates(t, t1, t2, preswitchdelay=pre, postwitchdelay=post)
+    np.testing.assert_array_equal(got, py_buildstates(t, t1, t2, pre, post))
+    assert set(np.unique(got)) <= {-1, 1, 2, 3}
+
+
+def test_golden_fixtures_reproduce(oracle):
+    """Regression fixtures (tests/golden/, generated by tests/golden/make_golden.py from the
+    oracle on seeded synthetic inputs).  Pins the oracle against silent changes."""
+    path = os.path.join(ROOT, "tests", "golden", "oracle_fits.json")
+    golden = json.load(open(path))
+    for case in golden["cases"]:
+        sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+        import make_golden
+
+        got = make_golden.run_case(oracle, case["spec"])
+        for key in ("b", "phi", "chi2", "a_re", "a_im"):
+            np.testing.assert_allclose(got[key], case["expect"][key], rtol=1e-12, atol=1e-14,
+                                       err_msg=f"{case['spec']['name']}:{key}")
+        np.testing.assert_array_equal(got["nfev"], case["expect"]["nfev"])
