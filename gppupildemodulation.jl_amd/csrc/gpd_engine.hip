@@ -79,7 +79,8 @@ struct Layout {
     long long chunk;
 };
 
-Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic, bool phbuf) {
+Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic, bool phbuf,
+            bool mfma) {
     Layout L{};
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -87,11 +88,14 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
         off += align_up(bytes);
         return o;
     };
-    const long long npg = (P + 63) / 64;
-    long long nch = harmonic ? std::max<long long>(1, 8192 / std::max<long long>(npg, 1)) : 1;
+    // moment-pass grid: (series groups) × (sample chunks), ~8k workgroups in total
+    const long long per = mfma ? MM_PIX : 64;
+    const long long npg = (P + per - 1) / per;
+    const long long target = mfma ? 6144 : 8192;
+    long long nch = harmonic ? std::max<long long>(1, target / std::max<long long>(npg, 1)) : 1;
     nch = std::min<long long>(nch, std::max<long long>(1, (N + 255) / 256));
     long long chunk = (N + nch - 1) / nch;
-    chunk = (chunk + MOM_TS - 1) / MOM_TS * MOM_TS;
+    chunk = (chunk + MM_TS - 1) / MM_TS * MM_TS;
     nch = (N + chunk - 1) / chunk;
     L.nch = (int)nch;
     L.chunk = chunk;
@@ -178,7 +182,12 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
 
     DevCtx *cx = ctx_for(device);
     std::lock_guard<std::mutex> lk(cx->mu);
-    const Layout L = plan(N, P, n_fc, faint, harmonic, phbuf);
+    // fp64 MFMA moment pass by default; GPD_MOMENTS=valu selects the VALU kernel (A/B runs)
+    const char *mk = getenv("GPD_MOMENTS");
+    // buffer descriptors of the MFMA kernel address 128 series rows with 32-bit offsets
+    const bool use_mfma = !(mk && std::string(mk) == "valu") &&
+                          (double)MM_PIX * (double)ldd * 16.0 < 2147483648.0;
+    const Layout L = plan(N, P, n_fc, faint, harmonic, phbuf, use_mfma);
     if (cx->ws_cap < L.total) {
         if (cx->ws) {
             HIP_TRY(hipDeviceSynchronize());
@@ -253,11 +262,19 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     if (harmonic) {
         k_table<<<(unsigned)((N + 255) / 256), 256, 0, stream>>>(t, N, omega, tab);
         mark("table");
-        dim3 g((unsigned)((P + 63) / 64), (unsigned)L.nch);
-        if (faint)
-            k_moments<true><<<g, 64, 0, stream>>>(pb, tab, fstat, L.chunk, part);
-        else
-            k_moments<false><<<g, 64, 0, stream>>>(pb, tab, fstat, L.chunk, part);
+        if (use_mfma) {
+            dim3 g((unsigned)((P + MM_PIX - 1) / MM_PIX), (unsigned)L.nch);
+            if (faint)
+                k_moments_mfma<true><<<g, 256, 0, stream>>>(pb, tab, fstat, L.chunk, part);
+            else
+                k_moments_mfma<false><<<g, 256, 0, stream>>>(pb, tab, fstat, L.chunk, part);
+        } else {
+            dim3 g((unsigned)((P + 63) / 64), (unsigned)L.nch);
+            if (faint)
+                k_moments<true><<<g, 64, 0, stream>>>(pb, tab, fstat, L.chunk, part);
+            else
+                k_moments<false><<<g, 64, 0, stream>>>(pb, tab, fstat, L.chunk, part);
+        }
         mark("moments");
         dim3 gr((unsigned)((P + 255) / 256), (unsigned)NMOM);
         k_reduce_moments<<<gr, 256, 0, stream>>>(part, L.nch, P, info, fstat, faint ? 1 : 0, mom, aux);

@@ -386,6 +386,215 @@ __global__ __launch_bounds__(64) void k_moments(Problem pb, const double *__rest
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// k_moments_mfma: the same moments as a dense fp64 contraction on the matrix cores.
+//   Out[row][col] = Σ_s A[row][s] · B[s][col],  row = (series, re/im of q), col = (harmonic n,
+//   cos/sin), s = sample.  v_mfma_f64_16x16x4_f64: A = 16 rows (8 series) × 4 samples, B = 4
+//   samples × 16 cols (8 harmonics); each wave owns 32 series (4 M-tiles) × 24 harmonics (3
+//   N-tiles) = 12 accumulators (48 f64 per lane).
+// Workgroup = 4 waves = 128 series; tile = MM_TS samples.  Software pipeline per tile:
+//   (1) from registers loaded one tile ahead: normalise the 4 FC samples of the thread's groups,
+//       form q = w p̄ d for its 16 (series, sample) elements → LDS [sample][series] (padded row +
+//       xor swizzle: conflict-free transposed writes and fragment reads); cos/sin rows → LDS;
+//   (2) issue the global loads of the next tile (coalesced 512-B row segments);
+//   (3) barrier; MFMA phase (MM_TS/4 K-steps × 12 MFMAs) while those loads fly; F0 = Σq and
+//       Σ|q|² accumulate on the VALU from the A fragments; (4) barrier.
+// Fragment maps (gfx950, cdna_hip_programming.md §3): A lane l ↔ A[l&15][l>>4];
+// B lane l ↔ B[l>>4][l&15]; D lane l, reg r ↔ D[(l>>4)+4r][l&15].
+typedef double v4d __attribute__((ext_vector_type(4)));
+constexpr int MM_TS = 32;          // samples per tile (8 MFMA K-steps)
+constexpr int MM_PIX = 128;        // series per workgroup
+constexpr int MM_ROW = MM_PIX + 1; // padded LDS row (16-B elements)
+constexpr int MM_GRP = MM_PIX / 4; // FC groups per workgroup
+
+__device__ __forceinline__ int mm_phys(int p, int s) { return s * MM_ROW + (p ^ ((s & 1) << 3)); }
+
+template <bool FAINT>
+__global__ __launch_bounds__(256, 2) void k_moments_mfma(Problem pb, const double *__restrict__ tab,
+                                                         const double *__restrict__ fstat,
+                                                         long long chunk_len,
+                                                         double *__restrict__ part) {
+    __shared__ c64 qs[MM_TS * MM_ROW];
+    __shared__ __attribute__((aligned(16))) double ts[MM_TS * 2 * KH];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const long long p0 = (long long)blockIdx.x * MM_PIX;
+    const long long s_begin = (long long)blockIdx.y * chunk_len;
+    long long s_end = s_begin + chunk_len;
+    if (s_end > pb.N) s_end = pb.N;
+
+    // ---- staging role: sample ss of the tile; FC groups gq + 8 r (r = 0..3), their 4 series
+    __shared__ int fcl[MM_PIX];             // FC column of each series of the workgroup
+    __shared__ double wml[FAINT ? MM_PIX * 5 : 1];  // faint: w·m per series and state
+    const int ss = tid & 31, gq = tid >> 5;
+    if (tid < MM_PIX) {
+        const long long p = p0 + tid;
+        fcl[tid] = p < pb.P ? pb.fcop[p] : 0;
+        if (FAINT) {
+#pragma unroll
+            for (int q = 0; q < 5; ++q)
+                wml[tid * 5 + q] = p < pb.P ? fstat[p * 16 + 5 + q] * fstat[p * 16 + q] : 0.0;
+        }
+    }
+    __syncthreads();
+    int gcol[4];        // group's FC column (series 4g)
+    unsigned ownmask = 0;  // bit 4r+j: series has its own FC column (general fc_of_pixel)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int g = gq + 8 * r;
+        gcol[r] = fcl[4 * g];
+#pragma unroll
+        for (int j = 1; j < 4; ++j)
+            if (fcl[4 * g + j] != gcol[r]) ownmask |= 1u << (4 * r + j);
+    }
+    const long long ldd = pb.ldd, ldfc = pb.ldfc;
+    // series rows of this workgroup through one buffer descriptor (wave-uniform base and size,
+    // T8/T20): per-thread voffset + per-load scalar soffset, out-of-range rows read as 0.
+    const long long nrows = (pb.P - p0) < MM_PIX ? (pb.P - p0) : MM_PIX;
+    const unsigned long long dptr = (unsigned long long)(pb.d + p0 * ldd);
+    const unsigned dlo = __builtin_amdgcn_readfirstlane((unsigned)dptr);
+    const unsigned dhi = __builtin_amdgcn_readfirstlane((unsigned)(dptr >> 32));
+    const unsigned dbytes = __builtin_amdgcn_readfirstlane((unsigned)(nrows * ldd * 16));
+    const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(((unsigned long long)dhi << 32) | dlo), (short)0, (int)dbytes, 0x00020000);
+    const int dvoff = (int)((4 * gq * ldd + ss) * 16);
+    const int ldd16 = __builtin_amdgcn_readfirstlane((int)(ldd * 16));
+    const c64 *fcp[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) fcp[r] = pb.fc + (long long)gcol[r] * ldfc + ss;
+    // ---- MFMA role
+    const int fi = lane & 15, fk = lane >> 4, comp = fi & 1, ppair = fi >> 1;
+    v4d acc[4][3];
+    double f0[4] = {0, 0, 0, 0}, q2[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 3; ++n) acc[m][n] = (v4d){0.0, 0.0, 0.0, 0.0};
+
+    // ---- prefetch registers (one tile ahead)
+    c64 rd[4][4], rf[4];
+    double2 rt[3];
+    auto issue = [&](long long s0) {
+        const bool in = s0 + ss < s_end;
+        const int s016 = (int)(s0 * 16);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            rf[r] = in ? fcp[r][s0] : c64{0.0, 0.0};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(
+                    drs, dvoff, (32 * r + j) * ldd16 + s016, 0);
+                rd[r][j] = __builtin_bit_cast(c64, v);
+            }
+        }
+        // cos/sin rows: MM_TS × 48 doubles = 768 double2, 3 per thread
+        const double2 *trow = (const double2 *)tab + s0 * KH;
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const int e = tid + 256 * u;  // double2 index in the tile
+            rt[u] = s0 + e / KH < s_end ? trow[e] : double2{0.0, 0.0};
+        }
+    };
+    if (s_begin < s_end) issue(s_begin);
+    for (long long s0 = s_begin; s0 < s_end; s0 += MM_TS) {
+        // (1) stage tile s0 from registers
+        const long long s = s0 + ss;
+        int st = 0;
+        const bool sok = (s < s_end) && sample_valid(pb, s, st);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const c64 z = rf[r];
+            const double r2 = z.re * z.re + z.im * z.im;
+            c64 ph = {1.0, 0.0};  // angle(0) = 0
+            if (r2 > 0.0) {
+                const double inv = 1.0 / sqrt(r2);
+                ph = {z.re * inv, z.im * inv};
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int pl = 4 * (gq + 8 * r) + j;  // series within the workgroup
+                c64 pj = ph;
+                if (ownmask & (1u << (4 * r + j))) {  // general fc_of_pixel: own FC column
+                    const c64 zz = pb.fc[(long long)fcl[pl] * ldfc + s];
+                    const double rr = zz.re * zz.re + zz.im * zz.im;
+                    pj = {1.0, 0.0};
+                    if (rr > 0.0) {
+                        const double iv = 1.0 / sqrt(rr);
+                        pj = {zz.re * iv, zz.im * iv};
+                    }
+                }
+                const c64 dv = rd[r][j];
+                c64 q;
+                q.re = fma(pj.re, dv.re, pj.im * dv.im);
+                q.im = fma(pj.re, dv.im, -(pj.im * dv.re));
+                if (FAINT) {
+                    const double f = wml[pl * 5 + st + 1];
+                    q.re *= f;
+                    q.im *= f;
+                }
+                const bool keep = sok && (p0 + pl < pb.P);  // rows beyond P read as 0 anyway
+                q.re = keep ? q.re : 0.0;
+                q.im = keep ? q.im : 0.0;
+                qs[mm_phys(4 * (gq + 8 * r) + j, ss)] = q;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 3; ++u) ((double2 *)ts)[tid + 256 * u] = rt[u];
+        // (2) next tile's loads fly during the MFMA phase
+        if (s0 + MM_TS < s_end) issue(s0 + MM_TS);
+        __syncthreads();
+        // (3) MFMA phase (unroll 2: bounds the LDS fragments the scheduler keeps in flight)
+#pragma unroll 2
+        for (int ks = 0; ks < MM_TS / 4; ++ks) {
+            const int k = ks * 4 + fk;
+            double a[4], b[3];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const c64 q = qs[mm_phys(wave * 32 + m * 8 + ppair, k)];
+                a[m] = comp ? q.im : q.re;
+                f0[m] += a[m];
+                q2[m] = fma(a[m], a[m], q2[m]);
+            }
+#pragma unroll
+            for (int n = 0; n < 3; ++n) b[n] = ts[k * 2 * KH + n * 16 + fi];
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int n = 0; n < 3; ++n)
+                    acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b[n], acc[m][n], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    // ---- epilogue: harmonic moments from the accumulators
+    double *base = part + (long long)blockIdx.y * NMOM * pb.P;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 3; ++n)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = fk + 4 * r, col = fi;
+                const long long pix = p0 + wave * 32 + m * 8 + (row >> 1);
+                const int cq = row & 1, trig = col & 1;
+                const int h = n * 8 + (col >> 1);  // harmonic index 0..K-1 (n = h + 1)
+                const int code = cq == 0 ? (trig == 0 ? 0 : 3) : (trig == 1 ? 1 : 2);
+                if (pix < pb.P) base[(long long)(3 + 4 * h + code) * pb.P + pix] = acc[m][n][r];
+            }
+    // ---- F0 (re/im lanes) and Σ|q|² (= Σ w²|p|²|d|²; Σ|d|² when w = |p| = 1)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        f0[m] += __shfl_xor(f0[m], 16, 64);
+        f0[m] += __shfl_xor(f0[m], 32, 64);
+        q2[m] += __shfl_xor(q2[m], 16, 64);
+        q2[m] += __shfl_xor(q2[m], 32, 64);
+        const double q2o = __shfl_xor(q2[m], 1, 64);
+        const long long pix = p0 + wave * 32 + m * 8 + ppair;
+        if (fk == 0 && pix < pb.P) {
+            base[(long long)comp * pb.P + pix] = f0[m];
+            if (comp == 0) base[2 * pb.P + pix] = q2[m] + q2o;
+        }
+    }
+}
+
 // k_reduce_moments: mom[m][k] = Σ_chunk part[chunk][m][k] (fixed order), plus per-series
 // aux[k] = {W2, DEN, Q2, 0}.
 __global__ __launch_bounds__(256) void k_reduce_moments(const double *__restrict__ part, int nch,
