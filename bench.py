@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--t0", type=float, default=0.0)
     ap.add_argument("--method", default="auto", choices=["auto", "exact", "harmonic"])
-    ap.add_argument("--cpu-pixels", type=int, default=256,
+    ap.add_argument("--cpu-pixels", type=int, default=2048,
                     help="series in the CPU-oracle baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")

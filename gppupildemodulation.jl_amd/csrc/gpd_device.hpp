@@ -66,49 +66,43 @@ __device__ __forceinline__ c64 cisj(double x) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Bessel functions of the first kind J_0..J_{KP} at b (any sign) by Miller's backward
-// recurrence J_{n-1} = (2n/b) J_n − J_{n+1}, normalised with J_0 + 2 Σ_k J_{2k} = 1, with
-// rescaling against overflow.  Relative accuracy ~1e-16 for |b| ≤ KP/2.
+// Bessel functions of the first kind J_0..J_{KP} at b (any sign), the coefficients of the
+// Jacobi–Anger expansion.  |b| ≥ 0.05: Miller's backward recurrence J_{n-1} = (2n/b) J_n − J_{n+1}
+// from the fixed, fully unrolled start order KP + 32 (compile-time indices: no select chains),
+// normalised with J_0 + 2 Σ_k J_{2k} = 1; relative accuracy ~1e-16 for |b| ≤ 0.45·KP (callers
+// reject larger |b|).  |b| < 0.05: ascending series J_n = Σ_k (−b²/4)^k (b/2)^n / (k! (n+k)!).
 template <int KP>
 __host__ __device__ __forceinline__ void bessel_j(double b, double (&J)[KP + 1]) {
     const double ab = fabs(b);
-    if (ab == 0.0) {
-        J[0] = 1.0;
+    if (ab < 0.05) {
+        const double h = 0.5 * ab, h2 = -h * h;
+        double pw = 1.0;  // (b/2)^n / n!
 #pragma unroll
-        for (int n = 1; n <= KP; ++n) J[n] = 0.0;
-        return;
-    }
-    // start order: even, comfortably above max(KP, |b|)
-    int m = KP + 20 + (int)ab;
-    m += (m & 1);
-    const double inv = 2.0 / ab;
-    double jp1 = 0.0, jn = 1.0e-280, norm = 0.0;
-#pragma unroll
-    for (int n = 0; n <= KP; ++n) J[n] = 0.0;
-    for (int n = m; n >= 1; --n) {
-        const double jm1 = (double)n * inv * jn - jp1;  // J_{n-1}
-        jp1 = jn;
-        jn = jm1;
-        // J_n now stored in jp1; record orders ≤ KP
-        if (n <= KP) {
-#pragma unroll
-            for (int q = 1; q <= KP; ++q)
-                if (q == n) J[q] = jp1;
+        for (int n = 0; n <= KP; ++n) {
+            // Σ_{k=0..4} h2^k / (k! (n+1)…(n+k)): |h2|^5 ≤ 4e-18 relative
+            const double c1 = h2 / (n + 1), c2 = c1 * h2 / (2.0 * (n + 2)),
+                         c3 = c2 * h2 / (3.0 * (n + 3)), c4 = c3 * h2 / (4.0 * (n + 4));
+            J[n] = pw * (1.0 + (c1 + (c2 + (c3 + c4))));
+            pw = pw * h / (n + 1);
         }
-        if ((n & 1) == 0) norm += 2.0 * jp1;  // even order n contributes 2 J_n
-        if (fabs(jn) > 1.0e250) {              // rescale everything accumulated so far
-            jn *= 1.0e-250;
-            jp1 *= 1.0e-250;
-            norm *= 1.0e-250;
+    } else {
+        constexpr int M = KP + 32;  // even start order
+        const double inv = 2.0 / ab;
+        double jp1 = 0.0, jn = 1.0e-280, norm = 0.0;
 #pragma unroll
-            for (int q = 1; q <= KP; ++q) J[q] *= 1.0e-250;
+        for (int n = M; n >= 1; --n) {
+            const double jm1 = (double)n * inv * jn - jp1;  // J_{n-1}
+            jp1 = jn;
+            jn = jm1;
+            if (n <= KP) J[n] = jp1;
+            if ((n & 1) == 0) norm += 2.0 * jp1;
         }
-    }
-    J[0] = jn;
-    norm += jn;
-    const double s = 1.0 / norm;
+        J[0] = jn;
+        norm += jn;
+        const double sc = 1.0 / norm;
 #pragma unroll
-    for (int n = 0; n <= KP; ++n) J[n] *= s;
+        for (int n = 0; n <= KP; ++n) J[n] *= sc;
+    }
     if (b < 0.0) {
 #pragma unroll
         for (int n = 1; n <= KP; n += 2) J[n] = -J[n];

@@ -138,7 +138,8 @@ typedef struct {
     gsum_t *gs;        /* reduction scratch */
     oracle_param *mod; /* mutated by every evaluation, like lkl.mod */
     int nfev;
-    uint64_t perturb;  /* 0, or a seed: χ² *= 1 ± 2^-52 per evaluation (tie-sensitivity probe) */
+    uint64_t perturb;  /* 0, or a seed: χ² *= 1 + u per evaluation (tie-sensitivity probe) */
+    double perturb_ulps; /* |u| = 2^-52 (≤ 1), or uniform in [0, perturb_ulps·2^-52] */
 } chi2_ctx;
 
 static uint64_t mix64(uint64_t x) {
@@ -242,7 +243,9 @@ static double chi2_eval(chi2_ctx *c, double b, double phi) {
         gsum_total(g, &s);
     }
     if (c->perturb) {
-        const double u = (mix64(c->perturb ^ ((uint64_t)c->nfev << 20)) & 1) ? 0x1p-52 : -0x1p-52;
+        const uint64_t r = mix64(c->perturb ^ ((uint64_t)c->nfev << 20));
+        double u = (r & 1) ? 0x1p-52 : -0x1p-52;
+        if (c->perturb_ulps > 1.0) u *= c->perturb_ulps * (double)(r >> 11) * 0x1p-53;
         return (s / (double)n) * (1.0 + u);
     }
     return s / (double)n;
@@ -383,7 +386,7 @@ static int julia_argmin(const double *v, int n) { /* findmin: first NaN, else fi
 static void fit_pixel(int64_t n, const double *t, const cplx *dcol, const cplx *fccol,
                       const int8_t *state, double omega, const double *xinit, uint32_t flags,
                       int maxfun, oracle_param *par, cplx *outcol, scratch_t *s,
-                      uint64_t perturb) {
+                      uint64_t perturb, double perturb_ulps) {
     const int offsets = (flags & ORACLE_FIT_OFFSETS) != 0;
     const int faint = state != NULL;
     int64_t nv = 0;
@@ -434,6 +437,7 @@ static void fit_pixel(int64_t n, const double *t, const cplx *dcol, const cplx *
     c.mod = par;
     c.nfev = 0;
     c.perturb = perturb;
+    c.perturb_ulps = perturb_ulps;
 
     double x[2];
     if (xinit) {
@@ -495,7 +499,7 @@ int oracle_fit_batch(int64_t n_samples, int64_t n_pixels, const double *t, const
                      int64_t ldd, const double *fc, int64_t ldfc, const int32_t *fc_of_pixel,
                      const int8_t *state, double omega, const double *xinit, uint32_t flags,
                      int maxfun, oracle_param *params, double *out, int64_t ldo, int nthreads,
-                     uint64_t perturb_seed) {
+                     uint64_t perturb_seed, double perturb_ulps) {
     (void)ldfc;
     const int64_t n = n_samples;
 #ifdef _OPENMP
@@ -519,7 +523,7 @@ int oracle_fit_batch(int64_t n_samples, int64_t n_pixels, const double *t, const
             const cplx *fcol = (const cplx *)fc + (size_t)fc_of_pixel[k] * (size_t)ldfc;
             cplx *ocol = out ? (cplx *)out + (size_t)k * (size_t)ldo : NULL;
             const uint64_t pk = perturb_seed ? mix64(perturb_seed * 0x100000001B3ull + (uint64_t)k) | 1u : 0;
-            fit_pixel(n, t, dcol, fcol, state, omega, xinit, flags, maxfun, &params[k], ocol, &s, pk);
+            fit_pixel(n, t, dcol, fcol, state, omega, xinit, flags, maxfun, &params[k], ocol, &s, pk, perturb_ulps);
         }
         free(s.t);
         free(s.w);

@@ -41,12 +41,14 @@ double oracle_chi2(int64_t n, const double *t, const double *d, const double *w,
  *   xinit: NULL (:auto grid) or 2 doubles
  *   out (optional, may be NULL): demodulated columns, column-major complex, ld = ldo
  * Returns 0.  nthreads <= 0 → all available.  perturb_seed != 0 multiplies every χ² value by
- * 1 ± 2^-52 (pseudo-random sign): probes how NEWUOA's tie-breaks react to 1-ulp differences. */
+ * 1 ± 2^-52 (pseudo-random sign; perturb_ulps ≤ 1) or by 1 + u, |u| uniform in
+ * [0, perturb_ulps·2^-52] (perturb_ulps > 1): probes how NEWUOA's tie-breaks react to χ²
+ * differences of the size other summation orders / evaluators produce. */
 int oracle_fit_batch(int64_t n_samples, int64_t n_pixels, const double *t, const double *d,
                      int64_t ldd, const double *fc, int64_t ldfc, const int32_t *fc_of_pixel,
                      const int8_t *state, double omega, const double *xinit, uint32_t flags,
                      int maxfun, oracle_param *params, double *out, int64_t ldo, int nthreads,
-                     uint64_t perturb_seed);
+                     uint64_t perturb_seed, double perturb_ulps);
 
 /* src/Faint.jl:21-73 buildstates (timers already lag-shifted by the caller when lag≠0). */
 int oracle_buildstates(int64_t n, const double *t, int64_t n1, const double *timer1, int64_t n2,

@@ -27,7 +27,10 @@ _lib = None
 
 
 def build(force: bool = False) -> str:
-    if force or not os.path.exists(_LIB):
+    srcs = ("newuoa_oracle.c", "demod_oracle.c", "oracle.h", "Makefile")
+    stale = not os.path.exists(_LIB) or any(
+        os.path.getmtime(os.path.join(_HERE, f)) > os.path.getmtime(_LIB) for f in srcs)
+    if force or stale:
         subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return _LIB
 
@@ -41,7 +44,7 @@ def lib():
         L.oracle_fit_batch.argtypes = [ctypes.c_int64, ctypes.c_int64, P, P, ctypes.c_int64, P,
                                        ctypes.c_int64, P, P, ctypes.c_double, P, ctypes.c_uint32,
                                        ctypes.c_int, P, P, ctypes.c_int64, ctypes.c_int,
-                                       ctypes.c_uint64]
+                                       ctypes.c_uint64, ctypes.c_double]
         L.oracle_fit_batch.restype = ctypes.c_int
         L.oracle_chi2.argtypes = [ctypes.c_int64, P, P, P, P, ctypes.c_double, ctypes.c_int,
                                   ctypes.c_double, ctypes.c_double, P]
@@ -84,7 +87,7 @@ def newuoa(f, x0, rhobeg, rhoend, maxfun=None, npt=None):
 
 
 def fit_batch(t, d, fc, fc_of_pixel, state=None, omega=M_2PI, xinit=None, flags=RECENTER,
-              maxfun=60, want_output=False, nthreads=0, perturb_seed=0):
+              maxfun=60, want_output=False, nthreads=0, perturb_seed=0, perturb_ulps=1.0):
     """Oracle batch fit.  d: (n_pixels, n_samples) complex128 (row k = pixel column k),
     fc: (n_fc, n_samples) complex128, fc_of_pixel: (n_pixels,) int32."""
     L = lib()
@@ -99,7 +102,8 @@ def fit_batch(t, d, fc, fc_of_pixel, state=None, omega=M_2PI, xinit=None, flags=
     out = np.zeros_like(d) if want_output else None
     rc = L.oracle_fit_batch(N, P, _ptr(t), _ptr(d), N, _ptr(fc), N, _ptr(fop), _ptr(st),
                             float(omega), _ptr(xi), int(flags), int(maxfun), _ptr(params),
-                            _ptr(out), N, int(nthreads), int(perturb_seed))
+                            _ptr(out), N, int(nthreads), int(perturb_seed),
+                            float(perturb_ulps))
     if rc != 0:
         raise RuntimeError(f"oracle_fit_batch failed: {rc}")
     return (params, out) if want_output else params
