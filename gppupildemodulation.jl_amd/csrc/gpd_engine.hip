@@ -182,11 +182,13 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
 
     DevCtx *cx = ctx_for(device);
     std::lock_guard<std::mutex> lk(cx->mu);
-    // fp64 MFMA moment pass by default; GPD_MOMENTS=valu selects the VALU kernel (A/B runs)
+    // fp64 MFMA moment pass by default (producer/consumer kernel for non-faint series);
+    // GPD_MOMENTS=valu | mfma1 selects the VALU / single-role MFMA kernel (A/B runs)
     const char *mk = getenv("GPD_MOMENTS");
     // buffer descriptors of the MFMA kernel address 128 series rows with 32-bit offsets
     const bool use_mfma = !(mk && std::string(mk) == "valu") &&
-                          (double)MM_PIX * (double)ldd * 16.0 < 2147483648.0;
+                          (double)MM_PIX * (double)ldd * 16.0 < 2147483648.0 &&
+                          (double)N * KH * 16.0 < 2147483648.0;
     const Layout L = plan(N, P, n_fc, faint, harmonic, phbuf, use_mfma);
     if (cx->ws_cap < L.total) {
         if (cx->ws) {
@@ -242,7 +244,13 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     Param *outp = (Param *)out_params;
 
     int nt = 0;
+    // GPD_SYNC_DEBUG=1: synchronise after every stage and name the stage that faulted
+    static const bool sync_debug = getenv("GPD_SYNC_DEBUG") != nullptr;
     auto mark = [&](const char *name) {
+        if (sync_debug) {
+            const hipError_t e = hipStreamSynchronize(stream);
+            if (e != hipSuccess) fprintf(stderr, "gpdemod: stage %s: %s\n", name, hipGetErrorString(e));
+        }
         if (nt < kMaxTimers) {
             cx->tname[nt] = name;
             (void)hipEventRecord(cx->ev[nt + 1], stream);
@@ -266,8 +274,14 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             dim3 g((unsigned)((P + MM_PIX - 1) / MM_PIX), (unsigned)L.nch);
             if (faint)
                 k_moments_mfma<true><<<g, 256, 0, stream>>>(pb, tab, fstat, L.chunk, part);
-            else
+            else if (mk && std::string(mk) == "mfma1")  // single-role kernel (A/B runs)
                 k_moments_mfma<false><<<g, 256, 0, stream>>>(pb, tab, fstat, L.chunk, part);
+            else if (mk && std::string(mk) == "ws_nomfma")  // timing experiments only
+                k_moments_ws<1><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
+            else if (mk && std::string(mk) == "ws_noload")
+                k_moments_ws<2><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
+            else
+                k_moments_ws<0><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
         } else {
             dim3 g((unsigned)((P + 63) / 64), (unsigned)L.nch);
             if (faint)

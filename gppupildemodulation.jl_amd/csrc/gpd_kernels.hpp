@@ -402,6 +402,16 @@ __global__ __launch_bounds__(64) void k_moments(Problem pb, const double *__rest
 // Fragment maps (gfx950, cdna_hip_programming.md §3): A lane l ↔ A[l&15][l>>4];
 // B lane l ↔ B[l>>4][l&15]; D lane l, reg r ↔ D[(l>>4)+4r][l&15].
 typedef double v4d __attribute__((ext_vector_type(4)));
+
+// A pointer made provably wave-uniform for a buffer descriptor (T8).  readfirstlane returns
+// int: each half is taken back to unsigned before widening, or a low word with bit 31 set
+// would sign-extend over the high word.
+__device__ __forceinline__ void *uniform_ptr(const void *p) {
+    const unsigned long long v = (unsigned long long)p;
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32));
+    return (void *)(((unsigned long long)hi << 32) | lo);
+}
 constexpr int MM_TS = 32;          // samples per tile (8 MFMA K-steps)
 constexpr int MM_PIX = 128;        // series per workgroup
 constexpr int MM_ROW = MM_PIX + 1; // padded LDS row (16-B elements)
@@ -450,12 +460,9 @@ __global__ __launch_bounds__(256, 2) void k_moments_mfma(Problem pb, const doubl
     // series rows of this workgroup through one buffer descriptor (wave-uniform base and size,
     // T8/T20): per-thread voffset + per-load scalar soffset, out-of-range rows read as 0.
     const long long nrows = (pb.P - p0) < MM_PIX ? (pb.P - p0) : MM_PIX;
-    const unsigned long long dptr = (unsigned long long)(pb.d + p0 * ldd);
-    const unsigned dlo = __builtin_amdgcn_readfirstlane((unsigned)dptr);
-    const unsigned dhi = __builtin_amdgcn_readfirstlane((unsigned)(dptr >> 32));
     const unsigned dbytes = __builtin_amdgcn_readfirstlane((unsigned)(nrows * ldd * 16));
     const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(((unsigned long long)dhi << 32) | dlo), (short)0, (int)dbytes, 0x00020000);
+        uniform_ptr(pb.d + p0 * ldd), (short)0, (int)dbytes, 0x00020000);
     const int dvoff = (int)((4 * gq * ldd + ss) * 16);
     const int ldd16 = __builtin_amdgcn_readfirstlane((int)(ldd * 16));
     const c64 *fcp[4];
@@ -481,8 +488,9 @@ __global__ __launch_bounds__(256, 2) void k_moments_mfma(Problem pb, const doubl
             rf[r] = in ? fcp[r][s0] : c64{0.0, 0.0};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
+                // every offset part in voffset: the range check ignores soffset
                 const auto v = __builtin_amdgcn_raw_buffer_load_b128(
-                    drs, dvoff, (32 * r + j) * ldd16 + s016, 0);
+                    drs, dvoff + (32 * r + j) * ldd16 + s016, 0, 0);
                 rd[r][j] = __builtin_bit_cast(c64, v);
             }
         }
@@ -580,6 +588,266 @@ __global__ __launch_bounds__(256, 2) void k_moments_mfma(Problem pb, const doubl
                 if (pix < pb.P) base[(long long)(3 + 4 * h + code) * pb.P + pix] = acc[m][n][r];
             }
     // ---- F0 (re/im lanes) and Σ|q|² (= Σ w²|p|²|d|²; Σ|d|² when w = |p| = 1)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        f0[m] += __shfl_xor(f0[m], 16, 64);
+        f0[m] += __shfl_xor(f0[m], 32, 64);
+        q2[m] += __shfl_xor(q2[m], 16, 64);
+        q2[m] += __shfl_xor(q2[m], 32, 64);
+        const double q2o = __shfl_xor(q2[m], 1, 64);
+        const long long pix = p0 + wave * 32 + m * 8 + ppair;
+        if (fk == 0 && pix < pb.P) {
+            base[(long long)comp * pb.P + pix] = f0[m];
+            if (comp == 0) base[2 * pb.P + pix] = q2[m] + q2o;
+        }
+    }
+}
+
+// k_moments_ws: the MFMA contraction with producer/consumer wave roles (non-faint series).
+//   Workgroup = 8 waves, one workgroup per CU (LDS 157 KB): waves 0-3 (consumers) only run the
+//   MFMA phase of k_moments_mfma (same fragments, same 12 accumulators per wave); waves 4-7
+//   (producers) stream d / FC / cos-sin rows two tiles ahead in registers, form q = p̄ d and
+//   write the next tile into the other half of a double-buffered LDS tile.  One barrier per
+//   tile: consumers on buffer i&1 while producers fill buffer (i+1)&1, so each SIMD hosts one
+//   consumer that keeps its matrix core busy and one producer whose loads and VALU work overlap
+//   it (the single-role kernel serialises staging and MFMA behind two barriers per tile).
+template <bool B>
+struct BoolTag {
+    static constexpr bool value = B;
+};
+
+struct WsRegs {
+    c64 d[4][4], f[4];
+};
+
+// DBG (timing experiments only, results invalid): 1 = consumers skip the MFMA phase,
+// 2 = producers skip the global loads.
+template <int DBG = 0>
+__global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double *__restrict__ tab,
+                                                       long long chunk_len,
+                                                       double *__restrict__ part) {
+    __shared__ c64 qs[2][MM_TS * MM_ROW];
+    __shared__ __attribute__((aligned(16))) double ts[2][MM_TS * 2 * KH];
+    __shared__ int fcl[MM_PIX];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const long long p0 = (long long)blockIdx.x * MM_PIX;
+    const long long s_begin = (long long)blockIdx.y * chunk_len;
+    long long s_end = s_begin + chunk_len;
+    if (s_end > pb.N) s_end = pb.N;
+    const int ntiles = s_end > s_begin ? (int)((s_end - s_begin + MM_TS - 1) / MM_TS) : 0;
+    if (tid < MM_PIX) {
+        const long long p = p0 + tid;
+        fcl[tid] = p < pb.P ? pb.fcop[p] : 0;
+    }
+    __syncthreads();
+    // general layout: some series of the workgroup does not use its 4-group's FC column
+    // (uniform: every thread scans the same 128 LDS words)
+    const int nrow = (int)((pb.P - p0) < MM_PIX ? (pb.P - p0) : MM_PIX);
+    bool general = false;
+    for (int k = 0; k < nrow; ++k) general |= fcl[k] != fcl[k & ~3];
+
+    if (wave >= 4) {
+        // ================================ producer ================================
+        // Branch-free loads (clamped indices; d through a buffer descriptor whose range check
+        // zero-fills rows beyond P), so the in-order vmcnt waits of stage() only ever wait for
+        // the register set being staged, never for the set two tiles ahead.
+        const int ptid = tid - 256;
+        const int ss = ptid & 31, gq = ptid >> 5;
+        const long long ldd = pb.ldd, ldfc = pb.ldfc, Nm1 = pb.N - 1;
+        const long long nrows = (pb.P - p0) < MM_PIX ? (pb.P - p0) : MM_PIX;
+        const unsigned dbytes = __builtin_amdgcn_readfirstlane((unsigned)(nrows * ldd * 16));
+        const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
+            uniform_ptr(pb.d + p0 * ldd), (short)0, (int)dbytes, 0x00020000);
+        const int dvoff = (int)((4 * gq * ldd + ss) * 16);
+        const int ldd16 = __builtin_amdgcn_readfirstlane((int)(ldd * 16));
+        const c64 *fcb[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) fcb[r] = pb.fc + (long long)fcl[4 * (gq + 8 * r)] * ldfc;
+        // cos/sin tile: MM_TS rows × KH double2; this thread's slots e = ptid + 256 u, read
+        // through a buffer descriptor (rows ≥ N read as 0; keeps the loads where they are issued
+        // — plain loads of the read-only table would be sunk to their use past the barrier)
+        const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(
+            uniform_ptr(tab), (short)0, __builtin_amdgcn_readfirstlane((int)(pb.N * KH * 16)),
+            0x00020000);
+        const int tvoff = ptid * 16;  // slot e = ptid + 256 u of a tile starting at row s0
+
+        auto issue = [&](WsRegs &R, int it) {
+            if constexpr (DBG == 2) {
+                for (int r = 0; r < 4; ++r) {
+                    R.f[r] = c64{1.0 + it, 0.0};
+                    for (int j = 0; j < 4; ++j) R.d[r][j] = c64{0.5 * it, 1.0};
+                }
+                return;
+            }
+            it = it < ntiles ? it : ntiles - 1;
+            const long long s0 = s_begin + (long long)it * MM_TS;
+            const long long sl = (s0 + ss) < Nm1 ? (s0 + ss) : Nm1;
+            const int s016 = (int)(s0 * 16);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                R.f[r] = fcb[r][sl];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    // all offset parts in voffset (the range check ignores soffset): rows
+                    // beyond P and samples beyond the last row read as 0
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(
+                        drs, dvoff + (32 * r + j) * ldd16 + s016, 0, 0);
+                    R.d[r][j] = __builtin_bit_cast(c64, v);
+                }
+            }
+        };
+        // cos/sin rows (L2-resident table) one tile ahead in a single register set
+        double2 T0, T1, T2;
+        auto issue_t = [&](int it) {
+            if constexpr (DBG == 2) {
+                T0 = T1 = T2 = double2{0.25 * it, 1.0};
+                return;
+            }
+            it = it < ntiles ? it : ntiles - 1;
+            const int vo = tvoff + (int)((s_begin + (long long)it * MM_TS) * KH * 16);
+            T0 = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(trs, vo, 0, 0));
+            T1 = __builtin_bit_cast(double2,
+                                    __builtin_amdgcn_raw_buffer_load_b128(trs, vo + 4096, 0, 0));
+            T2 = __builtin_bit_cast(double2,
+                                    __builtin_amdgcn_raw_buffer_load_b128(trs, vo + 8192, 0, 0));
+        };
+        auto stage = [&](const WsRegs &R, int it, auto gen) {
+            if (it >= ntiles) return;
+            const long long s = s_begin + (long long)it * MM_TS + ss;
+            const bool sok = s < s_end;
+            const long long sl = s < Nm1 ? s : Nm1;
+            c64 *q_out = qs[it & 1];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const c64 z = R.f[r];
+                const double r2 = z.re * z.re + z.im * z.im;
+                const double inv = r2 > 0.0 ? 1.0 / sqrt(r2) : 0.0;
+                c64 ph = {z.re * inv, z.im * inv};
+                ph.re = r2 > 0.0 ? ph.re : 1.0;  // angle(0) = 0
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int pl = 4 * (gq + 8 * r) + j;
+                    c64 pj = ph;
+                    if (decltype(gen)::value) {  // general layout: the series' own FC column
+                        const c64 zz = pb.fc[(long long)fcl[pl] * ldfc + sl];
+                        const double rr = zz.re * zz.re + zz.im * zz.im;
+                        const double iv = rr > 0.0 ? 1.0 / sqrt(rr) : 0.0;
+                        pj = {zz.re * iv, zz.im * iv};
+                        pj.re = rr > 0.0 ? pj.re : 1.0;
+                    }
+                    const c64 dv = R.d[r][j];
+                    c64 q;
+                    q.re = fma(pj.re, dv.re, pj.im * dv.im);
+                    q.im = fma(pj.re, dv.im, -(pj.im * dv.re));
+                    q.re = sok ? q.re : 0.0;  // rows beyond P read as 0 already
+                    q.im = sok ? q.im : 0.0;
+                    q_out[mm_phys(pl, ss)] = q;
+                }
+            }
+            double2 *tsb = (double2 *)ts[it & 1] + ptid;
+            tsb[0] = T0;
+            tsb[256] = T1;
+            tsb[512] = T2;
+        };
+
+        auto run = [&](auto gen) {
+            WsRegs R0, R1;
+            issue(R0, 0);
+            issue_t(0);
+            issue(R1, 1);
+            stage(R0, 0, gen);
+            issue_t(1);
+            issue(R0, 2);
+            __syncthreads();
+            // iteration i: stage tile i+1 (registers loaded two iterations ago), reload them
+            // with tile i+3; unrolled by two so each register set is a fixed set of VGPRs, with
+            // the odd last iteration peeled so the loop body has no conditional loads
+            int i = 0;
+            for (; i + 1 < ntiles; i += 2) {
+                stage(R1, i + 1, gen);
+                issue_t(i + 2);
+                issue(R1, i + 3);
+                __syncthreads();
+                stage(R0, i + 2, gen);
+                issue_t(i + 3);
+                issue(R0, i + 4);
+                __syncthreads();
+            }
+            if (i < ntiles) {
+                stage(R1, i + 1, gen);
+                __syncthreads();
+            }
+        };
+        if (general)
+            run(BoolTag<true>{});
+        else
+            run(BoolTag<false>{});
+        // the last iterations re-read the final tile; let those loads land before the wave
+        // ends rather than leave them in flight past s_endpgm
+        __builtin_amdgcn_s_waitcnt(0);
+        return;
+    }
+
+    // ================================ consumer ================================
+    const int fi = lane & 15, fk = lane >> 4, comp = fi & 1, ppair = fi >> 1;
+    v4d acc[4][3];
+    double f0[4] = {0, 0, 0, 0}, q2[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 3; ++n) acc[m][n] = (v4d){0.0, 0.0, 0.0, 0.0};
+    __syncthreads();  // tile 0 staged
+    // fragments of K-step ks+1 are read from LDS while the 12 MFMAs of K-step ks run
+    // (register double buffer; only the first read of each tile waits on LDS latency)
+    for (int i = 0; i < ntiles; ++i) {
+        const double *qd = (const double *)qs[i & 1];
+        const double *tb = ts[i & 1];
+        auto ldfrag = [&](int ks, double (&a)[4], double (&b)[3]) {
+            const int k = ks * 4 + fk;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) a[m] = qd[2 * mm_phys(wave * 32 + m * 8 + ppair, k) + comp];
+#pragma unroll
+            for (int n = 0; n < 3; ++n) b[n] = tb[k * 2 * KH + n * 16 + fi];
+        };
+        auto step = [&](const double (&a)[4], const double (&b)[3]) {
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int n = 0; n < 3; ++n)
+                    acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b[n], acc[m][n], 0, 0, 0);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                f0[m] += a[m];
+                q2[m] = fma(a[m], a[m], q2[m]);
+            }
+        };
+        if constexpr (DBG != 1) {
+            double a0[4], b0[3], a1[4], b1[3];
+            ldfrag(0, a0, b0);
+#pragma unroll
+            for (int ks = 0; ks < MM_TS / 4; ks += 2) {
+                ldfrag(ks + 1, a1, b1);
+                step(a0, b0);
+                if (ks + 2 < MM_TS / 4) ldfrag(ks + 2, a0, b0);
+                step(a1, b1);
+            }
+        }
+        __syncthreads();
+    }
+    double *base = part + (long long)blockIdx.y * NMOM * pb.P;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 3; ++n)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = fk + 4 * r, col = fi;
+                const long long pix = p0 + wave * 32 + m * 8 + (row >> 1);
+                const int cq = row & 1, trig = col & 1;
+                const int h = n * 8 + (col >> 1);
+                const int code = cq == 0 ? (trig == 0 ? 0 : 3) : (trig == 1 ? 1 : 2);
+                if (pix < pb.P) base[(long long)(3 + 4 * h + code) * pb.P + pix] = acc[m][n][r];
+            }
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
         f0[m] += __shfl_xor(f0[m], 16, 64);
