@@ -403,6 +403,17 @@ __global__ __launch_bounds__(64) void k_moments(Problem pb, const double *__rest
 // B lane l ↔ B[l>>4][l&15]; D lane l, reg r ↔ D[(l>>4)+4r][l&15].
 typedef double v4d __attribute__((ext_vector_type(4)));
 
+// z/|z| for the harmonic moments (angle(0) = 0 → 1): v_rsq_f64 + one Newton step, ~1 ulp
+// — the harmonic path's tolerance is set by its truncation test, not by correct rounding.
+__device__ __forceinline__ c64 unit_phasor(c64 z) {
+    const double r2 = fma(z.re, z.re, z.im * z.im);
+    double y = __builtin_amdgcn_rsq(r2);
+    y = y * fma(-0.5 * r2, y * y, 1.5);
+    c64 ph = {z.re * y, z.im * y};
+    if (!(r2 > 0.0)) ph = {1.0, 0.0};
+    return ph;
+}
+
 // A pointer made provably wave-uniform for a buffer descriptor (T8).  readfirstlane returns
 // int: each half is taken back to unsigned before widening, or a low word with bit 31 set
 // would sign-extend over the high word.
@@ -711,45 +722,48 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             T2 = __builtin_bit_cast(double2,
                                     __builtin_amdgcn_raw_buffer_load_b128(trs, vo + 8192, 0, 0));
         };
-        auto stage = [&](const WsRegs &R, int it, auto gen) {
-            if (it >= ntiles) return;
+        auto stage_q = [&](const WsRegs &R, int it, auto gen, auto partial) {
             const long long s = s_begin + (long long)it * MM_TS + ss;
             const bool sok = s < s_end;
             const long long sl = s < Nm1 ? s : Nm1;
             c64 *q_out = qs[it & 1];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const c64 z = R.f[r];
-                const double r2 = z.re * z.re + z.im * z.im;
-                const double inv = r2 > 0.0 ? 1.0 / sqrt(r2) : 0.0;
-                c64 ph = {z.re * inv, z.im * inv};
-                ph.re = r2 > 0.0 ? ph.re : 1.0;  // angle(0) = 0
+                const c64 ph = unit_phasor(R.f[r]);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int pl = 4 * (gq + 8 * r) + j;
                     c64 pj = ph;
-                    if (decltype(gen)::value) {  // general layout: the series' own FC column
-                        const c64 zz = pb.fc[(long long)fcl[pl] * ldfc + sl];
-                        const double rr = zz.re * zz.re + zz.im * zz.im;
-                        const double iv = rr > 0.0 ? 1.0 / sqrt(rr) : 0.0;
-                        pj = {zz.re * iv, zz.im * iv};
-                        pj.re = rr > 0.0 ? pj.re : 1.0;
-                    }
+                    if (decltype(gen)::value)  // general layout: the series' own FC column
+                        pj = unit_phasor(pb.fc[(long long)fcl[pl] * ldfc + sl]);
                     const c64 dv = R.d[r][j];
                     c64 q;
                     q.re = fma(pj.re, dv.re, pj.im * dv.im);
                     q.im = fma(pj.re, dv.im, -(pj.im * dv.re));
-                    q.re = sok ? q.re : 0.0;  // rows beyond P read as 0 already
-                    q.im = sok ? q.im : 0.0;
+                    if (decltype(partial)::value) {  // rows beyond P read as 0 already
+                        q.re = sok ? q.re : 0.0;
+                        q.im = sok ? q.im : 0.0;
+                    }
                     q_out[mm_phys(pl, ss)] = q;
                 }
             }
+        };
+        auto stage = [&](const WsRegs &R, int it, auto gen) {
+            if (it >= ntiles) return;
+            // only a chunk's last tile can be partial (chunks are whole tiles, N may not be)
+            if (s_begin + (long long)(it + 1) * MM_TS <= s_end)  // uniform
+                stage_q(R, it, gen, BoolTag<false>{});
+            else
+                stage_q(R, it, gen, BoolTag<true>{});
             double2 *tsb = (double2 *)ts[it & 1] + ptid;
             tsb[0] = T0;
             tsb[256] = T1;
             tsb[512] = T2;
         };
 
+        // loader waves first: their few VALU ops and the next loads must not queue behind the
+        // MFMA stream of the consumer wave on the same SIMD (fp64 MFMA and VALU share it)
+        __builtin_amdgcn_s_setprio(2);
         auto run = [&](auto gen) {
             WsRegs R0, R1;
             issue(R0, 0);
