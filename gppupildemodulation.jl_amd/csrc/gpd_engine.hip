@@ -56,6 +56,7 @@ struct DevCtx {
     const char *tname[kMaxTimers] = {};
     int ntimers = 0;
     bool have_timers = false;
+    int n_cu = 0;  // compute units (wave-quantisation of the moment grid)
 };
 
 std::mutex g_mu;
@@ -80,7 +81,7 @@ struct Layout {
 };
 
 Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic, bool phbuf,
-            bool mfma) {
+            bool mfma, int n_cu) {
     Layout L{};
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -88,11 +89,30 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
         off += align_up(bytes);
         return o;
     };
-    // moment-pass grid: (series groups) × (sample chunks), ~8k workgroups in total
+    // moment-pass grid: (series groups) × (sample chunks).  The producer/consumer kernel runs
+    // one workgroup per CU, so the chunk count is chosen to fill the last wave of workgroups:
+    // among 6..32 chunks the one whose grid wastes the smallest fraction of its last wave
+    // (C3 on 256 CUs: 782 × 17 = 13294 = 51.9 waves) — more chunks also mean more partial
+    // moments (nch·99·P doubles), so ties go to the smaller count.  Few series (npg·6 below
+    // the CU count): ~6k workgroups of short chunks instead.
     const long long per = mfma ? MM_PIX : 64;
     const long long npg = (P + per - 1) / per;
-    const long long target = mfma ? 6144 : 8192;
-    long long nch = harmonic ? std::max<long long>(1, target / std::max<long long>(npg, 1)) : 1;
+    long long nch = 1;
+    if (harmonic) {
+        if (mfma && n_cu > 0 && npg * 6 >= n_cu) {
+            double best = 2.0;
+            for (long long c = 6; c <= 32; ++c) {
+                const double w = (double)(npg * c) / n_cu;
+                const double waste = (std::ceil(w) - w) / std::ceil(w);
+                if (waste < best - 0.005) {
+                    best = waste;
+                    nch = c;
+                }
+            }
+        } else {
+            nch = std::max<long long>(1, (mfma ? 6144 : 8192) / std::max<long long>(npg, 1));
+        }
+    }
     nch = std::min<long long>(nch, std::max<long long>(1, (N + 255) / 256));
     long long chunk = (N + nch - 1) / nch;
     chunk = (chunk + MM_TS - 1) / MM_TS * MM_TS;
@@ -189,7 +209,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     const bool use_mfma = !(mk && std::string(mk) == "valu") &&
                           (double)MM_PIX * (double)ldd * 16.0 < 2147483648.0 &&
                           (double)N * KH * 16.0 < 2147483648.0;
-    const Layout L = plan(N, P, n_fc, faint, harmonic, phbuf, use_mfma);
+    if (cx->n_cu == 0) HIP_TRY(hipDeviceGetAttribute(&cx->n_cu, hipDeviceAttributeMultiprocessorCount, device));
+    const Layout L = plan(N, P, n_fc, faint, harmonic, phbuf, use_mfma, cx->n_cu);
     if (cx->ws_cap < L.total) {
         if (cx->ws) {
             HIP_TRY(hipDeviceSynchronize());
@@ -280,6 +301,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                 k_moments_ws<1><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
             else if (mk && std::string(mk) == "ws_noload")
                 k_moments_ws<2><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
+            else if (mk && std::string(mk) == "ws_mfmaonly")
+                k_moments_ws<5><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
             else
                 k_moments_ws<0><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
         } else {

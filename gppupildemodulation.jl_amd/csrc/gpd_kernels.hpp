@@ -632,7 +632,7 @@ struct WsRegs {
 };
 
 // DBG (timing experiments only, results invalid): 1 = consumers skip the MFMA phase,
-// 2 = producers skip the global loads.
+// 2 = producers skip the global loads, 5 = producers only keep the barrier cadence.
 template <int DBG = 0>
 __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double *__restrict__ tab,
                                                        long long chunk_len,
@@ -683,7 +683,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
         const int tvoff = ptid * 16;  // slot e = ptid + 256 u of a tile starting at row s0
 
         auto issue = [&](WsRegs &R, int it) {
-            if constexpr (DBG == 2) {
+            if constexpr (DBG == 2 || DBG == 5) {
                 for (int r = 0; r < 4; ++r) {
                     R.f[r] = c64{1.0 + it, 0.0};
                     for (int j = 0; j < 4; ++j) R.d[r][j] = c64{0.5 * it, 1.0};
@@ -710,7 +710,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
         // cos/sin rows (L2-resident table) one tile ahead in a single register set
         double2 T0, T1, T2;
         auto issue_t = [&](int it) {
-            if constexpr (DBG == 2) {
+            if constexpr (DBG == 2 || DBG == 5) {
                 T0 = T1 = T2 = double2{0.25 * it, 1.0};
                 return;
             }
@@ -750,6 +750,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
         };
         auto stage = [&](const WsRegs &R, int it, auto gen) {
             if (it >= ntiles) return;
+            if constexpr (DBG == 5) return;
             // only a chunk's last tile can be partial (chunks are whole tiles, N may not be)
             if (s_begin + (long long)(it + 1) * MM_TS <= s_end)  // uniform
                 stage_q(R, it, gen, BoolTag<false>{});
