@@ -914,7 +914,9 @@ struct HarmChi2 {
     int nfev;
     bool fallback;
 
-    __device__ double operator()(const double (&x)[2]) {
+    // one out-of-line copy: NEWUOA calls the objective from several sites, and each inlined
+    // copy of the Bessel recurrence + 24-harmonic sum adds its own live registers
+    __device__ __attribute__((noinline)) double operator()(const double (&x)[2]) {
         ++nfev;
         if (fallback) return 0.0;
         const double b = x[0];

@@ -19,6 +19,9 @@ namespace gpd {
 
 #define GPD_HD __host__ __device__ __forceinline__
 #define GPD_HDN __host__ __device__
+// the large NEWUOA subroutines stay out of line: inlined into one body their temporaries
+// exceed the register file (512 VGPR+AGPR and ~1.4 KB of spills per lane)
+#define GPD_HDX __host__ __device__ __attribute__((noinline))
 
 // ---------------------------------------------------------------- select helpers ------
 template <int L>
@@ -101,7 +104,7 @@ struct Newuoa {
 
     // ------------------------------------------------------------------------- TRSAPP
     // Truncated CG + 2-D boundary search for the trust-region step.  Writes step, crvmin.
-    GPD_HDN void trsapp(double delta, double (&step)[N], double &crvmin) const {
+    GPD_HDX void trsapp(double delta, double (&step)[N], double &crvmin) const {
         double dv[N], g[N], hd[N], hs[N];
         const double delsq = delta * delta;
         int iterc = 0;
@@ -255,7 +258,7 @@ struct Newuoa {
 
     // ------------------------------------------------------------------------- BIGLAG
     // Step that (approximately) maximises |Lagrange function knew| within radius delta.
-    GPD_HDN void biglag(int idz, int knew, double delta, double &alpha) {
+    GPD_HDX void biglag(int idz, int knew, double delta, double &alpha) {
         double hcol[NPT], gc[N], gd[N], s[N], wv[N];
         const double delsq = delta * delta;
         h_column(knew, idz, hcol);
@@ -384,7 +387,7 @@ struct Newuoa {
 
     // ------------------------------------------------------------------------- BIGDEN
     // Alternative step maximising |denominator| of the update; sets w (Wcheck), vlag, beta.
-    GPD_HDN void bigden(int idz, int kopt, int knew, double &beta) {
+    GPD_HDX void bigden(int idz, int kopt, int knew, double &beta) {
         double hw[N + NPT];                    // W(1..N+NPT) of the published routine
         double s[N], den[9], denex[9], par[9];
         double wvec[NDIM][5], prod[NDIM][5];
@@ -674,7 +677,7 @@ struct Newuoa {
 
     // ------------------------------------------------------------------------- UPDATE
     // Shift interpolation point knew: update BMAT, ZMAT, IDZ (vlag, beta from the step).
-    GPD_HDN void update(int &idz, double beta, int knew) {
+    GPD_HDX void update(int &idz, double beta, int knew) {
         double wk[NDIM];
         int jl = 1;  // 1-based column index into zmat
 #pragma unroll
@@ -1204,7 +1207,7 @@ struct Newuoa {
     }
 
     // Move XBASE to XBASE+XOPT (NEWUOB label 120 block).
-    GPD_HDN void shift_base(double &xoptsq, int idz) {
+    GPD_HDX void shift_base(double &xoptsq, int idz) {
         const double tempq = 0.25 * xoptsq;
         double wt[NPT], v[N], wi[N];
 #pragma unroll
