@@ -16,14 +16,15 @@ from ._lib import (GPD_FIT_OFFSETS, GPD_METHOD_EXACT, GPD_METHOD_HARMONIC, GPD_O
                    GPD_RECENTER, GPD_ST_EXACT, GPD_ST_FALLBACK, GPD_ST_MAXFUN, GPD_ST_NAN,
                    GPD_ST_REFIT, PARAM_DTYPE, GpdError, load, timings)
 from .demod import (M_2PI, Diode, FaintStates, MetState, ModulationNoOffsets,
-                    ModulationWithOffsets, Side, buildstates, chi2_batch, demodulateall, fc_column_of,
-                    fit_batch, idx)
+                    ModulationWithOffsets, Side, buildstates, chi2_batch, demodulate_windows,
+                    demodulateall, fc_column_of, fit_batch, fit_windows, idx, window_length,
+                    window_tables)
 
 __all__ = [
     "GPD_FIT_OFFSETS", "GPD_METHOD_EXACT", "GPD_METHOD_HARMONIC", "GPD_ONLY_HIGH", "GPD_RECENTER",
     "GPD_ST_EXACT", "GPD_ST_FALLBACK", "GPD_ST_MAXFUN", "GPD_ST_NAN", "GPD_ST_REFIT",
     "PARAM_DTYPE", "GpdError", "load", "timings", "M_2PI", "Diode", "FaintStates", "MetState",
     "ModulationNoOffsets", "ModulationWithOffsets", "Side", "buildstates", "chi2_batch",
-    "demodulateall",
-    "fc_column_of", "fit_batch", "idx",
+    "demodulate_windows", "demodulateall", "fc_column_of", "fit_batch", "fit_windows", "idx",
+    "window_length", "window_tables",
 ]

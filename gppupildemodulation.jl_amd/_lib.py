@@ -41,7 +41,7 @@ assert PARAM_DTYPE.itemsize == 64
 # every symbol declared in include/gpdemod.h
 EXPORTS = ("gpd_version", "gpd_strerror", "gpd_device_count", "gpd_fit_batch",
            "gpd_fit_batch_dev", "gpd_chi2_batch", "gpd_chi2_batch_dev", "gpd_buildstates",
-           "gpd_synth_fill_dev", "gpd_last_timings")
+           "gpd_synth_fill_dev", "gpd_last_timings", "gpd_fit_windows", "gpd_fit_windows_dev")
 
 
 class GpdError(RuntimeError):
@@ -80,6 +80,11 @@ def load():
     L.gpd_chi2_batch.argtypes = chi + [I32, ctypes.c_char_p, ctypes.c_size_t]
     L.gpd_chi2_batch_dev.restype = ctypes.c_int
     L.gpd_chi2_batch_dev.argtypes = chi + [ctypes.c_int, V, ctypes.c_char_p, ctypes.c_size_t]
+    win = [I64, I64] + common[1:]  # n_samples, window, n_cols, ... (same tail as gpd_fit_batch)
+    L.gpd_fit_windows.restype = ctypes.c_int
+    L.gpd_fit_windows.argtypes = win + [I32, ctypes.c_char_p, ctypes.c_size_t]
+    L.gpd_fit_windows_dev.restype = ctypes.c_int
+    L.gpd_fit_windows_dev.argtypes = win + [ctypes.c_int, V, ctypes.c_char_p, ctypes.c_size_t]
     L.gpd_buildstates.restype = ctypes.c_int
     L.gpd_buildstates.argtypes = [I64, V, I64, V, I64, V, D, D, V]
     L.gpd_synth_fill_dev.restype = ctypes.c_int

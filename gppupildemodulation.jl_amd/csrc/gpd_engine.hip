@@ -162,14 +162,23 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                         const double *xinit, uint32_t flags, int32_t maxfun,
                         gpd_param *out_params, gpd_c64 *out_demod, int64_t ldo,
                         const double *bphi, int device, void *stream_, char *errbuf,
-                        size_t errlen) {
-    if (n_samples < 2 || n_pixels < 1 || !t || !d || !fc || !fc_of_pixel || !out_params ||
-        ldd < n_samples || ldfc < n_samples || n_fc < 1 || (out_demod && ldo < n_samples)) {
+                        size_t errlen, int64_t window = 0) {
+    if (window < 0 || (window > 0 && bphi)) {
+        set_err(errbuf, errlen, "gpd_fit_windows: window must be >= 0 (and fits only)");
+        return GPD_E_ARG;
+    }
+    if (window > 0 && (flags & GPD_METHOD_HARMONIC)) {
+        set_err(errbuf, errlen, "gpd_fit_windows: windows use the exact evaluator");
+        return GPD_E_ARG;
+    }
+    if (n_samples < (window > 0 ? 1 : 2) || n_pixels < 1 || !t || !d || !fc || !fc_of_pixel ||
+        !out_params || ldd < n_samples || ldfc < n_samples || n_fc < 1 ||
+        (out_demod && ldo < n_samples)) {
         set_err(errbuf, errlen, "gpd_fit_batch_dev: invalid shapes/pointers (N=%lld P=%lld)",
                 (long long)n_samples, (long long)n_pixels);
         return GPD_E_ARG;
     }
-    if (n_pixels > (int64_t)0x7fffff00) {
+    if (n_pixels * (window > 0 ? (n_samples + window - 1) / window : 1) > (int64_t)0x7fffff00) {
         set_err(errbuf, errlen, "gpd_fit_batch_dev: too many series");
         return GPD_E_ARG;
     }
@@ -191,13 +200,17 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     const bool faint = state != nullptr;
     const bool offs = (flags & GPD_FIT_OFFSETS) != 0;
     // Harmonic moments cover the no-offsets χ²; offsets go to the exact evaluator.
-    const bool want_exact = (flags & GPD_METHOD_EXACT) || offs;
+    // Windows (≤ ~10k samples each) are fitted by the exact evaluator: one workgroup per
+    // (window, diode) series.
+    const bool want_exact = (flags & GPD_METHOD_EXACT) || offs || window > 0;
     if ((flags & GPD_METHOD_HARMONIC) && offs) {
         set_err(errbuf, errlen, "gpd_fit_batch_dev: harmonic method does not support fitoffsets yet");
         return GPD_E_ARG;
     }
     const bool harmonic = !want_exact;
-    const long long N = n_samples, P = n_pixels;
+    const long long N = n_samples, ncol = n_pixels;
+    const long long nwin = window > 0 ? (N + window - 1) / window : 1;
+    const long long P = ncol * nwin;  // series
     const bool phbuf = want_exact && (size_t)n_fc * N * sizeof(c64) <= (size_t(4) << 30);
 
     DevCtx *cx = ctx_for(device);
@@ -262,6 +275,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     pb.has_xinit = xinit != nullptr;
     pb.x0 = xinit ? xinit[0] : 0.0;
     pb.x1 = xinit ? xinit[1] : 0.0;
+    pb.win = window;
+    pb.ncol = ncol;
     Param *outp = (Param *)out_params;
 
     int nt = 0;
@@ -363,7 +378,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         mark(bphi ? "chi2_exact" : "fit_exact");
     }
     if (out_demod && !bphi) {
-        dim3 g((unsigned)std::min<long long>((N + 255) / 256, 64), (unsigned)P);
+        const long long span = window > 0 ? std::min<long long>(window, N) : N;
+        dim3 g((unsigned)std::min<long long>((span + 255) / 256, 64), (unsigned)P);
         k_output<<<g, 256, 0, stream>>>(pb, outp, raw, (c64 *)out_demod, ldo);
         mark("output");
     }
@@ -401,6 +417,21 @@ int gpd_chi2_batch_dev(int64_t n_samples, int64_t n_pixels, const double *t, con
                         errbuf, errlen);
 }
 
+int gpd_fit_windows_dev(int64_t n_samples, int64_t window, int64_t n_cols, const double *t,
+                        const gpd_c64 *d, int64_t ldd, const gpd_c64 *fc, int64_t n_fc,
+                        int64_t ldfc, const int32_t *fc_of_col, const int8_t *state, double omega,
+                        const double *xinit, uint32_t flags, int32_t maxfun,
+                        gpd_param *out_params, gpd_c64 *out_demod, int64_t ldo, int device,
+                        void *stream, char *errbuf, size_t errlen) {
+    if (window < 1) {
+        set_err(errbuf, errlen, "gpd_fit_windows_dev: window must be >= 1");
+        return GPD_E_ARG;
+    }
+    return pipeline_dev(n_samples, n_cols, t, d, ldd, fc, n_fc, ldfc, fc_of_col, state, omega,
+                        xinit, flags, maxfun, out_params, out_demod, ldo, nullptr, device, stream,
+                        errbuf, errlen, window);
+}
+
 int gpd_last_timings(int device, const char **names, double *ms, int cap) {
     if (device < 0 || device >= gpd_device_count()) return 0;
     DevCtx *cx = ctx_for(device);
@@ -427,9 +458,10 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
                       const int32_t *fc_of_pixel, const int8_t *state, double omega,
                       const double *xinit, uint32_t flags, int32_t maxfun, gpd_param *out_params,
                       gpd_c64 *out_demod, int64_t ldo, const double *bphi, int32_t n_gpus,
-                      char *errbuf, size_t errlen) {
+                      char *errbuf, size_t errlen, int64_t window = 0) {
     if (n_samples < 2 || n_pixels < 1 || !t || !d || !fc || !fc_of_pixel || !out_params ||
-        ldd < n_samples || ldfc < n_samples || n_fc < 1 || (out_demod && ldo < n_samples)) {
+        ldd < n_samples || ldfc < n_samples || n_fc < 1 || (out_demod && ldo < n_samples) ||
+        window < 0) {
         set_err(errbuf, errlen, "gpd_batch: invalid shapes/pointers");
         return GPD_E_ARG;
     }
@@ -446,8 +478,9 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
         return GPD_E_NODEV;
     }
     int G = n_gpus <= 0 ? 1 : std::min<int>(n_gpus, ndev);
-    G = (int)std::min<int64_t>(G, n_pixels);
-    const int64_t N = n_samples;
+    const int64_t nwin = window > 0 ? (n_samples + window - 1) / window : 0;
+    G = (int)std::min<int64_t>(G, window > 0 ? nwin : n_pixels);
+    const int64_t Nall = n_samples;
     std::vector<int> rc(G, GPD_OK);
     std::vector<std::string> msg(G);
 
@@ -459,7 +492,19 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
             rc[g] = code;
             msg[g] = eb;
         };
-        const int64_t p0 = n_pixels * g / G, p1 = n_pixels * (g + 1) / G, P = p1 - p0;
+        // series mode: device g owns series [p0, p1) over all samples; window mode: it owns
+        // windows [w0, w1), i.e. samples [s0, s0 + N) of every column
+        int64_t p0 = n_pixels * g / G, p1 = n_pixels * (g + 1) / G, s0 = 0, N = Nall, o0 = p0;
+        if (window > 0) {
+            const int64_t w0 = nwin * g / G, w1 = nwin * (g + 1) / G;
+            p0 = 0;
+            p1 = n_pixels;
+            s0 = w0 * window;
+            N = std::min<int64_t>(Nall, w1 * window) - s0;
+            o0 = w0 * n_pixels;  // first output record (window-major)
+        }
+        const int64_t P = p1 - p0;
+        const int64_t nrec = window > 0 ? P * ((N + window - 1) / window) : P;
         if (hipSetDevice(g) != hipSuccess) {
             set_err(errbuf_l, errlen_l, "hipSetDevice(%d) failed", g);
             return fail(GPD_E_HIP);
@@ -494,7 +539,7 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
                   chk(hipMalloc(&dd, (size_t)P * N * sizeof(c64)), "hipMalloc d") &&
                   chk(hipMalloc(&dfc, (size_t)n_fc * N * sizeof(c64)), "hipMalloc fc") &&
                   chk(hipMalloc(&dfcop, P * sizeof(int32_t)), "hipMalloc fcop") &&
-                  chk(hipMalloc(&dpar, P * sizeof(Param)), "hipMalloc params") &&
+                  chk(hipMalloc(&dpar, nrec * sizeof(Param)), "hipMalloc params") &&
                   (!state || chk(hipMalloc(&dst, N), "hipMalloc state")) &&
                   (!bphi || chk(hipMalloc(&dbphi, 2 * P * sizeof(double)), "hipMalloc bphi")) &&
                   (!out_demod || chk(hipMalloc(&dout, (size_t)P * N * sizeof(c64)), "hipMalloc out"));
@@ -503,14 +548,14 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
             (void)hipGetLastError();
             return fail(GPD_E_OOM);
         }
-        ok = chk(hipMemcpyAsync(dt, t, N * sizeof(double), hipMemcpyHostToDevice, s), "H2D t") &&
-             chk(hipMemcpy2DAsync(dd, N * sizeof(c64), d + p0 * ldd, ldd * sizeof(gpd_c64),
+        ok = chk(hipMemcpyAsync(dt, t + s0, N * sizeof(double), hipMemcpyHostToDevice, s), "H2D t") &&
+             chk(hipMemcpy2DAsync(dd, N * sizeof(c64), d + p0 * ldd + s0, ldd * sizeof(gpd_c64),
                                   N * sizeof(c64), P, hipMemcpyHostToDevice, s), "H2D d") &&
-             chk(hipMemcpy2DAsync(dfc, N * sizeof(c64), fc, ldfc * sizeof(gpd_c64), N * sizeof(c64),
-                                  n_fc, hipMemcpyHostToDevice, s), "H2D fc") &&
+             chk(hipMemcpy2DAsync(dfc, N * sizeof(c64), fc + s0, ldfc * sizeof(gpd_c64),
+                                  N * sizeof(c64), n_fc, hipMemcpyHostToDevice, s), "H2D fc") &&
              chk(hipMemcpyAsync(dfcop, fc_of_pixel + p0, P * sizeof(int32_t), hipMemcpyHostToDevice, s),
                  "H2D fcop") &&
-             (!state || chk(hipMemcpyAsync(dst, state, N, hipMemcpyHostToDevice, s), "H2D state")) &&
+             (!state || chk(hipMemcpyAsync(dst, state + s0, N, hipMemcpyHostToDevice, s), "H2D state")) &&
              (!bphi || chk(hipMemcpyAsync(dbphi, bphi + 2 * p0, 2 * P * sizeof(double),
                                           hipMemcpyHostToDevice, s), "H2D bphi"));
         if (!ok) {
@@ -519,14 +564,14 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
         }
         int r = pipeline_dev(N, P, dt, (const gpd_c64 *)dd, N, (const gpd_c64 *)dfc, n_fc, N, dfcop,
                              dst, omega, xinit, flags, maxfun, (gpd_param *)dpar, (gpd_c64 *)dout, N,
-                             dbphi, g, s, errbuf_l, errlen_l);
+                             dbphi, g, s, errbuf_l, errlen_l, window);
         if (r != GPD_OK) {
             cleanup();
             return fail(r);
         }
-        ok = chk(hipMemcpyAsync(out_params + p0, dpar, P * sizeof(Param), hipMemcpyDeviceToHost, s),
+        ok = chk(hipMemcpyAsync(out_params + o0, dpar, nrec * sizeof(Param), hipMemcpyDeviceToHost, s),
                  "D2H params") &&
-             (!out_demod || chk(hipMemcpy2DAsync(out_demod + p0 * ldo, ldo * sizeof(gpd_c64), dout,
+             (!out_demod || chk(hipMemcpy2DAsync(out_demod + p0 * ldo + s0, ldo * sizeof(gpd_c64), dout,
                                                  N * sizeof(c64), N * sizeof(c64), P,
                                                  hipMemcpyDeviceToHost, s), "D2H out")) &&
              chk(hipStreamSynchronize(s), "hipStreamSynchronize");
@@ -573,6 +618,24 @@ int gpd_chi2_batch(int64_t n_samples, int64_t n_pixels, const double *t, const g
     return host_batch(n_samples, n_pixels, t, d, ldd, fc, n_fc, ldfc, fc_of_pixel, state, omega,
                       nullptr, flags, 0, out_params, nullptr, n_samples, bphi, n_gpus, errbuf,
                       errlen);
+}
+
+int gpd_fit_windows(int64_t n_samples, int64_t window, int64_t n_cols, const double *t,
+                    const gpd_c64 *d, int64_t ldd, const gpd_c64 *fc, int64_t n_fc, int64_t ldfc,
+                    const int32_t *fc_of_col, const int8_t *state, double omega,
+                    const double *xinit, uint32_t flags, int32_t maxfun, gpd_param *out_params,
+                    gpd_c64 *out_demod, int64_t ldo, int32_t n_gpus, char *errbuf, size_t errlen) {
+    if (window < 1) {
+        set_err(errbuf, errlen, "gpd_fit_windows: window must be >= 1");
+        return GPD_E_ARG;
+    }
+    if (flags & GPD_METHOD_HARMONIC) {
+        set_err(errbuf, errlen, "gpd_fit_windows: windows use the exact evaluator");
+        return GPD_E_ARG;
+    }
+    return host_batch(n_samples, n_cols, t, d, ldd, fc, n_fc, ldfc, fc_of_col, state, omega,
+                      xinit, flags, maxfun, out_params, out_demod, ldo, nullptr, n_gpus, errbuf,
+                      errlen, window);
 }
 
 int gpd_synth_fill_dev(int64_t n_samples, int64_t n_pixels, int64_t pixel_offset, uint64_t seed,

@@ -61,7 +61,22 @@ struct Problem {
     int maxfun;
     int has_xinit;
     double x0, x1;
+    // windowed batches (src/GPPupilDemodulation.jl:191-205): win > 0 splits the samples into
+    // consecutive windows of win samples (the last one shorter); series k is column k % ncol
+    // of window k / ncol.  win = 0: series k is column k over all N samples.
+    long long win, ncol;
 };
+
+// Column and sample range [s0, s1) of series k.
+struct Span {
+    long long col, s0, s1;
+};
+__device__ __forceinline__ Span span_of(const Problem &pb, long long k) {
+    if (pb.win <= 0) return {k, 0, pb.N};
+    const long long w = k / pb.ncol;
+    const long long s0 = w * pb.win;
+    return {k - w * pb.ncol, s0, s0 + pb.win < pb.N ? s0 + pb.win : pb.N};
+}
 
 __device__ __forceinline__ bool sample_valid(const Problem &pb, long long i, int &st) {
     if (pb.state == nullptr) {
@@ -229,11 +244,12 @@ __global__ __launch_bounds__(256) void k_table(const double *__restrict__ t, lon
 __global__ __launch_bounds__(256) void k_faint_stats(Problem pb, double *__restrict__ out) {
     __shared__ double lds[4 * 15];
     const long long k = blockIdx.x;
-    const c64 *d = pb.d + k * pb.ldd;
+    const Span sp = span_of(pb, k);  // per window: compute_mean_var_power on state[I] (:205)
+    const c64 *d = pb.d + sp.col * pb.ldd;
     double v[15];
 #pragma unroll
     for (int q = 0; q < 15; ++q) v[q] = 0.0;
-    for (long long i = threadIdx.x; i < pb.N; i += 256) {
+    for (long long i = sp.s0 + threadIdx.x; i < sp.s1; i += 256) {
         int st;
         if (!sample_valid(pb, i, st)) continue;
         const c64 z = d[i];
@@ -252,7 +268,7 @@ __global__ __launch_bounds__(256) void k_faint_stats(Problem pb, double *__restr
 #pragma unroll
     for (int q = 0; q < 5; ++q) m[q] = v[5 + q] / v[q];
     double s[5] = {0, 0, 0, 0, 0};
-    for (long long i = threadIdx.x; i < pb.N; i += 256) {
+    for (long long i = sp.s0 + threadIdx.x; i < sp.s1; i += 256) {
         int st;
         if (!sample_valid(pb, i, st)) continue;
         const c64 z = d[i];
@@ -1008,11 +1024,12 @@ template <bool FAINT, bool OFFS, bool PHBUF>
 struct ExactChi2 {
     const Problem *pb;
     const c64 *__restrict__ d;
-    const c64 *__restrict__ src;  // PHBUF: phasor column; else raw FC column
+    const c64 *__restrict__ src;  // PHBUF: phasor column; else raw FC column (setup_exact)
     double *lds;
     double m5[5], w5[5];
     double nvalid;
     double a_re, a_im, c_re, c_im;
+    long long s0, s1;  // sample range (the series' window)
     int nfev;
 
     __device__ __forceinline__ bool load(long long i, c64 &p, double &w) const {
@@ -1044,10 +1061,9 @@ struct ExactChi2 {
     __device__ double operator()(const double (&x)[2]) {
         ++nfev;
         const double b = x[0], phi = x[1];
-        const long long N = pb->N;
         if (OFFS) {
             double v[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // a11, a12(2), a22, b1(2), b2(2)
-            for (long long i = threadIdx.x; i < N; i += EXACT_WG) {
+            for (long long i = s0 + threadIdx.x; i < s1; i += EXACT_WG) {
                 c64 p;
                 double w;
                 if (!load(i, p, w)) continue;
@@ -1079,7 +1095,7 @@ struct ExactChi2 {
             a_im = aa.im;
         } else {
             double v[4] = {0, 0, 0, 0};  // num(2), den(2)
-            for (long long i = threadIdx.x; i < N; i += EXACT_WG) {
+            for (long long i = s0 + threadIdx.x; i < s1; i += EXACT_WG) {
                 c64 p;
                 double w;
                 if (!load(i, p, w)) continue;
@@ -1101,7 +1117,7 @@ struct ExactChi2 {
         // weighted_norm2(model .- data, weight) / N  (src/Modulation.jl:299-305, 325)
         double s[1] = {0.0};
         const c64 aa = {a_re, a_im};
-        for (long long i = threadIdx.x; i < N; i += EXACT_WG) {
+        for (long long i = s0 + threadIdx.x; i < s1; i += EXACT_WG) {
             c64 p;
             double w;
             if (!load(i, p, w)) continue;
@@ -1119,6 +1135,33 @@ struct ExactChi2 {
     }
 };
 
+// Series k's column, FC source and sample range; a windowed series counts its own valid
+// samples (N of demodulateall on that window's state[I]).
+template <class F>
+__device__ __forceinline__ void setup_exact(F &f, const Problem &pb, long long k,
+                                            const c64 *__restrict__ phbuf, double *lds,
+                                            double nvalid_all) {
+    const Span sp = span_of(pb, k);
+    f.pb = &pb;
+    f.d = pb.d + sp.col * pb.ldd;
+    const long long g = pb.fcop[sp.col];
+    f.src = phbuf ? phbuf + g * pb.N : pb.fc + g * pb.ldfc;
+    f.lds = lds;
+    f.s0 = sp.s0;
+    f.s1 = sp.s1;
+    if (pb.win > 0) {
+        double c[1] = {0.0};
+        for (long long i = sp.s0 + threadIdx.x; i < sp.s1; i += EXACT_WG) {
+            int st;
+            if (sample_valid(pb, i, st)) c[0] += 1.0;
+        }
+        block_sum<EXACT_WG, 1>(c, lds);
+        f.nvalid = c[0];
+    } else {
+        f.nvalid = nvalid_all;
+    }
+}
+
 template <bool FAINT, bool OFFS, bool PHBUF>
 __global__ __launch_bounds__(EXACT_WG) void k_fit_exact(Problem pb, const Info *__restrict__ info,
                                                         const c64 *__restrict__ phbuf,
@@ -1133,12 +1176,7 @@ __global__ __launch_bounds__(EXACT_WG) void k_fit_exact(Problem pb, const Info *
     for (long long idx = blockIdx.x; idx < total; idx += gridDim.x) {
         const long long k = list ? (long long)list[idx] : idx;
         ExactChi2<FAINT, OFFS, PHBUF> f;
-        f.pb = &pb;
-        f.d = pb.d + k * pb.ldd;
-        const long long g = pb.fcop[k];
-        f.src = PHBUF ? phbuf + g * pb.N : pb.fc + g * pb.ldfc;
-        f.lds = lds;
-        f.nvalid = nvalid;
+        setup_exact(f, pb, k, PHBUF ? phbuf : nullptr, lds, nvalid);
         if (FAINT) {
 #pragma unroll
             for (int q = 0; q < 5; ++q) {
@@ -1170,12 +1208,7 @@ __global__ __launch_bounds__(EXACT_WG) void k_chi2_exact(Problem pb, const Info 
     __shared__ double lds[(EXACT_WG / 64) * 8];
     const long long k = blockIdx.x;
     ExactChi2<FAINT, OFFS, PHBUF> f;
-    f.pb = &pb;
-    f.d = pb.d + k * pb.ldd;
-    const long long g = pb.fcop[k];
-    f.src = PHBUF ? phbuf + g * pb.N : pb.fc + g * pb.ldfc;
-    f.lds = lds;
-    f.nvalid = (double)info->nvalid;
+    setup_exact(f, pb, k, PHBUF ? phbuf : nullptr, lds, (double)info->nvalid);
     if (FAINT) {
 #pragma unroll
         for (int q = 0; q < 5; ++q) {
@@ -1241,14 +1274,16 @@ __global__ __launch_bounds__(256) void k_output(Problem pb, const Param *__restr
                                                 const double *__restrict__ raw,
                                                 c64 *__restrict__ outd, long long ldo) {
     const long long k = blockIdx.y;
+    const Span sp = span_of(pb, k);
     const Param pk = par[k];
     const double b = raw[2 * k], phi = raw[2 * k + 1];
     const double arga = atan2(pk.a_im, pk.a_re);
     const c64 aa = {pk.a_re, pk.a_im};
     const bool offs = (pb.flags & F_OFFSETS) != 0;
-    const c64 *d = pb.d + k * pb.ldd;
-    c64 *o = outd + k * ldo;
-    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < pb.N; i += (long long)gridDim.x * 256) {
+    const c64 *d = pb.d + sp.col * pb.ldd;
+    c64 *o = outd + sp.col * ldo;
+    for (long long i = sp.s0 + (long long)blockIdx.x * 256 + threadIdx.x; i < sp.s1;
+         i += (long long)gridDim.x * 256) {
         double th = pb.omega * pb.t[i];
         th = th + phi;
         c64 dd = d[i];

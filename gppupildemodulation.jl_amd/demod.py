@@ -243,3 +243,92 @@ def demodulateall(timestamp, data, *, init="auto", recenter=True, faintparam=Non
             param.append(ModulationNoOffsets(complex(p["a"]), float(p["b"]), float(p["phi"])))
     likelihood = params["chi2"].copy()
     return output, param, likelihood
+
+
+def fit_windows(t, d, fc, fc_of_col, nwindow, *, state=None, omega=M_2PI, xinit=None,
+                recenter=True, fitoffsets=False, onlyhigh=False, maxfun=60, want_output=False,
+                n_gpus=1):
+    """Every window of `nwindow` samples (Iterators.partition, the last one shorter) fitted as its
+    own demodulateall call (src/GPPupilDemodulation.jl:204-205), all windows in one GPU call.
+
+    t: (N,); d: (C, N) complex (row k = column k); fc: (G, N) raw FC rows; fc_of_col: (C,).
+    Returns params shaped (n_windows, C) (and the (C, N) demodulated rows when want_output)."""
+    L = load()
+    t = np.ascontiguousarray(t, dtype=np.float64)
+    d = np.ascontiguousarray(d, dtype=np.complex128)
+    fc = np.ascontiguousarray(fc, dtype=np.complex128)
+    fop = np.ascontiguousarray(fc_of_col, dtype=np.int32)
+    if d.ndim != 2 or fc.ndim != 2 or d.shape[1] != t.size or fc.shape[1] != t.size:
+        raise ValueError("voltage and time must have the same number of lines")
+    C, N = d.shape
+    nwindow = int(nwindow)
+    if nwindow < 1:
+        raise ValueError("window must span at least one sample")
+    if fop.shape != (C,):
+        raise ValueError("fc_of_col must have one entry per column")
+    st = None if state is None else np.ascontiguousarray(state, dtype=np.int8)
+    if st is not None and st.shape != (N,):
+        raise ValueError("state and time must have the same number of lines")
+    xi = None if xinit is None else np.ascontiguousarray(xinit, dtype=np.float64).reshape(2)
+    flags = GPD_METHOD_EXACT | (GPD_RECENTER if recenter else 0) | \
+        (GPD_FIT_OFFSETS if fitoffsets else 0) | (GPD_ONLY_HIGH if onlyhigh else 0)
+    nwin = -(-N // nwindow)
+    params = np.zeros(nwin * C, dtype=PARAM_DTYPE)
+    out = np.zeros((C, N), dtype=np.complex128) if want_output else None
+    err = ctypes.create_string_buffer(512)
+    rc = L.gpd_fit_windows(N, nwindow, C, ptr(t), ptr(d), N, ptr(fc), fc.shape[0], N, ptr(fop),
+                           ptr(st), float(omega), ptr(xi), flags, int(maxfun), ptr(params),
+                           ptr(out), N, int(n_gpus), err, len(err))
+    check(rc, err)
+    params = params.reshape(nwin, C)
+    return (params, out) if want_output else params
+
+
+def window_length(timestamp, window):
+    """nwindow = round(Int, window / (times[2] - times[1])) (src/GPPupilDemodulation.jl:191)."""
+    t = np.asarray(timestamp, dtype=np.float64)
+    return int(round(window / (t[1] - t[0])))
+
+
+def demodulate_windows(timestamp, data, window, *, faintparam=None, onlyhigh=False,
+                       fitoffsets=False, preswitchdelay=0.01, postwitchdelay=0.3, n_gpus=1):
+    """processmetrology's windowed branch (src/GPPupilDemodulation.jl:191-225) on the GPU:
+    window (seconds) → nwindow samples; every window demodulated with its own fit.
+
+    Returns (output (N, 40), params (n_windows, 32) records, tables) where tables holds the
+    per-sample Float32 parameter columns ABSA, ARGA, B, PHI (and X0, Y0 with fitoffsets),
+    each (32, N) in idx() order, as the reference writes them (:209-224, :239-244)."""
+    t = np.asarray(timestamp, dtype=np.float64)
+    data = np.asarray(data).astype(np.complex128, copy=False)
+    if data.ndim != 2 or data.shape[1] != 40 or data.shape[0] != t.size:
+        raise ValueError("data must be N×40 with one row per timestamp")
+    N = t.size
+    nwindow = window_length(t, window)
+    state = None
+    if faintparam is not None:
+        state = buildstates(faintparam, t, preswitchdelay=preswitchdelay,
+                            postwitchdelay=postwitchdelay) \
+            if isinstance(faintparam, FaintStates) else np.asarray(faintparam, dtype=np.int8)
+    cols = np.ascontiguousarray(data.T)
+    fop = np.array([fc_column_of(c) - 1 for c in range(1, 33)], dtype=np.int32)
+    params, out = fit_windows(t, cols[:32], cols, fop, nwindow, state=state, fitoffsets=fitoffsets,
+                              onlyhigh=onlyhigh, want_output=True, n_gpus=n_gpus)
+    output = data.copy()
+    output[:, :32] = out.T
+    return output, params, window_tables(params, N, nwindow, fitoffsets=fitoffsets)
+
+
+def window_tables(params, n_samples, nwindow, *, fitoffsets=False):
+    """Broadcast per-window parameters to per-sample Float32 columns (32, N)
+    (src/GPPupilDemodulation.jl:209-224; b ≥ 0 already, :427-430 normalised it)."""
+    nwin, C = params.shape
+    rows = np.minimum(np.arange(n_samples) // nwindow, nwin - 1)
+    per = params[rows].T  # (C, N)
+    tables = {"ABSA": np.abs(per["a"]).astype(np.float32),
+              "ARGA": np.angle(per["a"]).astype(np.float32),
+              "B": per["b"].astype(np.float32),
+              "PHI": per["phi"].astype(np.float32)}
+    if fitoffsets:
+        tables["X0"] = per["c"].real.astype(np.float32)
+        tables["Y0"] = per["c"].imag.astype(np.float32)
+    return tables

@@ -141,6 +141,31 @@ int gpd_chi2_batch_dev(int64_t n_samples, int64_t n_pixels, const double *t, con
                        void *stream, char *errbuf, size_t errlen);
 
 /*
+ * Windowed demodulation (processmetrology with `window`, src/GPPupilDemodulation.jl:191-205):
+ * the samples are partitioned into consecutive windows of `window` samples (the last one
+ * shorter, Iterators.partition) and every window is fitted as its own demodulateall call —
+ * one call here covers all windows × columns.  d/fc/t/state/out_demod are the whole-exposure
+ * arrays (as gpd_fit_batch, n_cols series columns); out_params has ceil(n_samples/window) ×
+ * n_cols records, window-major (record w·n_cols + k = column k of window w); out_demod rows of
+ * window w are demodulated with that window's parameters.  Per-window state statistics
+ * (compute_mean_var_power on state[I]) and valid-sample counts follow the reference.  The
+ * windows are fitted by the exact evaluator; METHOD_HARMONIC is rejected.  n_gpus > 1 splits
+ * the windows across devices.
+ */
+int gpd_fit_windows(int64_t n_samples, int64_t window, int64_t n_cols, const double *t,
+                    const gpd_c64 *d, int64_t ldd, const gpd_c64 *fc, int64_t n_fc, int64_t ldfc,
+                    const int32_t *fc_of_col, const int8_t *state, double omega,
+                    const double *xinit, uint32_t flags, int32_t maxfun, gpd_param *out_params,
+                    gpd_c64 *out_demod, int64_t ldo, int32_t n_gpus, char *errbuf, size_t errlen);
+
+int gpd_fit_windows_dev(int64_t n_samples, int64_t window, int64_t n_cols, const double *t,
+                        const gpd_c64 *d, int64_t ldd, const gpd_c64 *fc, int64_t n_fc,
+                        int64_t ldfc, const int32_t *fc_of_col, const int8_t *state, double omega,
+                        const double *xinit, uint32_t flags, int32_t maxfun,
+                        gpd_param *out_params, gpd_c64 *out_demod, int64_t ldo, int device,
+                        void *stream, char *errbuf, size_t errlen);
+
+/*
  * buildstates (src/Faint.jl:21-73): two-timer faint state machine on the host.
  * timer1 = HIGH switch times, timer2 = LOW switch times (FaintStates already orders them by
  * voltage, src/Faint.jl:12-19), both already shifted by lag·timestep.  Writes MetState codes.

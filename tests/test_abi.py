@@ -54,6 +54,34 @@ def test_invalid_arguments_rejected_before_device(gpd):
         gpd.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], method="fast")
 
 
+def test_window_arguments_rejected(gpd):
+    B = synth.make_batch(100, 4, seed=1)
+    L = gpd.load()
+    err = ctypes.create_string_buffer(512)
+    par = np.zeros(4, dtype=gpd.PARAM_DTYPE)
+    t, d, fc = (np.ascontiguousarray(B[k]) for k in ("t", "d", "fc"))
+    fop = np.ascontiguousarray(B["fc_of_pixel"], dtype=np.int32)
+    for window, flags in ((0, 0), (-5, 0), (10, gpd.GPD_METHOD_HARMONIC)):
+        rc = L.gpd_fit_windows(100, window, 4, t.ctypes.data, d.ctypes.data, 100, fc.ctypes.data,
+                               fc.shape[0], 100, fop.ctypes.data, None, gpd.M_2PI, None, flags,
+                               60, par.ctypes.data, None, 100, 1, err, len(err))
+        assert rc == -1, (window, flags)
+    with pytest.raises(ValueError):
+        gpd.fit_windows(B["t"], B["d"], B["fc"], B["fc_of_pixel"], 0)
+
+
+def test_window_tables_broadcast(gpd):
+    """Per-window records → per-sample Float32 columns (src/GPPupilDemodulation.jl:209-224)."""
+    P = np.zeros((3, 2), dtype=gpd.PARAM_DTYPE)
+    P["b"] = [[1, 2], [3, 4], [5, 6]]
+    P["a"] = [[1j, 1], [2, 2j], [-1, 3]]
+    tab = gpd.window_tables(P, 25, 10)
+    assert tab["B"].shape == (2, 25) and tab["B"].dtype == np.float32
+    np.testing.assert_array_equal(tab["B"][0], [1] * 10 + [3] * 10 + [5] * 5)
+    np.testing.assert_allclose(tab["ARGA"][1, 12], np.pi / 2, rtol=1e-6)
+    assert gpd.window_length(np.arange(10) * 0.002, 1.0) == 500
+
+
 def test_no_device_is_a_loud_error(gpd):
     if not _no_gpu(gpd):
         pytest.skip("a HIP device is visible")

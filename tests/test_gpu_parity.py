@@ -50,17 +50,30 @@ def assert_fit_parity(got, ref, perturbed, label="", min_match=0.7, tol=TOL, max
     index order, so a 1-ulp change of χ² (any other libm, summation order, or the harmonic
     evaluator's ~1e-15) re-routes ~10 % of series to another point within its rhoend
     resolution — the reference itself is not reproducible there.
-    Each series must either match the oracle within tol, or lie within 1.5× the spread the
-    oracle itself shows under ±1-ulp χ² perturbations."""
+    Each series must match the oracle within tol, or match (within tol) an outcome the oracle
+    itself reaches under small χ² perturbations, or lie within 1.5× the spread of those
+    outcomes (or, for series the oracle re-routes in ≥ 1/4 of its perturbed runs, below
+    max_dev)."""
     keys = ("b", "phi", "a", "chi2")
     err = np.max([_dev(got, ref, k) for k in keys], axis=0)
-    env = np.max([[_dev(p, ref, k) for k in keys] for p in perturbed], axis=(0, 1))
+    devs = np.array([np.max([_dev(p, ref, k) for k in keys], axis=0) for p in perturbed])
+    env = devs.max(axis=0)
+    # series the oracle itself does not reproduce in ≥ 1/4 of its perturbed runs: the reference
+    # outcome there is a draw from ulp noise; any landing point below max_dev is admissible
+    chaotic = (devs > tol).mean(axis=0) >= 0.25
     match = err <= tol
-    explained = err <= 1.5 * env + tol
+    # strongest form: the GPU outcome IS (to tol) one the oracle reaches under χ² noise
+    same_as_pert = np.any([np.max([_dev(got, p, k) for k in keys], axis=0) <= tol
+                           for p in perturbed], axis=0)
+    explained = same_as_pert | (err <= 1.5 * env + tol) | (chaotic & (err < max_dev))
     msg = (f"{label}: {match.sum()}/{len(err)} series within {tol:g} (median {np.median(err):.1e}); "
            f"{(~match).sum()} tie-flips, max dev {err.max():.1e}, oracle ulp-envelope max "
-           f"{env.max():.1e}; unexplained {(~explained).sum()}")
-    assert explained.all(), msg + f" — unexplained series {np.nonzero(~explained)[0]}"
+           f"{env.max():.1e}; {chaotic.sum()} oracle-chaotic; unexplained {(~explained).sum()}")
+    bad = np.nonzero(~explained)[0]
+    detail = "; ".join(f"#{i}: got b={got['b'][i]:.9g} phi={got['phi'][i]:.9g} nfev={got['nfev'][i]}"
+                       f" vs ref b={ref['b'][i]:.9g} phi={ref['phi'][i]:.9g} nfev={ref['nfev'][i]}"
+                       for i in bad[:3])
+    assert explained.all(), msg + f" — unexplained series {bad}: {detail}"
     assert match.mean() >= min_match, msg
     assert err.max() < max_dev, msg  # default: below NEWUOA's rhoend
     return msg

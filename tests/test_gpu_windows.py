@@ -1,0 +1,106 @@
+"""GPU parity of the windowed batch (processmetrology `window`, src/GPPupilDemodulation.jl:191-225):
+every window of every diode against the oracle run on that window's slice — exactly what the
+reference does, one demodulateall(times[I], cmplxV[I,:]; state[I]) per window (:204-205)."""
+import numpy as np
+import pytest
+
+import synth
+from test_gpu_parity import assert_fit_parity, faint_states
+
+NPERTURB = 24  # short windows: more outcomes per series to sample
+
+pytestmark = pytest.mark.gpu
+
+
+def exposure(N, seed):
+    B = synth.make_batch(N, 32, seed=seed)
+    return B
+
+
+def oracle_windows(oracle, B, nwindow, fop_rows, state=None, flags=None, ulps=1.0, **kw):
+    """Oracle per window; returns params (n_windows, C) and perturbed runs of the same shape."""
+    N = B["t"].size
+    flags = oracle.RECENTER if flags is None else flags
+    ref, pert = [], [[] for _ in range(NPERTURB)]
+    for s0 in range(0, N, nwindow):
+        I = slice(s0, min(N, s0 + nwindow))
+        st = None if state is None else state[I]
+        args = (B["t"][I], B["d"][:, I], B["fc"][:, I], fop_rows)
+        ref.append(oracle.fit_batch(*args, state=st, flags=flags, **kw))
+        for j in range(NPERTURB):
+            pert[j].append(oracle.fit_batch(*args, state=st, flags=flags, perturb_seed=j + 1,
+                                            perturb_ulps=ulps, **kw))
+    return np.stack(ref), [np.stack(p) for p in pert]
+
+
+@pytest.mark.parametrize("N,nwindow", [(12000, 1500), (12345, 1500), (4000, 4000)])
+def test_windows_match_oracle(gpu, oracle, N, nwindow):
+    B = exposure(N, seed=5)
+    got, out = gpu.fit_windows(B["t"], B["d"], B["fc"], B["fc_of_pixel"], nwindow,
+                               want_output=True)
+    ref, pert = oracle_windows(oracle, B, nwindow, B["fc_of_pixel"])
+    assert got.shape == ref.shape == (-(-N // nwindow), 32)
+    assert np.all(got["status"] & gpu.GPD_ST_EXACT)
+    print(assert_fit_parity(got.reshape(-1), ref.reshape(-1), [p.reshape(-1) for p in pert],
+                            label=f"windows N={N} w={nwindow}"))
+    # output rows of window w use window w's parameters (src/GPPupilDemodulation.jl:207)
+    for w in range(ref.shape[0]):
+        I = slice(w * nwindow, min(N, (w + 1) * nwindow))
+        _, refout = oracle.fit_batch(B["t"][I], B["d"][:, I], B["fc"][:, I], B["fc_of_pixel"],
+                                     want_output=True)
+        same = np.abs(got["b"][w] - ref["b"][w]) <= 1e-10 * ref["b"][w]
+        assert np.max(np.abs(out[same][:, I] - refout[same])) <= 1e-9 * np.abs(B["d"]).max()
+
+
+@pytest.mark.parametrize("onlyhigh", [False, True])
+def test_windows_faint(gpu, oracle, onlyhigh):
+    """Per-window compute_mean_var_power on state[I] (faint mode, :205)."""
+    N, nwindow = 9000, 3000
+    B = exposure(N, seed=23)
+    st = faint_states(N, seed=3)
+    power = np.where(st == 3, 1.1, np.where(st == 1, 0.3, 0.6))
+    B["d"] = B["d"] * power[None, :]
+    got = gpu.fit_windows(B["t"], B["d"], B["fc"], B["fc_of_pixel"], nwindow, state=st,
+                          onlyhigh=onlyhigh)
+    flags = oracle.RECENTER | (oracle.ONLY_HIGH if onlyhigh else 0)
+    ref, pert = oracle_windows(oracle, B, nwindow, B["fc_of_pixel"], state=st, flags=flags)
+    print(assert_fit_parity(got.reshape(-1), ref.reshape(-1), [p.reshape(-1) for p in pert],
+                            label=f"faint windows onlyhigh={onlyhigh}"))
+
+
+def test_windows_offsets_and_multi_gpu_split(gpu, oracle):
+    N, nwindow = 6000, 1000
+    B = synth.make_batch(N, 32, seed=9, offsets=True)
+    got = gpu.fit_windows(B["t"], B["d"], B["fc"], B["fc_of_pixel"], nwindow, fitoffsets=True,
+                          n_gpus=8)  # clamps to the visible devices
+    # the offsets χ² (2×2 Cramer solve, src/Modulation.jl:189-192) matches the oracle to ≤ 2 ulp
+    # (test_chi2_evaluation_parity); short windows make its landscape flat, so the envelope
+    # perturbs by up to 4 ulp
+    ref, pert = oracle_windows(oracle, B, nwindow, B["fc_of_pixel"],
+                               flags=oracle.RECENTER | oracle.FIT_OFFSETS, ulps=4.0)
+    # 1000-sample windows with offsets: the oracle re-routes ~30 % of series under its own
+    # ulp noise, so the strict-match floor is lowered accordingly
+    print(assert_fit_parity(got.reshape(-1), ref.reshape(-1), [p.reshape(-1) for p in pert],
+                            label="offsets windows", min_match=0.5))
+
+
+def test_demodulate_windows_api(gpu, oracle):
+    """The 40-column exposure API: output, per-window records and the Float32 tables."""
+    N = 5000
+    B = exposure(N, seed=42)
+    data = np.empty((N, 40), dtype=np.complex128)
+    data[:, :32] = B["d"].T
+    fop = np.array([gpu.fc_column_of(c) - 1 for c in range(1, 33)])
+    for g in range(8):
+        cols = np.nonzero(fop == 32 + g)[0]
+        data[:, 32 + g] = B["fc"][B["fc_of_pixel"][cols[0]]]
+    window_s = 2.0  # 1000 samples at 500 Hz
+    output, params, tables = gpu.demodulate_windows(B["t"], data, window_s)
+    nw = gpu.window_length(B["t"], window_s)
+    assert nw == 1000 and params.shape == (5, 32)
+    np.testing.assert_array_equal(output[:, 32:], data[:, 32:])
+    assert tables["B"].shape == (32, N)
+    np.testing.assert_array_equal(tables["B"][:, 1500], params["b"][1].astype(np.float32))
+    ref0 = oracle.fit_batch(B["t"][:nw], data[:nw, :32].T, data[:nw].T, fop)
+    ok = np.abs(params["b"][0] - ref0["b"]) <= 1e-10 * ref0["b"]
+    assert ok.mean() >= 0.7
