@@ -17,8 +17,8 @@ from ._lib import (GPD_FIT_OFFSETS, GPD_METHOD_EXACT, GPD_METHOD_HARMONIC, GPD_O
                    GPD_ST_REFIT, PARAM_DTYPE, GpdError, load, timings)
 from .demod import (M_2PI, Diode, FaintStates, MetState, ModulationNoOffsets,
                     ModulationWithOffsets, Side, buildstates, chi2_batch, demodulate_windows,
-                    demodulateall, fc_column_of, fit_batch, fit_windows, idx, window_length,
-                    window_tables)
+                    demodulateall, fc_column_of, fit_batch, fit_windows, idx, process_volt,
+                    read_stefan_file, window_length, window_tables)
 
 __all__ = [
     "GPD_FIT_OFFSETS", "GPD_METHOD_EXACT", "GPD_METHOD_HARMONIC", "GPD_ONLY_HIGH", "GPD_RECENTER",
@@ -26,5 +26,5 @@ __all__ = [
     "PARAM_DTYPE", "GpdError", "load", "timings", "M_2PI", "Diode", "FaintStates", "MetState",
     "ModulationNoOffsets", "ModulationWithOffsets", "Side", "buildstates", "chi2_batch",
     "demodulate_windows", "demodulateall", "fc_column_of", "fit_batch", "fit_windows", "idx",
-    "window_length", "window_tables",
+    "window_length", "window_tables", "process_volt", "read_stefan_file",
 ]

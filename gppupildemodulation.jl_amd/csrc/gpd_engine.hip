@@ -638,6 +638,106 @@ int gpd_fit_windows(int64_t n_samples, int64_t window, int64_t n_cols, const dou
                       errlen, window);
 }
 
+int gpd_process_volt(int64_t n_samples, const double *t, const float *volt, int64_t ldv,
+                     const gpd_c64 *centers, const int8_t *state, double omega,
+                     const double *xinit, uint32_t flags, int32_t maxfun, int64_t window,
+                     gpd_param *out_params, float *out_volt, int64_t ldov, int device,
+                     char *errbuf, size_t errlen) {
+    // processmetrology's numeric core (src/GPPupilDemodulation.jl:147-171, 191-207) on one
+    // device: Float32 VOLT rows → centred complex128 columns → demodulateall (or every window)
+    // → demodulated Float32 VOLT rows.  Column c < 32 uses FC column 32 + c/4 (idx(), :388).
+    const int64_t N = n_samples;
+    if (N < 2 || !t || !volt || ldv < 80 || !out_params || (out_volt && ldov < 80) || window < 0 ||
+        (window > 0 && (flags & GPD_METHOD_HARMONIC))) {
+        set_err(errbuf, errlen, "gpd_process_volt: invalid shapes/pointers");
+        return GPD_E_ARG;
+    }
+    const int ndev = gpd_device_count();
+    if (ndev <= 0) {
+        set_err(errbuf, errlen, "gpd_process_volt: no HIP device visible");
+        return GPD_E_NODEV;
+    }
+    if (device < 0 || device >= ndev) {
+        set_err(errbuf, errlen, "gpd_process_volt: device %d out of range", device);
+        return GPD_E_ARG;
+    }
+    HIP_TRY(hipSetDevice(device));
+    const int64_t nrec = 32 * (window > 0 ? (N + window - 1) / window : 1);
+    double *dt = nullptr;
+    float *dv = nullptr, *dov = nullptr;
+    c64 *dcen = nullptr, *dcplx = nullptr, *dout = nullptr;
+    int8_t *dst = nullptr;
+    int32_t *dfcop = nullptr;
+    Param *dpar = nullptr;
+    hipStream_t s = nullptr;
+    auto cleanup = [&]() {
+        if (s) (void)hipStreamDestroy(s);
+        (void)hipFree(dt);
+        (void)hipFree(dv);
+        (void)hipFree(dov);
+        (void)hipFree(dcen);
+        (void)hipFree(dcplx);
+        (void)hipFree(dout);
+        (void)hipFree(dst);
+        (void)hipFree(dfcop);
+        (void)hipFree(dpar);
+    };
+    auto chk = [&](hipError_t e, const char *what) {
+        if (e != hipSuccess) {
+            set_err(errbuf, errlen, "gpd_process_volt: %s: %s", what, hipGetErrorString(e));
+            return false;
+        }
+        return true;
+    };
+    int32_t fcop[32];
+    for (int c = 0; c < 32; ++c) fcop[c] = c / 4;  // idx(side, tel, FC) - 33 for diode column c
+    bool ok = chk(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "stream") &&
+              chk(hipMalloc(&dt, N * sizeof(double)), "malloc t") &&
+              chk(hipMalloc(&dv, (size_t)N * 80 * sizeof(float)), "malloc volt") &&
+              chk(hipMalloc(&dcplx, (size_t)40 * N * sizeof(c64)), "malloc columns") &&
+              chk(hipMalloc(&dfcop, 32 * sizeof(int32_t)), "malloc fcop") &&
+              chk(hipMalloc(&dpar, nrec * sizeof(Param)), "malloc params") &&
+              (!centers || chk(hipMalloc(&dcen, 40 * sizeof(c64)), "malloc centres")) &&
+              (!state || chk(hipMalloc(&dst, N), "malloc state")) &&
+              (!out_volt || (chk(hipMalloc(&dout, (size_t)32 * N * sizeof(c64)), "malloc out") &&
+                             chk(hipMalloc(&dov, (size_t)N * 80 * sizeof(float)), "malloc out volt")));
+    if (!ok) {
+        cleanup();
+        (void)hipGetLastError();
+        return GPD_E_OOM;
+    }
+    ok = chk(hipMemcpyAsync(dt, t, N * sizeof(double), hipMemcpyHostToDevice, s), "H2D t") &&
+         chk(hipMemcpy2DAsync(dv, 80 * sizeof(float), volt, ldv * sizeof(float), 80 * sizeof(float),
+                              N, hipMemcpyHostToDevice, s), "H2D volt") &&
+         chk(hipMemcpyAsync(dfcop, fcop, sizeof fcop, hipMemcpyHostToDevice, s), "H2D fcop") &&
+         (!centers || chk(hipMemcpyAsync(dcen, centers, 40 * sizeof(c64), hipMemcpyHostToDevice, s),
+                          "H2D centres")) &&
+         (!state || chk(hipMemcpyAsync(dst, state, N, hipMemcpyHostToDevice, s), "H2D state"));
+    if (!ok) {
+        cleanup();
+        return GPD_E_HIP;
+    }
+    const unsigned tiles = (unsigned)((N + VT_ROWS - 1) / VT_ROWS);
+    k_volt_ingest<<<tiles, 256, 0, s>>>(N, dv, 80, dcen, dcplx, N);
+    int r = pipeline_dev(N, 32, dt, (const gpd_c64 *)dcplx, N, (const gpd_c64 *)(dcplx + 32 * N), 8,
+                         N, dfcop, dst, omega, xinit, flags, maxfun, (gpd_param *)dpar,
+                         (gpd_c64 *)dout, N, nullptr, device, s, errbuf, errlen, window);
+    if (r != GPD_OK) {
+        cleanup();
+        return r;
+    }
+    if (out_volt) k_volt_egress<<<tiles, 256, 0, s>>>(N, dout, dcplx, N, dov, 80);
+    ok = chk(hipGetLastError(), "launch") &&
+         chk(hipMemcpyAsync(out_params, dpar, nrec * sizeof(Param), hipMemcpyDeviceToHost, s),
+             "D2H params") &&
+         (!out_volt || chk(hipMemcpy2DAsync(out_volt, ldov * sizeof(float), dov, 80 * sizeof(float),
+                                            80 * sizeof(float), N, hipMemcpyDeviceToHost, s),
+                           "D2H volt")) &&
+         chk(hipStreamSynchronize(s), "synchronize");
+    cleanup();
+    return ok ? GPD_OK : GPD_E_HIP;
+}
+
 int gpd_synth_fill_dev(int64_t n_samples, int64_t n_pixels, int64_t pixel_offset, uint64_t seed,
                        double t0, double dt, double sigma, int with_offsets, double omega,
                        double *t, gpd_c64 *d, int64_t ldd, gpd_c64 *fc, int64_t ldfc,

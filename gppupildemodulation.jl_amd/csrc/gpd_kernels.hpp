@@ -1383,4 +1383,55 @@ __global__ __launch_bounds__(256) void k_synth_t(long long N, double t0, double 
     if (i < N) t[i] = t0 + (double)i * dt;
 }
 
+// ---------------------------------------------------------------------------------------
+// VOLT ingest / egress (processmetrology, src/GPPupilDemodulation.jl:147-157, 164-171): the FITS
+// table rows are Float32 [re1 im1 … re40 im40]; the fit wants complex128 columns (Julia
+// Matrix{ComplexF64} N×40) with the centre of each column subtracted.  64-row tiles through LDS:
+// row-major coalesced reads, column-major coalesced writes (and the reverse for egress).
+constexpr int VT_ROWS = 64;
+
+__global__ __launch_bounds__(256) void k_volt_ingest(long long N, const float *__restrict__ volt,
+                                                     long long ldv, const c64 *__restrict__ centers,
+                                                     c64 *__restrict__ out, long long ldo) {
+    __shared__ float tile[VT_ROWS][81];
+    const long long r0 = (long long)blockIdx.x * VT_ROWS;
+    const int nr = (int)((N - r0) < VT_ROWS ? (N - r0) : VT_ROWS);
+    for (int e = threadIdx.x; e < VT_ROWS * 80; e += 256) {
+        const int r = e / 80, c = e - r * 80;
+        tile[r][c] = r < nr ? volt[(r0 + r) * ldv + c] : 0.f;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 40 * VT_ROWS; e += 256) {
+        const int k = e / VT_ROWS, r = e - k * VT_ROWS;
+        if (r >= nr) continue;
+        c64 z = {(double)tile[r][2 * k], (double)tile[r][2 * k + 1]};  // Float64.(VOLT)
+        if (centers) {  // cmplxV .-= reshape(offsets, 1, 40)
+            z.re = z.re - centers[k].re;
+            z.im = z.im - centers[k].im;
+        }
+        out[k * ldo + r0 + r] = z;
+    }
+}
+
+// Demodulated columns 0..31 (dem, ld) + the (centred) FC columns 32..39 (src, ld) → Float32 rows.
+__global__ __launch_bounds__(256) void k_volt_egress(long long N, const c64 *__restrict__ dem,
+                                                     const c64 *__restrict__ src, long long ld,
+                                                     float *__restrict__ outv, long long ldov) {
+    __shared__ float tile[VT_ROWS][81];
+    const long long r0 = (long long)blockIdx.x * VT_ROWS;
+    const int nr = (int)((N - r0) < VT_ROWS ? (N - r0) : VT_ROWS);
+    for (int e = threadIdx.x; e < 40 * VT_ROWS; e += 256) {
+        const int k = e / VT_ROWS, r = e - k * VT_ROWS;
+        if (r >= nr) continue;
+        const c64 z = k < 32 ? dem[k * ld + r0 + r] : src[k * ld + r0 + r];
+        tile[r][2 * k] = (float)z.re;  // Float32.(volt) after volt[1:2:end,:] .= real(output)'
+        tile[r][2 * k + 1] = (float)z.im;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < VT_ROWS * 80; e += 256) {
+        const int r = e / 80, c = e - r * 80;
+        if (r < nr) outv[(r0 + r) * ldov + c] = tile[r][c];
+    }
+}
+
 }  // namespace gpd

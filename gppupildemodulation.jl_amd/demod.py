@@ -332,3 +332,70 @@ def window_tables(params, n_samples, nwindow, *, fitoffsets=False):
         tables["X0"] = per["c"].real.astype(np.float32)
         tables["Y0"] = per["c"].imag.astype(np.float32)
     return tables
+
+
+def read_stefan_file(filename):
+    """Column centres from a Stefan calibration file (src/GPPupilDemodulation.jl:84-104): every
+    `avg` row names (side, telescope, diode) and gives VX, VY in mV; centre = 1e-3·(VX + i·VY)
+    at idx(side, telescope, diode).  Returns (40,) complex128 (unset columns stay 0)."""
+    offsets = np.zeros(40, dtype=np.complex128)
+    with open(filename) as f:
+        for line in f:
+            if not line.startswith("avg"):
+                continue
+            values = line.split()
+            name = values[1]
+            side = Side[name[0:2]]
+            telescope = int(name[3])
+            diode = Diode[name[4:6]]
+            offsets[idx(side, telescope, diode) - 1] = 1e-3 * (float(values[2]) + 1j * float(values[4]))
+    return offsets
+
+
+def process_volt(timestamp, volt, *, offsets=None, window=None, faintparam=None, onlyhigh=False,
+                 preswitchdelay=0.01, postwitchdelay=0.3, init="auto", device=0):
+    """processmetrology's numeric core (src/GPPupilDemodulation.jl:137-171, 191-244) straight from
+    the FITS VOLT column on the GPU.
+
+    volt: (N, 80) float32 rows [re1 im1 … re40 im40].  offsets: (40,) complex centres subtracted
+    first (a Stefan file, read_stefan_file), False → no centring and fitoffsets (:151-157), None →
+    no centring.  window: seconds (None = one fit per diode over the exposure).
+    Returns (volt_out (N, 80) float32 demodulated rows, params, tables) — params (32,) or
+    (n_windows, 32); tables = per-sample Float32 parameter columns in window mode, else None."""
+    L = load()
+    t = np.ascontiguousarray(timestamp, dtype=np.float64)
+    v = np.ascontiguousarray(volt, dtype=np.float32)
+    if v.ndim != 2 or v.shape[1] != 80 or v.shape[0] != t.size:
+        raise ValueError("VOLT must be N×80 Float32 rows")
+    N = t.size
+    fitoffsets = offsets is False
+    if offsets is True:
+        raise NotImplementedError("compute_offsets (circle fit) is outside the hot path")
+    cen = None
+    if offsets is not None and offsets is not False:
+        cen = np.ascontiguousarray(offsets, dtype=np.complex128)
+        if cen.shape != (40,):
+            raise ValueError("offsets must hold 40 complex centres")
+    state = None
+    if faintparam is not None:
+        state = buildstates(faintparam, t, preswitchdelay=preswitchdelay,
+                            postwitchdelay=postwitchdelay) \
+            if isinstance(faintparam, FaintStates) else np.asarray(faintparam, dtype=np.int8)
+        state = np.ascontiguousarray(state, dtype=np.int8)
+    xi = None if (isinstance(init, str) and init == "auto") else \
+        np.ascontiguousarray(init, dtype=np.float64).reshape(2)
+    nwindow = 0 if window is None else window_length(t, window)
+    flags = GPD_RECENTER | (GPD_FIT_OFFSETS if fitoffsets else 0) | \
+        (GPD_ONLY_HIGH if onlyhigh else 0)
+    nrec = 32 * (-(-N // nwindow) if nwindow else 1)
+    params = np.zeros(nrec, dtype=PARAM_DTYPE)
+    out = np.zeros((N, 80), dtype=np.float32)
+    err = ctypes.create_string_buffer(512)
+    rc = L.gpd_process_volt(N, ptr(t), ptr(v), 80, ptr(cen), ptr(state), float(M_2PI), ptr(xi),
+                            flags, 60, nwindow, ptr(params), ptr(out), 80, int(device), err,
+                            len(err))
+    check(rc, err)
+    if nwindow:
+        params = params.reshape(-1, 32)
+        return out, params, window_tables(params, N, nwindow, fitoffsets=fitoffsets)
+    return out, params, None

@@ -166,6 +166,22 @@ int gpd_fit_windows_dev(int64_t n_samples, int64_t window, int64_t n_cols, const
                         void *stream, char *errbuf, size_t errlen);
 
 /*
+ * processmetrology's numeric core (src/GPPupilDemodulation.jl:147-171 and, with window > 0,
+ * 191-207) on one device, straight from the FITS VOLT column: volt = n_samples Float32 rows
+ * of 80 values [re1 im1 … re40 im40] (row pitch ldv floats, the FITS/Julia layout), centres =
+ * the 40 column centres subtracted first (`offsets` vector; NULL = none, e.g. fitoffsets), then
+ * demodulateall over the 32 diode columns (window = 0) or every window of `window` samples.
+ * out_params: 32 records (window = 0) or ceil(n_samples/window)×32, window-major.
+ * out_volt (optional, pitch ldov ≥ 80 floats): the demodulated rows in the same Float32 layout,
+ * FC columns carrying the centred input (volt[1:2:end,:] .= real(output)', Float32.(volt)).
+ */
+int gpd_process_volt(int64_t n_samples, const double *t, const float *volt, int64_t ldv,
+                     const gpd_c64 *centres, const int8_t *state, double omega,
+                     const double *xinit, uint32_t flags, int32_t maxfun, int64_t window,
+                     gpd_param *out_params, float *out_volt, int64_t ldov, int device,
+                     char *errbuf, size_t errlen);
+
+/*
  * buildstates (src/Faint.jl:21-73): two-timer faint state machine on the host.
  * timer1 = HIGH switch times, timer2 = LOW switch times (FaintStates already orders them by
  * voltage, src/Faint.jl:12-19), both already shifted by lag·timestep.  Writes MetState codes.

@@ -1,0 +1,67 @@
+"""GPU: processmetrology's numeric core straight from Float32 VOLT rows (§8f rank 3) —
+ingest (Float64.(VOLT), centring), demodulateall / windows, egress to Float32 rows."""
+import numpy as np
+import pytest
+
+import synth
+from test_gpu_parity import assert_fit_parity, perturbed_runs
+
+pytestmark = pytest.mark.gpu
+
+
+def volt_exposure(gpu, N, seed):
+    B = synth.make_batch(N, 32, seed=seed)
+    data = np.empty((N, 40), dtype=np.complex128)
+    data[:, :32] = B["d"].T
+    fop = np.array([gpu.fc_column_of(c) - 1 for c in range(1, 33)])
+    for g in range(8):
+        cols = np.nonzero(fop == 32 + g)[0]
+        data[:, 32 + g] = B["fc"][B["fc_of_pixel"][cols[0]]]
+    rng = np.random.default_rng(seed)
+    centres = 0.05 * (rng.standard_normal(40) + 1j * rng.standard_normal(40))
+    raw = data + centres[None, :]  # what the instrument records before centring
+    volt = np.empty((N, 80), dtype=np.float32)
+    volt[:, 0::2] = raw.real
+    volt[:, 1::2] = raw.imag
+    cplx = volt[:, 0::2].astype(np.float64) + 1j * volt[:, 1::2].astype(np.float64)
+    return B["t"], volt, centres, cplx - centres[None, :], fop
+
+
+def test_process_volt_matches_oracle(gpu, oracle):
+    t, volt, centres, cplx, fop = volt_exposure(gpu, 20000, seed=17)
+    out, params, tables = gpu.process_volt(t, volt, offsets=centres)
+    assert tables is None and params.shape == (32,)
+    ref, refout = oracle.fit_batch(t, cplx[:, :32].T, cplx.T, fop, want_output=True)
+    B = {"t": t, "d": np.ascontiguousarray(cplx[:, :32].T), "fc": np.ascontiguousarray(cplx.T),
+         "fc_of_pixel": fop}
+    print(assert_fit_parity(params, ref, perturbed_runs(oracle, B, ulps=128.0), label="volt"))
+    # egress: demodulated columns and centred FC columns as Float32 rows
+    fc32 = cplx[:, 32:].astype(np.complex64)
+    np.testing.assert_array_equal(out[:, 64::2], fc32.real)
+    np.testing.assert_array_equal(out[:, 65::2], fc32.imag)
+    same = np.abs(params["b"] - ref["b"]) <= 1e-10 * ref["b"]
+    got = out[:, 0:64:2].astype(np.float64) + 1j * out[:, 1:64:2]
+    ref32 = refout.T.astype(np.complex64)
+    diff = np.abs(got[:, same] - ref32[:, same])
+    assert diff.max() <= 2 * np.spacing(np.float32(np.abs(cplx).max()))  # ≤ Float32 rounding
+
+
+def test_process_volt_windows_equal_fit_windows(gpu):
+    t, volt, centres, cplx, fop = volt_exposure(gpu, 12000, seed=29)
+    out, params, tables = gpu.process_volt(t, volt, offsets=centres, window=8.0)  # 4000 samples
+    assert params.shape == (3, 32) and tables["PHI"].shape == (32, 12000)
+    fw = gpu.fit_windows(t, cplx[:, :32].T, cplx.T, fop, 4000)
+    np.testing.assert_array_equal(params["b"], fw["b"])  # same device pipeline, same inputs
+    np.testing.assert_array_equal(params["chi2"], fw["chi2"])
+
+
+def test_process_volt_fitoffsets_without_centring(gpu, oracle):
+    t, volt, centres, cplx, fop = volt_exposure(gpu, 8000, seed=31)
+    out, params, _ = gpu.process_volt(t, volt, offsets=False)  # fitoffsets, no centring (:155-157)
+    raw = volt[:, 0::2].astype(np.float64) + 1j * volt[:, 1::2].astype(np.float64)
+    ref = oracle.fit_batch(t, raw[:, :32].T, raw.T, fop, flags=oracle.RECENTER | oracle.FIT_OFFSETS)
+    B = {"t": t, "d": np.ascontiguousarray(raw[:, :32].T), "fc": np.ascontiguousarray(raw.T),
+         "fc_of_pixel": fop}
+    print(assert_fit_parity(params, ref, perturbed_runs(oracle, B, ulps=4.0, fitoffsets=True),
+                            label="volt offsets"))
+    assert np.max(np.abs(params["c"] - ref["c"])[np.abs(params["b"] - ref["b"]) <= 1e-10]) <= 1e-9

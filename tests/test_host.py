@@ -1,5 +1,7 @@
 """CPU checks of the host-side mirror (idx/Side/Diode/MetState, FaintStates, argument handling)
 and of the multi-GPU sharding helpers."""
+import os
+
 import numpy as np
 import pytest
 
@@ -57,3 +59,26 @@ def test_shard_range_partitions_whole_groups(gpd):
     assert shard.weak_offset(100_000, 3) == 300_000
     with pytest.raises(ValueError):
         shard.weak_offset(10, 1)
+
+
+def test_read_stefan_file_fixture(gpd):
+    """The reference's own calibration data (data/Stefan_file.txt, copied to tests/golden/):
+    40 `avg` rows → 40 centres at idx(side, telescope, diode) (src/GPPupilDemodulation.jl:88-104)."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "Stefan_file.txt")
+    with open(path) as f:
+        n_avg = sum(1 for line in f if line.startswith("avg"))
+    assert n_avg == 40
+    c = gpd.read_stefan_file(path)
+    assert c.shape == (40,) and np.all(c != 0)
+    k = gpd.idx(gpd.Side.FT, 1, gpd.Diode.FC) - 1  # "avg FTT1FC 0.5056591585058203 … 0.6414248583206548"
+    assert c[k] == 1e-3 * (0.5056591585058203 + 1j * 0.6414248583206548)
+    k = gpd.idx(gpd.Side.FT, 1, gpd.Diode.D1) - 1  # "avg FTT1D1 -3.9217663072871978 … -5.375368693370768"
+    assert c[k] == 1e-3 * (-3.9217663072871978 - 1j * 5.375368693370768)
+
+
+def test_process_volt_argument_checks(gpd):
+    t = np.arange(100) * 0.002
+    with pytest.raises(ValueError):
+        gpd.process_volt(t, np.zeros((100, 79), np.float32))
+    with pytest.raises(NotImplementedError):
+        gpd.process_volt(t, np.zeros((100, 80), np.float32), offsets=True)
