@@ -95,7 +95,8 @@ __device__ __forceinline__ c64 fc_phasor(c64 z) { return cisj(atan2(z.im, z.re))
 // ---------------------------------------------------------------------------------------
 // Driver shared by both evaluators (src/Modulation.jl:402-416).  F: double operator()(double(&)[2])
 template <class F>
-__device__ __forceinline__ void drive_fit(F &f, const Problem &pb, double (&x)[2], int &status) {
+__device__ __forceinline__ void drive_fit(F &f, const Problem &pb, double (&x)[2], int &status,
+                                          Newuoa<2, 5> &nw) {
     if (pb.has_xinit) {
         x[0] = pb.x0;
         x[1] = pb.x1;
@@ -117,7 +118,6 @@ __device__ __forceinline__ void drive_fit(F &f, const Problem &pb, double (&x)[2
         x[0] = 0.1;
         x[1] = g;
     }
-    Newuoa<2, 5> nw;
     double fx;
     int nf = nw.run(x, 1.0, 1e-3, pb.maxfun, f, fx);
     if (nf >= pb.maxfun) status |= ST_MAXFUN;
@@ -130,6 +130,12 @@ __device__ __forceinline__ void drive_fit(F &f, const Problem &pb, double (&x)[2
         nf = nw.run(x, 1.0, 1e-3, pb.maxfun, f, fx);
         if (nf >= pb.maxfun) status |= ST_MAXFUN;
     }
+}
+
+template <class F>
+__device__ __forceinline__ void drive_fit(F &f, const Problem &pb, double (&x)[2], int &status) {
+    Newuoa<2, 5> nw;  // per-thread state (exact path: replicated in every thread)
+    drive_fit(f, pb, x, status, nw);
 }
 
 __device__ __forceinline__ void store_param(Param *out, double *raw, long long k, double c_re,
@@ -985,6 +991,9 @@ __global__ __launch_bounds__(64) void k_fit_harmonic(Problem pb, const Info *__r
                                                      const double *__restrict__ aux,
                                                      Param *__restrict__ out, double *__restrict__ raw,
                                                      int *__restrict__ list, int *__restrict__ count) {
+    // NEWUOA state of each lane in LDS (71 doubles, odd 8-byte stride): its ~1e3 dependent
+    // accesses per iteration stay at LDS latency instead of spilling through the caches
+    __shared__ Newuoa<2, 5> nwpool[64];
     const long long k = (long long)blockIdx.x * 64 + threadIdx.x;
     if (k >= pb.P) return;
     const Info in = *info;
@@ -1008,7 +1017,7 @@ __global__ __launch_bounds__(64) void k_fit_harmonic(Problem pb, const Info *__r
     f.fallback = false;
     double x[2];
     int status = 0;
-    drive_fit(f, pb, x, status);
+    drive_fit(f, pb, x, status, nwpool[threadIdx.x]);
     const double chi2 = f(x);  // likelihood[idx] = lkl(x) (src/Modulation.jl:416)
     if (f.fallback) {
         list[atomicAdd(count, 1)] = (int)k;
