@@ -318,6 +318,20 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                 k_moments_ws<2><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
             else if (mk && std::string(mk) == "ws_mfmaonly")
                 k_moments_ws<5><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
+            else if (mk && std::string(mk) == "ws_prof") {  // cycle split per role (stderr)
+                unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_wsprof), z, sizeof z, 0,
+                                               hipMemcpyHostToDevice, stream));
+                k_moments_ws<6><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
+                HIP_TRY(hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_wsprof), sizeof z, 0,
+                                                 hipMemcpyDeviceToHost, stream));
+                HIP_TRY(hipStreamSynchronize(stream));
+                const double pw = 4.0 * g.x * g.y, cw = pw;  // waves per role
+                fprintf(stderr,
+                        "ws_prof cycles/wave: producer stage %.3g issue %.3g barrier %.3g | "
+                        "consumer mfma %.3g barrier %.3g\n",
+                        z[0] / pw, z[1] / pw, z[2] / pw, z[3] / cw, z[4] / cw);
+            }
             else
                 k_moments_ws<0><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
         } else {

@@ -644,6 +644,11 @@ __global__ __launch_bounds__(256, 2) void k_moments_mfma(Problem pb, const doubl
 //   tile: consumers on buffer i&1 while producers fill buffer (i+1)&1, so each SIMD hosts one
 //   consumer that keeps its matrix core busy and one producer whose loads and VALU work overlap
 //   it (the single-role kernel serialises staging and MFMA behind two barriers per tile).
+// DBG == 6 (diagnostics only): per-role cycle split, summed over waves
+//   [0] producer stage, [1] producer issue, [2] producer barrier, [3] consumer MFMA phase,
+//   [4] consumer barrier
+__device__ unsigned long long g_wsprof[8];
+
 template <bool B>
 struct BoolTag {
     static constexpr bool value = B;
@@ -787,6 +792,11 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
         // loader waves first: their few VALU ops and the next loads must not queue behind the
         // MFMA stream of the consumer wave on the same SIMD (fp64 MFMA and VALU share it)
         __builtin_amdgcn_s_setprio(2);
+        unsigned long long pst = 0, pis = 0, pbar = 0, tq = 0;
+        auto tick = [&]() -> unsigned long long {
+            if constexpr (DBG == 6) return __builtin_amdgcn_s_memtime();
+            return 0;
+        };
         auto run = [&](auto gen) {
             WsRegs R0, R1;
             issue(R0, 0);
@@ -801,14 +811,21 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             // the odd last iteration peeled so the loop body has no conditional loads
             int i = 0;
             for (; i + 1 < ntiles; i += 2) {
+                tq = tick();
                 stage(R1, i + 1, gen);
+                if constexpr (DBG == 6) { const auto t1 = tick(); pst += t1 - tq; tq = t1; }
                 issue_t(i + 2);
                 issue(R1, i + 3);
+                if constexpr (DBG == 6) { const auto t1 = tick(); pis += t1 - tq; tq = t1; }
                 __syncthreads();
+                if constexpr (DBG == 6) { const auto t1 = tick(); pbar += t1 - tq; tq = t1; }
                 stage(R0, i + 2, gen);
+                if constexpr (DBG == 6) { const auto t1 = tick(); pst += t1 - tq; tq = t1; }
                 issue_t(i + 3);
                 issue(R0, i + 4);
+                if constexpr (DBG == 6) { const auto t1 = tick(); pis += t1 - tq; tq = t1; }
                 __syncthreads();
+                if constexpr (DBG == 6) { const auto t1 = tick(); pbar += t1 - tq; tq = t1; }
             }
             if (i < ntiles) {
                 stage(R1, i + 1, gen);
@@ -819,6 +836,13 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             run(BoolTag<true>{});
         else
             run(BoolTag<false>{});
+        if constexpr (DBG == 6) {
+            if (lane == 0) {
+                atomicAdd(&g_wsprof[0], pst);
+                atomicAdd(&g_wsprof[1], pis);
+                atomicAdd(&g_wsprof[2], pbar);
+            }
+        }
         // the last iterations re-read the final tile; let those loads land before the wave
         // ends rather than leave them in flight past s_endpgm
         __builtin_amdgcn_s_waitcnt(0);
@@ -834,6 +858,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
 #pragma unroll
         for (int n = 0; n < 3; ++n) acc[m][n] = (v4d){0.0, 0.0, 0.0, 0.0};
     __syncthreads();  // tile 0 staged
+    unsigned long long cmf = 0, cbar = 0;  // DBG == 6 only
     // fragments of K-step ks+1 are read from LDS while the 12 MFMAs of K-step ks run
     // (register double buffer; only the first read of each tile waits on LDS latency)
     for (int i = 0; i < ntiles; ++i) {
@@ -858,6 +883,8 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
                 q2[m] = fma(a[m], a[m], q2[m]);
             }
         };
+        unsigned long long c0 = 0;
+        if constexpr (DBG == 6) c0 = __builtin_amdgcn_s_memtime();
         if constexpr (DBG != 1) {
             double a0[4], b0[3], a1[4], b1[3];
             ldfrag(0, a0, b0);
@@ -869,7 +896,14 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
                 step(a1, b1);
             }
         }
+        unsigned long long c1 = 0;
+        if constexpr (DBG == 6) {
+            // the MFMA results are consumed at the end; count issue time of the phase
+            c1 = __builtin_amdgcn_s_memtime();
+            cmf += c1 - c0;
+        }
         __syncthreads();
+        if constexpr (DBG == 6) cbar += __builtin_amdgcn_s_memtime() - c1;
     }
     double *base = part + (long long)blockIdx.y * NMOM * pb.P;
 #pragma unroll
@@ -896,6 +930,12 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
         if (fk == 0 && pix < pb.P) {
             base[(long long)comp * pb.P + pix] = f0[m];
             if (comp == 0) base[2 * pb.P + pix] = q2[m] + q2o;
+        }
+    }
+    if constexpr (DBG == 6) {
+        if (lane == 0) {
+            atomicAdd(&g_wsprof[3], cmf);
+            atomicAdd(&g_wsprof[4], cbar);
         }
     }
 }
