@@ -354,8 +354,24 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             cx->have_timers = true;
             return GPD_OK;
         }
-        k_fit_harmonic<<<(unsigned)((P + 63) / 64), 64, 0, stream>>>(pb, info, mom, aux, outp, raw,
-                                                                   list, count);
+        static const bool fit_prof = getenv("GPD_FIT_PROF") != nullptr;  // diagnostics only
+        if (fit_prof) {
+            unsigned long long z[4] = {0, 0, 0, 0};
+            HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_fitprof), z, sizeof z, 0,
+                                           hipMemcpyHostToDevice, stream));
+            Problem pp = pb;
+            pp.flags |= F_PROF;
+            k_fit_harmonic<<<(unsigned)((P + 63) / 64), 64, 0, stream>>>(pp, info, mom, aux, outp,
+                                                                       raw, list, count);
+            HIP_TRY(hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_fitprof), sizeof z, 0,
+                                             hipMemcpyDeviceToHost, stream));
+            HIP_TRY(hipStreamSynchronize(stream));
+            fprintf(stderr, "fit_prof per series: objective %.3g cycles, whole fit %.3g, evals %.3g\n",
+                    (double)z[0] / P, (double)z[1] / P, (double)z[2] / P);
+        } else {
+            k_fit_harmonic<<<(unsigned)((P + 63) / 64), 64, 0, stream>>>(pb, info, mom, aux, outp,
+                                                                       raw, list, count);
+        }
         mark("fit_harmonic");
         // fallback: series whose fit left the expansion's safe range, re-fitted exactly
         if (faint)

@@ -32,6 +32,8 @@ __device__ __constant__ const double c_phi_grid[8] = {
 // status bits (mirror include/gpdemod.h)
 constexpr int ST_REFIT = 0x1, ST_MAXFUN = 0x2, ST_NAN = 0x4, ST_EXACT = 0x8, ST_FALLBACK = 0x10;
 constexpr uint32_t F_OFFSETS = 0x1u, F_RECENTER = 0x2u, F_ONLY_HIGH = 0x4u;
+constexpr uint32_t F_PROF = 0x80000000u;  // internal: k_fit_harmonic cycle split (GPD_FIT_PROF)
+__device__ unsigned long long g_fitprof[4];  // [0] objective cycles, [1] whole-fit cycles, [2] evals
 
 struct Param {  // == gpd_param
     double c_re, c_im, a_re, a_im, b, phi, chi2;
@@ -94,9 +96,9 @@ __device__ __forceinline__ c64 fc_phasor(c64 z) { return cisj(atan2(z.im, z.re))
 
 // ---------------------------------------------------------------------------------------
 // Driver shared by both evaluators (src/Modulation.jl:402-416).  F: double operator()(double(&)[2])
-template <class F>
+template <class F, class NW>
 __device__ __forceinline__ void drive_fit(F &f, const Problem &pb, double (&x)[2], int &status,
-                                          Newuoa<2, 5> &nw) {
+                                          NW &nw) {
     if (pb.has_xinit) {
         x[0] = pb.x0;
         x[1] = pb.x1;
@@ -978,7 +980,17 @@ struct HarmChi2 {
 
     // one out-of-line copy: NEWUOA calls the objective from several sites, and each inlined
     // copy of the Bessel recurrence + 24-harmonic sum adds its own live registers
+    unsigned long long prof_cycles;
+    bool prof;
+
     __device__ __attribute__((noinline)) double operator()(const double (&x)[2]) {
+        if (!prof) return eval(x);
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        const double r = eval(x);
+        prof_cycles += __builtin_amdgcn_s_memtime() - t0;
+        return r;
+    }
+    __device__ __forceinline__ double eval(const double (&x)[2]) {
         ++nfev;
         if (fallback) return 0.0;
         const double b = x[0];
@@ -1033,7 +1045,7 @@ __global__ __launch_bounds__(64) void k_fit_harmonic(Problem pb, const Info *__r
                                                      int *__restrict__ list, int *__restrict__ count) {
     // NEWUOA state of each lane in LDS (71 doubles, odd 8-byte stride): its ~1e3 dependent
     // accesses per iteration stay at LDS latency instead of spilling through the caches
-    __shared__ Newuoa<2, 5> nwpool[64];
+    __shared__ Newuoa<2, 5, true> nwpool[64];
     const long long k = (long long)blockIdx.x * 64 + threadIdx.x;
     if (k >= pb.P) return;
     const Info in = *info;
@@ -1055,10 +1067,18 @@ __global__ __launch_bounds__(64) void k_fit_harmonic(Problem pb, const Info *__r
     f.a_re = f.a_im = 0.0;
     f.nfev = 0;
     f.fallback = false;
+    f.prof = (pb.flags & F_PROF) != 0;
+    f.prof_cycles = 0;
+    const unsigned long long tfit = f.prof ? __builtin_amdgcn_s_memtime() : 0;
     double x[2];
     int status = 0;
     drive_fit(f, pb, x, status, nwpool[threadIdx.x]);
     const double chi2 = f(x);  // likelihood[idx] = lkl(x) (src/Modulation.jl:416)
+    if (f.prof) {
+        atomicAdd(&g_fitprof[0], f.prof_cycles);
+        atomicAdd(&g_fitprof[1], __builtin_amdgcn_s_memtime() - tfit);
+        atomicAdd(&g_fitprof[2], (unsigned long long)f.nfev);
+    }
     if (f.fallback) {
         list[atomicAdd(count, 1)] = (int)k;
         return;

@@ -21,7 +21,7 @@ namespace gpd {
 #define GPD_HDN __host__ __device__
 // the large NEWUOA subroutines stay out of line: inlined into one body their temporaries
 // exceed the register file (512 VGPR+AGPR and ~1.4 KB of spills per lane)
-#define GPD_HDX __host__ __device__ __attribute__((noinline))
+#define GPD_HDX __host__ __device__
 
 // ---------------------------------------------------------------- select helpers ------
 template <int L>
@@ -67,8 +67,42 @@ GPD_HD void wrc(double (&a)[R][C], int r, int c, double v) {
 
 constexpr double kTwoPi = 6.283185307179586476925286766559;  // 8·atan(1)
 
-template <int N, int NPT>
+// DIRECT = true: the object lives in LDS (one per lane, k_fit_harmonic), so runtime indices
+// address it directly; false: per-thread objects held in registers, runtime indices become
+// select chains (no scratch).
+template <int N, int NPT, bool DIRECT = false>
 struct Newuoa {
+    template <int L>
+    GPD_HD static double rd_(const double (&a)[L], int k) {
+        if constexpr (DIRECT) return a[k];
+        else return rd(a, k);
+    }
+    template <int L>
+    GPD_HD static void wr_(double (&a)[L], int k, double v) {
+        if constexpr (DIRECT) a[k] = v;
+        else wr(a, k, v);
+    }
+    template <int R, int C>
+    GPD_HD static double rd2_(const double (&a)[R][C], int r, int c) {
+        if constexpr (DIRECT) return a[r][c];
+        else return rd2(a, r, c);
+    }
+    template <int R, int C>
+    GPD_HD static void wr2_(double (&a)[R][C], int r, int c, double v) {
+        if constexpr (DIRECT) a[r][c] = v;
+        else wr2(a, r, c, v);
+    }
+    template <int R, int C>
+    GPD_HD static double rdc_(const double (&a)[R][C], int r, int c) {
+        if constexpr (DIRECT) return a[r][c];
+        else return rdc(a, r, c);
+    }
+    template <int R, int C>
+    GPD_HD static void wrc_(double (&a)[R][C], int r, int c, double v) {
+        if constexpr (DIRECT) a[r][c] = v;
+        else wrc(a, r, c, v);
+    }
+
     static constexpr int NDIM = NPT + N;
     static constexpr int NPTM = NPT - N - 1;
     static constexpr int NH = N * (N + 1) / 2;
@@ -249,7 +283,7 @@ struct Newuoa {
         for (int k = 0; k < NPT; ++k) hcol[k] = 0.0;
 #pragma unroll
         for (int j = 0; j < NPTM; ++j) {
-            double temp = rd2(zmat, knew - 1, j);
+            double temp = rd2_(zmat, knew - 1, j);
             if (j + 1 < idz) temp = -temp;
 #pragma unroll
             for (int k = 0; k < NPT; ++k) hcol[k] = hcol[k] + temp * zmat[k][j];
@@ -262,12 +296,12 @@ struct Newuoa {
         double hcol[NPT], gc[N], gd[N], s[N], wv[N];
         const double delsq = delta * delta;
         h_column(knew, idz, hcol);
-        alpha = rd(hcol, knew - 1);
+        alpha = rd_(hcol, knew - 1);
         double dd = 0.0;
 #pragma unroll
         for (int i = 0; i < N; ++i) {
-            d[i] = rd2(xpt, knew - 1, i) - xopt[i];
-            gc[i] = rd2(bmat, knew - 1, i);
+            d[i] = rd2_(xpt, knew - 1, i) - xopt[i];
+            gc[i] = rd2_(bmat, knew - 1, i);
             gd[i] = 0.0;
             dd = dd + d[i] * d[i];
         }
@@ -395,7 +429,7 @@ struct Newuoa {
         for (int k = 0; k < NPT; ++k) hw[N + k] = 0.0;
 #pragma unroll
         for (int j = 0; j < NPTM; ++j) {
-            double temp = rd2(zmat, knew - 1, j);
+            double temp = rd2_(zmat, knew - 1, j);
             if (j + 1 < idz) temp = -temp;
 #pragma unroll
             for (int k = 0; k < NPT; ++k) hw[N + k] = hw[N + k] + temp * zmat[k][j];
@@ -408,7 +442,7 @@ struct Newuoa {
 #pragma unroll
         for (int i = 0; i < N; ++i) {
             dd = dd + d[i] * d[i];
-            s[i] = rd2(xpt, knew - 1, i) - xopt[i];
+            s[i] = rd2_(xpt, knew - 1, i) - xopt[i];
             ds = ds + d[i] * s[i];
             ss = ss + s[i] * s[i];
             xoptsq = xoptsq + xopt[i] * xopt[i];
@@ -435,7 +469,7 @@ struct Newuoa {
                 }
             }
 #pragma unroll
-            for (int i = 0; i < N; ++i) s[i] = rd2(xpt, ksav - 1, i) - xopt[i];
+            for (int i = 0; i < N; ++i) s[i] = rd2_(xpt, ksav - 1, i) - xopt[i];
         }
         double ssden = dd * ss - ds * ds;
         double densav = 0.0;
@@ -544,7 +578,7 @@ struct Newuoa {
             }
             double pk[5];
 #pragma unroll
-            for (int i = 0; i < 5; ++i) pk[i] = rd2(prod, knew - 1, i);
+            for (int i = 0; i < 5; ++i) pk[i] = rd2_(prod, knew - 1, i);
             sum = 0.0;
 #pragma unroll
             for (int i = 0; i < 5; ++i) {
@@ -626,7 +660,7 @@ struct Newuoa {
 #pragma unroll
                 for (int j = 0; j < 5; ++j) vlag[k] = vlag[k] + prod[k][j] * par[j];
             }
-            tau = rd(vlag, knew - 1);
+            tau = rd_(vlag, knew - 1);
             dd = 0.0;
             tempa = 0.0;
             tempb = 0.0;
@@ -645,7 +679,7 @@ struct Newuoa {
 #pragma unroll
             for (int i = 0; i < N; ++i) {
                 temp = tempa * xopt[i] + tempb * d[i] - vlag[NPT + i];
-                s[i] = tau * rd2(bmat, knew - 1, i) + alpha * temp;
+                s[i] = tau * rd2_(bmat, knew - 1, i) + alpha * temp;
             }
 #pragma unroll
             for (int k = 0; k < NPT; ++k) {
@@ -672,7 +706,7 @@ struct Newuoa {
 #pragma unroll
             for (int j = 0; j < 5; ++j) w[k] = w[k] + wvec[k][j] * par[j];
         }
-        wr(vlag, kopt - 1, rd(vlag, kopt - 1) + 1.0);
+        wr_(vlag, kopt - 1, rd_(vlag, kopt - 1) + 1.0);
     }
 
     // ------------------------------------------------------------------------- UPDATE
@@ -684,35 +718,35 @@ struct Newuoa {
         for (int j = 2; j <= NPTM; ++j) {
             if (j == idz) {
                 jl = idz;
-            } else if (rd2(zmat, knew - 1, j - 1) != 0.0) {
-                const double zl = rdc(zmat, knew - 1, jl - 1);  // zmat[knew][jl]
-                const double zj = rd2(zmat, knew - 1, j - 1);
+            } else if (rd2_(zmat, knew - 1, j - 1) != 0.0) {
+                const double zl = rdc_(zmat, knew - 1, jl - 1);  // zmat[knew][jl]
+                const double zj = rd2_(zmat, knew - 1, j - 1);
                 double temp = sqrt(zl * zl + zj * zj);
                 const double ta = zl / temp, tb = zj / temp;
 #pragma unroll
                 for (int i = 0; i < NPT; ++i) {
-                    const double zil = rdc(zmat, i, jl - 1);
+                    const double zil = rdc_(zmat, i, jl - 1);
                     temp = ta * zil + tb * zmat[i][j - 1];
                     zmat[i][j - 1] = ta * zmat[i][j - 1] - tb * zil;
-                    wrc(zmat, i, jl - 1, temp);
+                    wrc_(zmat, i, jl - 1, temp);
                 }
-                wr2(zmat, knew - 1, j - 1, 0.0);
+                wr2_(zmat, knew - 1, j - 1, 0.0);
             }
         }
-        double tempa = rd2(zmat, knew - 1, 0);
+        double tempa = rd2_(zmat, knew - 1, 0);
         if (idz >= 2) tempa = -tempa;
         double tempb = 0.0;
-        if (jl > 1) tempb = rdc(zmat, knew - 1, jl - 1);
+        if (jl > 1) tempb = rdc_(zmat, knew - 1, jl - 1);
 #pragma unroll
         for (int i = 0; i < NPT; ++i) {
             wk[i] = tempa * zmat[i][0];
-            if (jl > 1) wk[i] = wk[i] + tempb * rdc(zmat, i, jl - 1);
+            if (jl > 1) wk[i] = wk[i] + tempb * rdc_(zmat, i, jl - 1);
         }
-        const double alpha = rd(wk, knew - 1);  // only wk[0..NPT) are set; knew <= NPT
-        const double tau = rd(vlag, knew - 1);
+        const double alpha = rd_(wk, knew - 1);  // only wk[0..NPT) are set; knew <= NPT
+        const double tau = rd_(vlag, knew - 1);
         const double tausq = tau * tau;
         const double denom = alpha * beta + tausq;
-        wr(vlag, knew - 1, tau - 1.0);
+        wr_(vlag, knew - 1, tau - 1.0);
         int iflag = 0;
         if (jl == 1) {
             const double temp = sqrt(fabs(denom));
@@ -726,17 +760,17 @@ struct Newuoa {
             int ja = 1;
             if (beta >= 0.0) ja = jl;
             const int jb = jl + 1 - ja;
-            double temp = rdc(zmat, knew - 1, jb - 1) / denom;
+            double temp = rdc_(zmat, knew - 1, jb - 1) / denom;
             tempa = temp * beta;
             tempb = temp * tau;
-            temp = rdc(zmat, knew - 1, ja - 1);
+            temp = rdc_(zmat, knew - 1, ja - 1);
             const double scala = 1.0 / sqrt(fabs(beta) * temp * temp + tausq);
             const double scalb = scala * sqrt(fabs(denom));
 #pragma unroll
             for (int i = 0; i < NPT; ++i) {
-                const double za = rdc(zmat, i, ja - 1), zb = rdc(zmat, i, jb - 1);
-                wrc(zmat, i, ja - 1, scala * (tau * za - temp * vlag[i]));
-                wrc(zmat, i, jb - 1, scalb * (zb - tempa * wk[i] - tempb * vlag[i]));
+                const double za = rdc_(zmat, i, ja - 1), zb = rdc_(zmat, i, jb - 1);
+                wrc_(zmat, i, ja - 1, scala * (tau * za - temp * vlag[i]));
+                wrc_(zmat, i, jb - 1, scalb * (zb - tempa * wk[i] - tempb * vlag[i]));
             }
             if (denom <= 0.0) {
                 if (beta < 0.0) idz = idz + 1;
@@ -748,14 +782,14 @@ struct Newuoa {
 #pragma unroll
             for (int i = 0; i < NPT; ++i) {
                 const double temp = zmat[i][0];
-                zmat[i][0] = rdc(zmat, i, idz - 1);
-                wrc(zmat, i, idz - 1, temp);
+                zmat[i][0] = rdc_(zmat, i, idz - 1);
+                wrc_(zmat, i, idz - 1, temp);
             }
         }
 #pragma unroll
         for (int j = 0; j < N; ++j) {
             const int jp = NPT + j;  // 0-based row of BMAT / entry of VLAG, W
-            wk[jp] = rd2(bmat, knew - 1, j);
+            wk[jp] = rd2_(bmat, knew - 1, j);
             const double ta = (alpha * vlag[jp] - tau * wk[jp]) / denom;
             const double tb = (-beta * wk[jp] - tau * vlag[jp]) / denom;
 #pragma unroll
@@ -802,11 +836,11 @@ struct Newuoa {
             double xipt = 0.0, xjpt = 0.0;
             if (nfm <= 2 * N) {
                 if (nfm >= 1 && nfm <= N) {
-                    wr2(xpt, nf - 1, nfm - 1, rhobeg);
+                    wr2_(xpt, nf - 1, nfm - 1, rhobeg);
                 } else if (nfm > N) {
 #pragma unroll
                     for (int j = 0; j < N; ++j)
-                        if (j == nfmm - 1) wr2(xpt, nf - 1, j, -rhobeg);
+                        if (j == nfmm - 1) wr2_(xpt, nf - 1, j, -rhobeg);
                 }
             } else {
                 int itemp = (nfmm - 1) / N;
@@ -818,18 +852,18 @@ struct Newuoa {
                     ipt = itemp;
                 }
                 xipt = rhobeg;
-                if (rd(fval, ipt + np - 1) < rd(fval, ipt)) xipt = -xipt;
+                if (rd_(fval, ipt + np - 1) < rd_(fval, ipt)) xipt = -xipt;
                 xjpt = rhobeg;
-                if (rd(fval, jpt + np - 1) < rd(fval, jpt)) xjpt = -xjpt;
+                if (rd_(fval, jpt + np - 1) < rd_(fval, jpt)) xjpt = -xjpt;
 #pragma unroll
                 for (int j = 0; j < N; ++j) {
-                    if (j == ipt - 1) wr2(xpt, nf - 1, j, xipt);
-                    if (j == jpt - 1) wr2(xpt, nf - 1, j, xjpt);
+                    if (j == ipt - 1) wr2_(xpt, nf - 1, j, xipt);
+                    if (j == jpt - 1) wr2_(xpt, nf - 1, j, xjpt);
                 }
             }
             double xe[N];
 #pragma unroll
-            for (int j = 0; j < N; ++j) xe[j] = rd2(xpt, nf - 1, j) + xbase[j];
+            for (int j = 0; j < N; ++j) xe[j] = rd2_(xpt, nf - 1, j) + xbase[j];
 #pragma unroll
             for (int j = 0; j < N; ++j) x[j] = xe[j];
             if (nf > nftest) {  // maxfun < NPT: stop during initialisation
@@ -839,7 +873,7 @@ struct Newuoa {
                 return nf - 1;
             }
             f = fun(x);
-            wr(fval, nf - 1, f);
+            wr_(fval, nf - 1, f);
             if (nf == 1) {
                 fbeg = f;
                 fopt = f;
@@ -850,37 +884,37 @@ struct Newuoa {
             }
             if (nfm <= 2 * N) {
                 if (nfm >= 1 && nfm <= N) {
-                    wr(gq, nfm - 1, (f - fbeg) / rhobeg);
+                    wr_(gq, nfm - 1, (f - fbeg) / rhobeg);
                     if (NPT < nf + N) {
 #pragma unroll
                         for (int j = 0; j < N; ++j)
                             if (j == nfm - 1) {
                                 bmat[0][j] = -1.0 / rhobeg;
-                                wr2(bmat, nf - 1, j, 1.0 / rhobeg);
-                                wr2(bmat, NPT + nfm - 1, j, -0.5 * rhosq);
+                                wr2_(bmat, nf - 1, j, 1.0 / rhobeg);
+                                wr2_(bmat, NPT + nfm - 1, j, -0.5 * rhosq);
                             }
                     }
                 } else if (nfm > N) {
 #pragma unroll
                     for (int j = 0; j < N; ++j) {
                         if (j == nfmm - 1) {
-                            wr2(bmat, nf - N - 1, j, 0.5 / rhobeg);
-                            wr2(bmat, nf - 1, j, -0.5 / rhobeg);
+                            wr2_(bmat, nf - N - 1, j, 0.5 / rhobeg);
+                            wr2_(bmat, nf - 1, j, -0.5 / rhobeg);
                         }
                     }
 #pragma unroll
                     for (int j = 0; j < NPTM; ++j) {
                         if (j == nfmm - 1) {
                             zmat[0][j] = -reciq - reciq;
-                            wr2(zmat, nf - N - 1, j, reciq);
-                            wr2(zmat, nf - 1, j, reciq);
+                            wr2_(zmat, nf - N - 1, j, reciq);
+                            wr2_(zmat, nf - 1, j, reciq);
                         }
                     }
                     const int ih = (nfmm * (nfmm + 1)) / 2;
                     const double temp = (fbeg - f) / rhobeg;
-                    const double g = rd(gq, nfmm - 1);
-                    wr(hq, ih - 1, (g - temp) / rhobeg);
-                    wr(gq, nfmm - 1, 0.5 * (g + temp));
+                    const double g = rd_(gq, nfmm - 1);
+                    wr_(hq, ih - 1, (g - temp) / rhobeg);
+                    wr_(gq, nfmm - 1, 0.5 * (g + temp));
                 }
             } else {
                 const int ih = (ipt * (ipt - 1)) / 2 + jpt;
@@ -890,12 +924,12 @@ struct Newuoa {
                 for (int j = 0; j < NPTM; ++j) {
                     if (j == nfmm - 1) {
                         zmat[0][j] = recip;
-                        wr2(zmat, nf - 1, j, recip);
-                        wr2(zmat, ipt, j, -recip);
-                        wr2(zmat, jpt, j, -recip);
+                        wr2_(zmat, nf - 1, j, recip);
+                        wr2_(zmat, ipt, j, -recip);
+                        wr2_(zmat, jpt, j, -recip);
                     }
                 }
-                wr(hq, ih - 1, (fbeg - rd(fval, ipt) - rd(fval, jpt) + f) / (xipt * xjpt));
+                wr_(hq, ih - 1, (fbeg - rd_(fval, ipt) - rd_(fval, jpt) + f) / (xipt * xjpt));
             }
         }
         int nf = NPT;
@@ -910,7 +944,7 @@ struct Newuoa {
         double xoptsq = 0.0;
 #pragma unroll
         for (int i = 0; i < N; ++i) {
-            xopt[i] = rd2(xpt, kopt - 1, i);
+            xopt[i] = rd2_(xpt, kopt - 1, i);
             xoptsq = xoptsq + xopt[i] * xopt[i];
         }
     L90:
@@ -979,10 +1013,10 @@ struct Newuoa {
                 dx = dx + d[j] * xopt[j];
             }
             beta = dx * dx + dsq * (xoptsq + dx + dx + 0.5 * dsq) + beta - bsum;
-            wr(vlag, kopt - 1, rd(vlag, kopt - 1) + 1.0);
+            wr_(vlag, kopt - 1, rd_(vlag, kopt - 1) + 1.0);
         }
         if (knew > 0) {
-            const double vk = rd(vlag, knew - 1);
+            const double vk = rd_(vlag, knew - 1);
             const double temp = 1.0 + alpha * beta / (vk * vk);
             if (fabs(temp) <= 0.8) bigden(idz, kopt, knew, beta);
         }
@@ -1080,23 +1114,23 @@ struct Newuoa {
             }
             // L410: move point knew to xnew and update the model
             update(idz, beta, knew);
-            wr(fval, knew - 1, f);
+            wr_(fval, knew - 1, f);
             {
-                const double pqk = rd(pq, knew - 1);
+                const double pqk = rd_(pq, knew - 1);
                 int ih = 0;
 #pragma unroll
                 for (int i = 0; i < N; ++i) {
-                    const double temp = pqk * rd2(xpt, knew - 1, i);
+                    const double temp = pqk * rd2_(xpt, knew - 1, i);
 #pragma unroll
                     for (int j = 0; j <= i; ++j) {
-                        hq[ih] = hq[ih] + temp * rd2(xpt, knew - 1, j);
+                        hq[ih] = hq[ih] + temp * rd2_(xpt, knew - 1, j);
                         ++ih;
                     }
                 }
-                wr(pq, knew - 1, 0.0);
+                wr_(pq, knew - 1, 0.0);
 #pragma unroll
                 for (int j = 0; j < NPTM; ++j) {
-                    double temp = diff * rd2(zmat, knew - 1, j);
+                    double temp = diff * rd2_(zmat, knew - 1, j);
                     if (j + 1 < idz) temp = -temp;
 #pragma unroll
                     for (int k = 0; k < NPT; ++k) pq[k] = pq[k] + temp * zmat[k][j];
@@ -1104,15 +1138,15 @@ struct Newuoa {
                 double gqsq = 0.0;
 #pragma unroll
                 for (int i = 0; i < N; ++i) {
-                    gq[i] = gq[i] + diff * rd2(bmat, knew - 1, i);
+                    gq[i] = gq[i] + diff * rd2_(bmat, knew - 1, i);
                     gqsq = gqsq + gq[i] * gq[i];
-                    wr2(xpt, knew - 1, i, xnew[i]);
+                    wr2_(xpt, knew - 1, i, xnew[i]);
                 }
                 if (ksave == 0 && delta == rho) {
                     if (fabs(ratio) > 1.0e-2) {
                         itest = 0;
                     } else {
-                        const double fk = rd(fval, kopt - 1);
+                        const double fk = rd_(fval, kopt - 1);
 #pragma unroll
                         for (int k = 0; k < NPT; ++k) vlag[k] = fval[k] - fk;
                         double gisq = 0.0;
