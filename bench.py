@@ -26,6 +26,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "complex samples/sec through demodulate fit (fp64), 1/2/4/8 MI355X + CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# dense fp64 matrix peak: v_mfma_f64_16x16x4 keeps the pipe 64 cycles per 2048 FLOP (measured,
+# SQ_VALU_MFMA_BUSY_CYCLES / SQ_INSTS_MFMA, profiles/r1b/sq_counters.json) = 32 FLOP/clk/SIMD
+# × 1024 SIMDs × 2.4 GHz
+MFMA_F64_PEAK_TFLOPS = 78.6
 
 
 def parse():
@@ -140,10 +144,17 @@ def main():
     if mom:
         avg_ms = float(np.mean(mom))
         achieved = algo_bytes / (avg_ms * 1e-3) / 1e9
+        # the same kernel against the dense fp64 MFMA peak: 4 real MACs per harmonic
+        # (K = 24) per complex sample — the pipe it actually saturates
+        mfma_flops = 2.0 * 4 * 24 * P * N
+        tflops = mfma_flops / (avg_ms * 1e-3) / 1e12
         roofline = {"bound": "hbm", "kernel": "k_moments", "achieved": round(achieved, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": traffic_from_profiles(P, N), "algorithmic_bytes": algo_bytes,
-                    "avg_ms": round(avg_ms, 3)}
+                    "avg_ms": round(avg_ms, 3),
+                    "mfma": {"achieved": round(tflops, 2), "peak": MFMA_F64_PEAK_TFLOPS,
+                             "unit": "TFLOP/s", "frac": round(tflops / MFMA_F64_PEAK_TFLOPS, 4),
+                             "algorithmic_flops": mfma_flops}}
     kernels = {k: round(float(np.mean(v)), 3) for k, v in kern.items()}
     status = par["status"]
     fits = {"fallback_exact": int(np.count_nonzero(status & gpd.GPD_ST_FALLBACK)),
