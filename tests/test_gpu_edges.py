@@ -1,0 +1,60 @@
+"""GPU edge cases: ragged shapes (N not a multiple of the 32-sample tile, P not a multiple of
+the 128-series workgroup or of 4), a general fc_of_pixel (series not grouped by FC column —
+the per-series FC path of both moment kernels), FC samples equal to 0 (angle(0) = 0), NaN
+samples, and the smallest series."""
+import numpy as np
+import pytest
+
+import synth
+from test_gpu_parity import assert_fit_parity, perturbed_runs, ulps_for
+
+pytestmark = pytest.mark.gpu
+
+
+def run_both(gpu, oracle, B, label, methods=("exact", "harmonic"), **kw):
+    ref = oracle.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], flags=oracle.RECENTER)
+    for method in methods:
+        got = gpu.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], method=method, **kw)
+        print(assert_fit_parity(got, ref, perturbed_runs(oracle, B, ulps=ulps_for(method)),
+                                label=f"{label}/{method}"))
+
+
+@pytest.mark.parametrize("N,P", [(1037, 7), (4099, 133), (3000, 258)])
+def test_ragged_shapes(gpu, oracle, N, P):
+    run_both(gpu, oracle, synth.make_batch(N, P, seed=N + P), f"ragged {N}x{P}")
+
+
+def test_general_fc_assignment(gpu, oracle):
+    """fc_of_pixel not grouped by 4: every workgroup takes the per-series FC path."""
+    B = synth.make_batch(3000, 40, seed=8)
+    rng = np.random.default_rng(1)
+    perm = rng.permutation(40)
+    B["d"] = B["d"][perm]
+    B["fc_of_pixel"] = np.ascontiguousarray(B["fc_of_pixel"][perm])
+    run_both(gpu, oracle, B, "general fc")
+
+
+def test_fc_zero_samples_take_angle_zero(gpu, oracle):
+    B = synth.make_batch(2500, 16, seed=12)
+    B["fc"][:, 100:140] = 0.0  # angle(0) = 0 → phasor 1 (src/Modulation.jl:388)
+    run_both(gpu, oracle, B, "fc zeros")
+
+
+def test_nan_sample_propagates(gpu, oracle):
+    B = synth.make_batch(2000, 8, seed=14)
+    B["d"][3, 500] = np.nan
+    for method in ("exact", "harmonic"):
+        got = gpu.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], method=method)
+        ref = oracle.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"])
+        assert np.isnan(ref["chi2"][3]) and np.isnan(got["chi2"][3])
+        assert got["status"][3] & gpu.GPD_ST_NAN
+        ok = np.arange(8) != 3
+        assert np.all(np.isfinite(got["chi2"][ok]))
+
+
+def test_two_samples(gpu, oracle):
+    """The smallest series the API accepts (n_samples = 2)."""
+    B = synth.make_batch(2, 4, seed=2)
+    ref = oracle.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"])
+    got = gpu.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], method="exact")
+    np.testing.assert_allclose(got["chi2"], ref["chi2"], rtol=1e-10, atol=1e-300)
