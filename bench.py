@@ -165,7 +165,7 @@ def main():
     fits["median_abs_b_err_vs_truth"] = float(np.median(np.abs(par["b"] - tr["b"])))
 
     cpu = None
-    if not args.no_cpu and args.cpu_pixels > 0:
+    if not args.no_cpu and args.cpu_pixels > 0 and world == 1:  # rank 0 at N=1 only
         cpu = cpu_baseline(gpd, t, d, fc, fcop, par, args, N)
 
     out = {
