@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdarg>
 #include <cstdio>
 #include <cmath>
@@ -564,10 +565,20 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
             }
             return true;
         };
+        // only the FC columns this shard references travel (e.g. 8 of the 40 columns of an
+        // exposure matrix passed whole as `fc`)
+        int32_t cmin = INT32_MAX, cmax = 0;
+        for (int64_t k = p0; k < p1; ++k) {
+            cmin = std::min(cmin, fc_of_pixel[k]);
+            cmax = std::max(cmax, fc_of_pixel[k]);
+        }
+        const int64_t nfc = (int64_t)cmax - cmin + 1;
+        std::vector<int32_t> fcop_l(fc_of_pixel + p0, fc_of_pixel + p1);
+        for (auto &c : fcop_l) c -= cmin;
         bool ok = chk(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate") &&
                   chk(hipMalloc(&dt, N * sizeof(double)), "hipMalloc t") &&
                   chk(hipMalloc(&dd, (size_t)P * N * sizeof(c64)), "hipMalloc d") &&
-                  chk(hipMalloc(&dfc, (size_t)n_fc * N * sizeof(c64)), "hipMalloc fc") &&
+                  chk(hipMalloc(&dfc, (size_t)nfc * N * sizeof(c64)), "hipMalloc fc") &&
                   chk(hipMalloc(&dfcop, P * sizeof(int32_t)), "hipMalloc fcop") &&
                   chk(hipMalloc(&dpar, nrec * sizeof(Param)), "hipMalloc params") &&
                   (!state || chk(hipMalloc(&dst, N), "hipMalloc state")) &&
@@ -581,9 +592,10 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
         ok = chk(hipMemcpyAsync(dt, t + s0, N * sizeof(double), hipMemcpyHostToDevice, s), "H2D t") &&
              chk(hipMemcpy2DAsync(dd, N * sizeof(c64), d + p0 * ldd + s0, ldd * sizeof(gpd_c64),
                                   N * sizeof(c64), P, hipMemcpyHostToDevice, s), "H2D d") &&
-             chk(hipMemcpy2DAsync(dfc, N * sizeof(c64), fc + s0, ldfc * sizeof(gpd_c64),
-                                  N * sizeof(c64), n_fc, hipMemcpyHostToDevice, s), "H2D fc") &&
-             chk(hipMemcpyAsync(dfcop, fc_of_pixel + p0, P * sizeof(int32_t), hipMemcpyHostToDevice, s),
+             chk(hipMemcpy2DAsync(dfc, N * sizeof(c64), fc + (int64_t)cmin * ldfc + s0,
+                                  ldfc * sizeof(gpd_c64), N * sizeof(c64), nfc,
+                                  hipMemcpyHostToDevice, s), "H2D fc") &&
+             chk(hipMemcpyAsync(dfcop, fcop_l.data(), P * sizeof(int32_t), hipMemcpyHostToDevice, s),
                  "H2D fcop") &&
              (!state || chk(hipMemcpyAsync(dst, state + s0, N, hipMemcpyHostToDevice, s), "H2D state")) &&
              (!bphi || chk(hipMemcpyAsync(dbphi, bphi + 2 * p0, 2 * P * sizeof(double),
@@ -592,7 +604,7 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
             cleanup();
             return fail(GPD_E_HIP);
         }
-        int r = pipeline_dev(N, P, dt, (const gpd_c64 *)dd, N, (const gpd_c64 *)dfc, n_fc, N, dfcop,
+        int r = pipeline_dev(N, P, dt, (const gpd_c64 *)dd, N, (const gpd_c64 *)dfc, nfc, N, dfcop,
                              dst, omega, xinit, flags, maxfun, (gpd_param *)dpar, (gpd_c64 *)dout, N,
                              dbphi, g, s, errbuf_l, errlen_l, window);
         if (r != GPD_OK) {

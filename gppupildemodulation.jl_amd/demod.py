@@ -322,15 +322,19 @@ def window_tables(params, n_samples, nwindow, *, fitoffsets=False):
     """Broadcast per-window parameters to per-sample Float32 columns (32, N)
     (src/GPPupilDemodulation.jl:209-224; b ≥ 0 already, :427-430 normalised it)."""
     nwin, C = params.shape
-    rows = np.minimum(np.arange(n_samples) // nwindow, nwin - 1)
-    per = params[rows].T  # (C, N)
-    tables = {"ABSA": np.abs(per["a"]).astype(np.float32),
-              "ARGA": np.angle(per["a"]).astype(np.float32),
-              "B": per["b"].astype(np.float32),
-              "PHI": per["phi"].astype(np.float32)}
+    counts = np.full(nwin, nwindow)
+    counts[-1] = n_samples - nwindow * (nwin - 1)
+
+    def per_sample(v):  # (nwin, C) per-window values → (C, N) Float32 rows
+        return np.repeat(v.astype(np.float32), counts, axis=0).T.copy()
+
+    tables = {"ABSA": per_sample(np.abs(params["a"])),
+              "ARGA": per_sample(np.angle(params["a"])),
+              "B": per_sample(params["b"]),
+              "PHI": per_sample(params["phi"])}
     if fitoffsets:
-        tables["X0"] = per["c"].real.astype(np.float32)
-        tables["Y0"] = per["c"].imag.astype(np.float32)
+        tables["X0"] = per_sample(params["c"].real)
+        tables["Y0"] = per_sample(params["c"].imag)
     return tables
 
 
