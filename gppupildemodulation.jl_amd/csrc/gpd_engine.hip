@@ -76,13 +76,13 @@ DevCtx *ctx_for(int dev) {
 size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
 struct Layout {
-    size_t info, tab, part, mom, aux, fstat, raw, list, phbuf, total;
+    size_t info, tab, part, mom, aux, fstat, raw, list, phbuf, partG, momG, auxG, fcid, d0, total;
     int nch;
     long long chunk;
 };
 
 Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic, bool phbuf,
-            bool mfma, int n_cu) {
+            bool mfma, int n_cu, bool harm_offs) {
     Layout L{};
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -129,6 +129,12 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     L.raw = take((size_t)P * 2 * sizeof(double));
     L.list = take((size_t)(P + 64) * sizeof(int));
     L.phbuf = take(phbuf ? (size_t)n_fc * N * sizeof(c64) : 0);
+    // harmonic fitoffsets: G moments of the FC columns (same chunking), Σ d per series
+    L.partG = take(harm_offs ? (size_t)nch * NMOM * n_fc * sizeof(double) : 0);
+    L.momG = take(harm_offs ? (size_t)NMOM * n_fc * sizeof(double) : 0);
+    L.auxG = take(harm_offs ? (size_t)4 * n_fc * sizeof(double) : 0);
+    L.fcid = take(harm_offs ? (size_t)n_fc * sizeof(int32_t) : 0);
+    L.d0 = take(harm_offs ? (size_t)2 * P * sizeof(double) : 0);
     L.total = off;
     return L;
 }
@@ -200,15 +206,33 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     hipStream_t stream = (hipStream_t)stream_;
     const bool faint = state != nullptr;
     const bool offs = (flags & GPD_FIT_OFFSETS) != 0;
-    // Harmonic moments cover the no-offsets χ²; offsets go to the exact evaluator.
-    // Windows (≤ ~10k samples each) are fitted by the exact evaluator: one workgroup per
-    // (window, diode) series.
-    const bool want_exact = (flags & GPD_METHOD_EXACT) || offs || window > 0;
-    if ((flags & GPD_METHOD_HARMONIC) && offs) {
-        set_err(errbuf, errlen, "gpd_fit_batch_dev: harmonic method does not support fitoffsets yet");
+    // fp64 MFMA moment pass by default (producer/consumer kernel for non-faint series);
+    // GPD_MOMENTS=valu | mfma1 selects the VALU / single-role MFMA kernel (A/B runs)
+    const char *mk = getenv("GPD_MOMENTS");
+    // buffer descriptors of the MFMA kernels address 128 series rows / the cos-sin table
+    // with 32-bit offsets
+    const bool use_mfma = !(mk && std::string(mk) == "valu") &&
+                          (double)MM_PIX * (double)ldd * 16.0 < 2147483648.0 &&
+                          (double)n_samples * KH * 16.0 < 2147483648.0;
+    // Harmonic fitoffsets (non-faint, on request): the χ² of the 2×2 system needs the moments
+    // G_n of the FC phasors (producer/consumer kernel in UNIT mode over the FC columns) and Σ d
+    // per series.  Windows (≤ ~10k samples each: one workgroup per (window, diode)) and
+    // METHOD_EXACT use the exact evaluator.
+    const bool harm_offs_ok =
+        !faint && use_mfma && (double)MM_PIX * (double)ldfc * 16.0 < 2147483648.0;
+    // Offsets default to the exact evaluator: the 2×2 system is ill-conditioned for small b and
+    // the flat landscape turns the expansion's ~1e-14 χ² rounding into ~1e-10 moves of NEWUOA's
+    // iterate; METHOD_HARMONIC asks for the fast path anyway (parity ~1e-9).
+    const bool want_exact = (flags & GPD_METHOD_EXACT) ||
+                            (offs && !(harm_offs_ok && (flags & GPD_METHOD_HARMONIC))) ||
+                            window > 0;
+    if ((flags & GPD_METHOD_HARMONIC) && want_exact) {
+        set_err(errbuf, errlen, "gpd_fit_batch_dev: harmonic method unavailable here "
+                                "(fitoffsets with faint states, or windows)");
         return GPD_E_ARG;
     }
     const bool harmonic = !want_exact;
+    const bool harm_offs = harmonic && offs;
     const long long N = n_samples, ncol = n_pixels;
     const long long nwin = window > 0 ? (N + window - 1) / window : 1;
     const long long P = ncol * nwin;  // series
@@ -216,15 +240,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
 
     DevCtx *cx = ctx_for(device);
     std::lock_guard<std::mutex> lk(cx->mu);
-    // fp64 MFMA moment pass by default (producer/consumer kernel for non-faint series);
-    // GPD_MOMENTS=valu | mfma1 selects the VALU / single-role MFMA kernel (A/B runs)
-    const char *mk = getenv("GPD_MOMENTS");
-    // buffer descriptors of the MFMA kernel address 128 series rows with 32-bit offsets
-    const bool use_mfma = !(mk && std::string(mk) == "valu") &&
-                          (double)MM_PIX * (double)ldd * 16.0 < 2147483648.0 &&
-                          (double)N * KH * 16.0 < 2147483648.0;
     if (cx->n_cu == 0) HIP_TRY(hipDeviceGetAttribute(&cx->n_cu, hipDeviceAttributeMultiprocessorCount, device));
-    const Layout L = plan(N, P, n_fc, faint, harmonic, phbuf, use_mfma, cx->n_cu);
+    const Layout L = plan(N, P, n_fc, faint, harmonic, phbuf, use_mfma, cx->n_cu, harm_offs);
     if (cx->ws_cap < L.total) {
         if (cx->ws) {
             HIP_TRY(hipDeviceSynchronize());
@@ -346,8 +363,30 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         dim3 gr((unsigned)((P + 255) / 256), (unsigned)NMOM);
         k_reduce_moments<<<gr, 256, 0, stream>>>(part, L.nch, P, info, fstat, faint ? 1 : 0, mom, aux);
         mark("reduce");
+        double *momG = (double *)(ws + L.momG), *d0 = (double *)(ws + L.d0);
+        if (harm_offs) {
+            // G_n of every FC column: the producer/consumer kernel in UNIT mode with the FC
+            // columns as its series (identity fc_of_pixel → per-series FC path)
+            int32_t *fcid = (int32_t *)(ws + L.fcid);
+            k_iota<<<(unsigned)((n_fc + 255) / 256), 256, 0, stream>>>(fcid, n_fc);
+            Problem pg = pb;
+            pg.P = n_fc;
+            pg.d = (const c64 *)fc;
+            pg.ldd = ldfc;
+            pg.fcop = fcid;
+            pg.win = 0;
+            pg.ncol = n_fc;
+            double *partG = (double *)(ws + L.partG), *auxG = (double *)(ws + L.auxG);
+            dim3 gG((unsigned)((n_fc + MM_PIX - 1) / MM_PIX), (unsigned)L.nch);
+            k_moments_ws<0, true><<<gG, 512, 0, stream>>>(pg, tab, L.chunk, partG);
+            dim3 grG((unsigned)((n_fc + 255) / 256), (unsigned)NMOM);
+            k_reduce_moments<<<grG, 256, 0, stream>>>(partG, L.nch, n_fc, info, nullptr, 0, momG, auxG);
+            k_series_sum<<<(unsigned)P, 256, 0, stream>>>(pb, d0);
+            mark("offsets_moments");
+        }
         if (bphi) {
-            k_chi2_harmonic<<<(unsigned)((P + 63) / 64), 64, 0, stream>>>(pb, info, mom, aux, bphi, outp);
+            k_chi2_harmonic<<<(unsigned)((P + 63) / 64), 64, 0, stream>>>(pb, info, mom, aux, momG,
+                                                                        n_fc, d0, bphi, outp);
             mark("chi2_harmonic");
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipEventRecord(cx->done, stream));
@@ -362,26 +401,35 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                                            hipMemcpyHostToDevice, stream));
             Problem pp = pb;
             pp.flags |= F_PROF;
-            k_fit_harmonic<<<(unsigned)((P + 63) / 64), 64, 0, stream>>>(pp, info, mom, aux, outp,
-                                                                       raw, list, count);
+            k_fit_harmonic<<<(unsigned)((P + 63) / 64), 64, 0, stream>>>(pp, info, mom, aux, momG,
+                                                                       n_fc, d0, outp, raw, list,
+                                                                       count);
             HIP_TRY(hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_fitprof), sizeof z, 0,
                                              hipMemcpyDeviceToHost, stream));
             HIP_TRY(hipStreamSynchronize(stream));
             fprintf(stderr, "fit_prof per series: objective %.3g cycles, whole fit %.3g, evals %.3g\n",
                     (double)z[0] / P, (double)z[1] / P, (double)z[2] / P);
         } else {
-            k_fit_harmonic<<<(unsigned)((P + 63) / 64), 64, 0, stream>>>(pb, info, mom, aux, outp,
-                                                                       raw, list, count);
+            k_fit_harmonic<<<(unsigned)((P + 63) / 64), 64, 0, stream>>>(pb, info, mom, aux, momG,
+                                                                       n_fc, d0, outp, raw, list,
+                                                                       count);
         }
         mark("fit_harmonic");
         // fallback: series whose fit left the expansion's safe range, re-fitted exactly
         if (faint)
             k_fit_exact<true, false, false><<<exact_grid, EXACT_WG, 0, stream>>>(
                 pb, info, nullptr, fstat, list, count, outp, raw, ST_FALLBACK);
+        else if (harm_offs)
+            k_fit_exact<false, true, false><<<exact_grid, EXACT_WG, 0, stream>>>(
+                pb, info, nullptr, fstat, list, count, outp, raw, ST_FALLBACK);
         else
             k_fit_exact<false, false, false><<<exact_grid, EXACT_WG, 0, stream>>>(
                 pb, info, nullptr, fstat, list, count, outp, raw, ST_FALLBACK);
         mark("fit_fallback");
+        if (harm_offs) {
+            k_refine_exact<false><<<exact_grid, EXACT_WG, 0, stream>>>(pb, info, nullptr, raw, outp);
+            mark("refine_exact");
+        }
     } else {
         if (phbuf) {
             dim3 g((unsigned)std::min<long long>((N + 255) / 256, 256), (unsigned)n_fc);

