@@ -216,7 +216,15 @@ def cpu_baseline(gpd, t, d, fc, fcop, par, args, N):
     ref = oracle.fit_batch(th, dd, ff, fo, flags=oracle.RECENTER, nthreads=threads)
     dt = time.perf_counter() - t0
     err = np.abs(par["b"][:k] - ref["b"]) / ref["b"]
+    cpu_model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next(line.split(":", 1)[1].strip() for line in f
+                             if line.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
     return {"value": k * N / dt, "unit": "complex samples/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model,
             "sample": f"{k} of the device-generated series x {N} samples (first FC groups), "
                       f"oracle/ C restatement, OpenMP over series, {dt:.1f} s wall",
             "parity_b_within_1e-10": f"{int((err <= 1e-10).sum())}/{k}",
