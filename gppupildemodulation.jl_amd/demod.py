@@ -304,6 +304,8 @@ def demodulate_windows(timestamp, data, window, *, faintparam=None, onlyhigh=Fal
         raise ValueError("data must be N×40 with one row per timestamp")
     N = t.size
     nwindow = window_length(t, window)
+    if nwindow < 1:
+        raise ValueError("window shorter than half a sample interval")
     state = None
     if faintparam is not None:
         state = buildstates(faintparam, t, preswitchdelay=preswitchdelay,
@@ -389,6 +391,8 @@ def process_volt(timestamp, volt, *, offsets=None, window=None, faintparam=None,
     xi = None if (isinstance(init, str) and init == "auto") else \
         np.ascontiguousarray(init, dtype=np.float64).reshape(2)
     nwindow = 0 if window is None else window_length(t, window)
+    if window is not None and nwindow < 1:
+        raise ValueError("window shorter than half a sample interval")
     flags = GPD_RECENTER | (GPD_FIT_OFFSETS if fitoffsets else 0) | \
         (GPD_ONLY_HIGH if onlyhigh else 0)
     nrec = 32 * (-(-N // nwindow) if nwindow else 1)
