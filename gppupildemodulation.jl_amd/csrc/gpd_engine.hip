@@ -82,7 +82,7 @@ struct Layout {
 };
 
 Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic, bool phbuf,
-            bool mfma, int n_cu, bool harm_offs) {
+            bool mfma, int n_cu, bool harm_offs, bool windowed = false) {
     Layout L{};
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -122,7 +122,8 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     L.chunk = chunk;
     L.info = take(sizeof(Info));
     L.tab = take(harmonic ? (size_t)N * 2 * KH * sizeof(double) : 0);
-    L.part = take(harmonic ? (size_t)nch * NMOM * P * sizeof(double) : 0);
+    // windowed series: k_moments_win writes mom directly (no partial moments)
+    L.part = take(harmonic && !windowed ? (size_t)nch * NMOM * P * sizeof(double) : 0);
     L.mom = take(harmonic ? (size_t)NMOM * P * sizeof(double) : 0);
     L.aux = take((size_t)P * 4 * sizeof(double));
     L.fstat = take(faint ? (size_t)P * 16 * sizeof(double) : 0);
@@ -174,10 +175,6 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         set_err(errbuf, errlen, "gpd_fit_windows: window must be >= 0 (and fits only)");
         return GPD_E_ARG;
     }
-    if (window > 0 && (flags & GPD_METHOD_HARMONIC)) {
-        set_err(errbuf, errlen, "gpd_fit_windows: windows use the exact evaluator");
-        return GPD_E_ARG;
-    }
     if (n_samples < (window > 0 ? 1 : 2) || n_pixels < 1 || !t || !d || !fc || !fc_of_pixel ||
         !out_params || ldd < n_samples || ldfc < n_samples || n_fc < 1 ||
         (out_demod && ldo < n_samples)) {
@@ -216,19 +213,20 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                           (double)n_samples * KH * 16.0 < 2147483648.0;
     // Harmonic fitoffsets (non-faint, on request): the χ² of the 2×2 system needs the moments
     // G_n of the FC phasors (producer/consumer kernel in UNIT mode over the FC columns) and Σ d
-    // per series.  Windows (≤ ~10k samples each: one workgroup per (window, diode)) and
-    // METHOD_EXACT use the exact evaluator.
+    // per series.  METHOD_EXACT uses the exact evaluator; so do windows with fitoffsets.
     const bool harm_offs_ok =
         !faint && use_mfma && (double)MM_PIX * (double)ldfc * 16.0 < 2147483648.0;
     // Offsets default to the exact evaluator: the 2×2 system is ill-conditioned for small b and
     // the flat landscape turns the expansion's ~1e-14 χ² rounding into ~1e-10 moves of NEWUOA's
     // iterate; METHOD_HARMONIC asks for the fast path anyway (parity ~1e-9).
-    const bool want_exact = (flags & GPD_METHOD_EXACT) ||
-                            (offs && !(harm_offs_ok && (flags & GPD_METHOD_HARMONIC))) ||
-                            window > 0;
+    // Windows of ≥ HARM_MIN_SPAN samples: harmonic moments from k_moments_win (a shorter last
+    // window is re-fitted exactly); shorter windows: the exact evaluator.
+    const bool want_exact =
+        (flags & GPD_METHOD_EXACT) || (window > 0 && window < HARM_MIN_SPAN) ||
+        (offs && !(harm_offs_ok && window == 0 && (flags & GPD_METHOD_HARMONIC)));
     if ((flags & GPD_METHOD_HARMONIC) && want_exact) {
         set_err(errbuf, errlen, "gpd_fit_batch_dev: harmonic method unavailable here "
-                                "(fitoffsets with faint states, or windows)");
+                                "(fitoffsets with faint states or windows, short windows)");
         return GPD_E_ARG;
     }
     const bool harmonic = !want_exact;
@@ -241,7 +239,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     DevCtx *cx = ctx_for(device);
     std::lock_guard<std::mutex> lk(cx->mu);
     if (cx->n_cu == 0) HIP_TRY(hipDeviceGetAttribute(&cx->n_cu, hipDeviceAttributeMultiprocessorCount, device));
-    const Layout L = plan(N, P, n_fc, faint, harmonic, phbuf, use_mfma, cx->n_cu, harm_offs);
+    const Layout L =
+        plan(N, P, n_fc, faint, harmonic, phbuf, use_mfma, cx->n_cu, harm_offs, window > 0);
     if (cx->ws_cap < L.total) {
         if (cx->ws) {
             HIP_TRY(hipDeviceSynchronize());
@@ -324,7 +323,13 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     if (harmonic) {
         k_table<<<(unsigned)((N + 255) / 256), 256, 0, stream>>>(t, N, omega, tab);
         mark("table");
-        if (use_mfma) {
+        if (window > 0) {
+            if (faint)
+                k_moments_win<true><<<(unsigned)P, 256, 0, stream>>>(pb, tab, fstat, mom, aux);
+            else
+                k_moments_win<false><<<(unsigned)P, 256, 0, stream>>>(pb, tab, fstat, mom, aux);
+            mark("moments_win");
+        } else if (use_mfma) {
             dim3 g((unsigned)((P + MM_PIX - 1) / MM_PIX), (unsigned)L.nch);
             if (faint)
                 k_moments_mfma<true><<<g, 256, 0, stream>>>(pb, tab, fstat, L.chunk, part);
@@ -359,10 +364,13 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             else
                 k_moments<false><<<g, 64, 0, stream>>>(pb, tab, fstat, L.chunk, part);
         }
-        mark("moments");
-        dim3 gr((unsigned)((P + 255) / 256), (unsigned)NMOM);
-        k_reduce_moments<<<gr, 256, 0, stream>>>(part, L.nch, P, info, fstat, faint ? 1 : 0, mom, aux);
-        mark("reduce");
+        if (window == 0) {
+            mark("moments");
+            dim3 gr((unsigned)((P + 255) / 256), (unsigned)NMOM);
+            k_reduce_moments<<<gr, 256, 0, stream>>>(part, L.nch, P, info, fstat, faint ? 1 : 0,
+                                                     mom, aux);
+            mark("reduce");
+        }
         double *momG = (double *)(ws + L.momG), *d0 = (double *)(ws + L.d0);
         if (harm_offs) {
             // G_n of every FC column: the producer/consumer kernel in UNIT mode with the FC
@@ -719,10 +727,6 @@ int gpd_fit_windows(int64_t n_samples, int64_t window, int64_t n_cols, const dou
         set_err(errbuf, errlen, "gpd_fit_windows: window must be >= 1");
         return GPD_E_ARG;
     }
-    if (flags & GPD_METHOD_HARMONIC) {
-        set_err(errbuf, errlen, "gpd_fit_windows: windows use the exact evaluator");
-        return GPD_E_ARG;
-    }
     return host_batch(n_samples, n_cols, t, d, ldd, fc, n_fc, ldfc, fc_of_col, state, omega,
                       xinit, flags, maxfun, out_params, out_demod, ldo, nullptr, n_gpus, errbuf,
                       errlen, window);
@@ -737,8 +741,7 @@ int gpd_process_volt(int64_t n_samples, const double *t, const float *volt, int6
     // device: Float32 VOLT rows → centred complex128 columns → demodulateall (or every window)
     // → demodulated Float32 VOLT rows.  Column c < 32 uses FC column 32 + c/4 (idx(), :388).
     const int64_t N = n_samples;
-    if (N < 2 || !t || !volt || ldv < 80 || !out_params || (out_volt && ldov < 80) || window < 0 ||
-        (window > 0 && (flags & GPD_METHOD_HARMONIC))) {
+    if (N < 2 || !t || !volt || ldv < 80 || !out_params || (out_volt && ldov < 80) || window < 0) {
         set_err(errbuf, errlen, "gpd_process_volt: invalid shapes/pointers");
         return GPD_E_ARG;
     }

@@ -20,6 +20,9 @@ namespace gpd {
 
 constexpr int KH = 24;               // harmonics kept (|b| ≤ ~4.3 at 1e-16 tail)
 constexpr int NMOM = 3 + 4 * KH;     // F0r, F0i, W2, then (A,B,C,D)_n for n = 1..K
+// shortest window fitted from harmonic moments: below it NEWUOA's landing point drifts by
+// ~1e-10 under the expansion's χ² rounding and the exact evaluator is cheap
+constexpr long long HARM_MIN_SPAN = 256;
 constexpr int MOM_TS = 8;            // samples per LDS tile in the moment kernel
 constexpr int EXACT_WG = 256;        // threads per series in the exact evaluator
 constexpr double PI_F64 = 3.141592653589793;
@@ -968,7 +971,93 @@ __global__ __launch_bounds__(256) void k_reduce_moments(const double *__restrict
             aux[4 * k + 1] = (double)info->nvalid;  // Σ|p|² (|p| = 1)
             aux[4 * k + 2] = s;                    // Σ|q|² = Σ|d|²
         }
-        aux[4 * k + 3] = 0.0;
+        aux[4 * k + 3] = (double)info->nvalid;  // N of the χ² (per series: windows)
+    }
+}
+
+// Harmonic moments of windowed series (short spans, ≤ ~10k samples): one 256-thread workgroup
+// per (window, column) series; thread = (harmonic group hg of 3 harmonics, sample lane sl of
+// 32), samples sl, sl+32, … of the span; lanes reduced by a fixed xor tree, groups write
+// their own rows.  Writes mom[m][k] and aux[k] = {Σw|d|², Σw|p|², Σ|q|², N_valid} directly.
+template <bool FAINT>
+__global__ __launch_bounds__(256) void k_moments_win(Problem pb, const double *__restrict__ tab,
+                                                     const double *__restrict__ fstat,
+                                                     double *__restrict__ mom,
+                                                     double *__restrict__ aux) {
+    const long long k = blockIdx.x;
+    const Span sp = span_of(pb, k);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int hg = wave * 2 + (lane >> 5), sl = lane & 31;  // hg 0..7 → harmonics 3hg+1..3hg+3
+    const c64 *d = pb.d + sp.col * pb.ldd;
+    const c64 *fcol = pb.fc + (long long)pb.fcop[sp.col] * pb.ldfc;
+    double wm[5] = {0, 0, 0, 0, 0};
+    if (FAINT) {
+#pragma unroll
+        for (int q = 0; q < 5; ++q) wm[q] = fstat[k * 16 + 5 + q] * fstat[k * 16 + q];
+    }
+    double acc[12], f0r = 0.0, f0i = 0.0, w2 = 0.0, cnt = 0.0;
+#pragma unroll
+    for (int q = 0; q < 12; ++q) acc[q] = 0.0;
+    for (long long i = sp.s0 + sl; i < sp.s1; i += 32) {
+        int st = 0;
+        if (FAINT && !sample_valid(pb, i, st)) continue;
+        const c64 ph = unit_phasor(fcol[i]);
+        const c64 dv = d[i];
+        double qr = fma(ph.re, dv.re, ph.im * dv.im);  // q = w m p̄ d
+        double qi = fma(ph.re, dv.im, -(ph.im * dv.re));
+        if (FAINT) {
+            double f = wm[0];
+#pragma unroll
+            for (int q = 1; q < 5; ++q) f = (st + 1 == q) ? wm[q] : f;
+            qr *= f;
+            qi *= f;
+        }
+        const double *row = tab + i * (2 * KH) + 6 * hg;
+#pragma unroll
+        for (int h = 0; h < 3; ++h) {
+            const double c = row[2 * h], sn = row[2 * h + 1];
+            acc[4 * h + 0] = fma(qr, c, acc[4 * h + 0]);
+            acc[4 * h + 1] = fma(qi, sn, acc[4 * h + 1]);
+            acc[4 * h + 2] = fma(qi, c, acc[4 * h + 2]);
+            acc[4 * h + 3] = fma(qr, sn, acc[4 * h + 3]);
+        }
+        if (hg == 0) {
+            f0r += qr;
+            f0i += qi;
+            w2 = fma(dv.re, dv.re, fma(dv.im, dv.im, w2));
+            cnt += 1.0;
+        }
+    }
+#pragma unroll
+    for (int off = 1; off < 32; off <<= 1) {
+#pragma unroll
+        for (int q = 0; q < 12; ++q) acc[q] += __shfl_xor(acc[q], off, 64);
+        f0r += __shfl_xor(f0r, off, 64);
+        f0i += __shfl_xor(f0i, off, 64);
+        w2 += __shfl_xor(w2, off, 64);
+        cnt += __shfl_xor(cnt, off, 64);
+    }
+    if (sl == 0) {
+#pragma unroll
+        for (int h = 0; h < 3; ++h)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                mom[(long long)(3 + 4 * (3 * hg + h) + c) * pb.P + k] = acc[4 * h + c];
+        if (hg == 0) {
+            mom[0 * pb.P + k] = f0r;
+            mom[1 * pb.P + k] = f0i;
+            mom[2 * pb.P + k] = FAINT ? 0.0 : w2;
+            if (FAINT) {
+                aux[4 * k + 0] = fstat[k * 16 + 10];
+                aux[4 * k + 1] = fstat[k * 16 + 11];
+                aux[4 * k + 2] = fstat[k * 16 + 12];
+            } else {
+                aux[4 * k + 0] = w2;
+                aux[4 * k + 1] = cnt;
+                aux[4 * k + 2] = w2;
+            }
+            aux[4 * k + 3] = cnt;
+        }
     }
 }
 
@@ -1105,7 +1194,9 @@ __global__ __launch_bounds__(64) void k_fit_harmonic(Problem pb, const Info *__r
     const long long k = (long long)blockIdx.x * 64 + threadIdx.x;
     if (k >= pb.P) return;
     const Info in = *info;
-    if (in.mode == 2) {  // harmonic path unusable for these timestamps
+    const Span sp = span_of(pb, k);
+    // harmonic path unusable for these timestamps, or a short (last) window: exact fit
+    if (in.mode == 2 || sp.s1 - sp.s0 < HARM_MIN_SPAN) {
         list[atomicAdd(count, 1)] = (int)k;
         return;
     }
@@ -1113,7 +1204,7 @@ __global__ __launch_bounds__(64) void k_fit_harmonic(Problem pb, const Info *__r
     f.mom = mom;
     f.P = pb.P;
     f.k = k;
-    f.nvalid = (double)in.nvalid;
+    f.nvalid = aux[4 * k + 3];
     f.W2 = aux[4 * k + 0];
     f.DEN = aux[4 * k + 1];
     const double Q2 = aux[4 * k + 2];
@@ -1403,7 +1494,7 @@ __global__ __launch_bounds__(64) void k_chi2_harmonic(Problem pb, const Info *__
     f.mom = mom;
     f.P = pb.P;
     f.k = k;
-    f.nvalid = (double)in.nvalid;
+    f.nvalid = aux[4 * k + 3];
     f.W2 = aux[4 * k + 0];
     f.DEN = aux[4 * k + 1];
     f.tailref = 0.5e-16 * sqrt(f.W2 * f.DEN) / sqrt(f.nvalid * aux[4 * k + 2]);

@@ -247,11 +247,12 @@ def demodulateall(timestamp, data, *, init="auto", recenter=True, faintparam=Non
 
 def fit_windows(t, d, fc, fc_of_col, nwindow, *, state=None, omega=M_2PI, xinit=None,
                 recenter=True, fitoffsets=False, onlyhigh=False, maxfun=60, want_output=False,
-                n_gpus=1):
+                method="auto", n_gpus=1):
     """Every window of `nwindow` samples (Iterators.partition, the last one shorter) fitted as its
     own demodulateall call (src/GPPupilDemodulation.jl:204-205), all windows in one GPU call.
 
     t: (N,); d: (C, N) complex (row k = column k); fc: (G, N) raw FC rows; fc_of_col: (C,).
+    method: "auto" (harmonic moments per window; exact with fitoffsets), "exact", "harmonic".
     Returns params shaped (n_windows, C) (and the (C, N) demodulated rows when want_output)."""
     L = load()
     t = np.ascontiguousarray(t, dtype=np.float64)
@@ -270,7 +271,7 @@ def fit_windows(t, d, fc, fc_of_col, nwindow, *, state=None, omega=M_2PI, xinit=
     if st is not None and st.shape != (N,):
         raise ValueError("state and time must have the same number of lines")
     xi = None if xinit is None else np.ascontiguousarray(xinit, dtype=np.float64).reshape(2)
-    flags = GPD_METHOD_EXACT | (GPD_RECENTER if recenter else 0) | \
+    flags = _method_flags(method) | (GPD_RECENTER if recenter else 0) | \
         (GPD_FIT_OFFSETS if fitoffsets else 0) | (GPD_ONLY_HIGH if onlyhigh else 0)
     nwin = -(-N // nwindow)
     params = np.zeros(nwin * C, dtype=PARAM_DTYPE)
@@ -291,7 +292,8 @@ def window_length(timestamp, window):
 
 
 def demodulate_windows(timestamp, data, window, *, faintparam=None, onlyhigh=False,
-                       fitoffsets=False, preswitchdelay=0.01, postwitchdelay=0.3, n_gpus=1):
+                       fitoffsets=False, preswitchdelay=0.01, postwitchdelay=0.3, method="auto",
+                       n_gpus=1):
     """processmetrology's windowed branch (src/GPPupilDemodulation.jl:191-225) on the GPU:
     window (seconds) → nwindow samples; every window demodulated with its own fit.
 
@@ -314,7 +316,7 @@ def demodulate_windows(timestamp, data, window, *, faintparam=None, onlyhigh=Fal
     cols = np.ascontiguousarray(data.T)
     fop = np.array([fc_column_of(c) - 1 for c in range(1, 33)], dtype=np.int32)
     params, out = fit_windows(t, cols[:32], cols, fop, nwindow, state=state, fitoffsets=fitoffsets,
-                              onlyhigh=onlyhigh, want_output=True, n_gpus=n_gpus)
+                              onlyhigh=onlyhigh, want_output=True, method=method, n_gpus=n_gpus)
     output = data.copy()
     output[:, :32] = out.T
     return output, params, window_tables(params, N, nwindow, fitoffsets=fitoffsets)
@@ -359,7 +361,7 @@ def read_stefan_file(filename):
 
 
 def process_volt(timestamp, volt, *, offsets=None, window=None, faintparam=None, onlyhigh=False,
-                 preswitchdelay=0.01, postwitchdelay=0.3, init="auto", device=0):
+                 preswitchdelay=0.01, postwitchdelay=0.3, init="auto", method="auto", device=0):
     """processmetrology's numeric core (src/GPPupilDemodulation.jl:137-171, 191-244) straight from
     the FITS VOLT column on the GPU.
 
@@ -393,7 +395,7 @@ def process_volt(timestamp, volt, *, offsets=None, window=None, faintparam=None,
     nwindow = 0 if window is None else window_length(t, window)
     if window is not None and nwindow < 1:
         raise ValueError("window shorter than half a sample interval")
-    flags = GPD_RECENTER | (GPD_FIT_OFFSETS if fitoffsets else 0) | \
+    flags = _method_flags(method) | GPD_RECENTER | (GPD_FIT_OFFSETS if fitoffsets else 0) | \
         (GPD_ONLY_HIGH if onlyhigh else 0)
     nrec = 32 * (-(-N // nwindow) if nwindow else 1)
     params = np.zeros(nrec, dtype=PARAM_DTYPE)

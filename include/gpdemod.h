@@ -148,9 +148,10 @@ int gpd_chi2_batch_dev(int64_t n_samples, int64_t n_pixels, const double *t, con
  * arrays (as gpd_fit_batch, n_cols series columns); out_params has ceil(n_samples/window) ×
  * n_cols records, window-major (record w·n_cols + k = column k of window w); out_demod rows of
  * window w are demodulated with that window's parameters.  Per-window state statistics
- * (compute_mean_var_power on state[I]) and valid-sample counts follow the reference.  The
- * windows are fitted by the exact evaluator; METHOD_HARMONIC is rejected.  n_gpus > 1 splits
- * the windows across devices.
+ * (compute_mean_var_power on state[I]) and valid-sample counts follow the reference.  By
+ * default the windows are fitted from per-window harmonic moments (one workgroup per window ×
+ * column); with FIT_OFFSETS, or METHOD_EXACT, by the exact evaluator (METHOD_HARMONIC with
+ * FIT_OFFSETS is rejected here).  n_gpus > 1 splits the windows across devices.
  */
 int gpd_fit_windows(int64_t n_samples, int64_t window, int64_t n_cols, const double *t,
                     const gpd_c64 *d, int64_t ldd, const gpd_c64 *fc, int64_t n_fc, int64_t ldfc,

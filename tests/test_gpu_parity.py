@@ -72,6 +72,8 @@ def assert_fit_parity(got, ref, perturbed, label="", min_match=0.7, tol=TOL, max
     bad = np.nonzero(~explained)[0]
     detail = "; ".join(f"#{i}: got b={got['b'][i]:.9g} phi={got['phi'][i]:.9g} nfev={got['nfev'][i]}"
                        f" vs ref b={ref['b'][i]:.9g} phi={ref['phi'][i]:.9g} nfev={ref['nfev'][i]}"
+                       f" (dev " + " ".join(f"{k} {_dev(got[i:i + 1], ref[i:i + 1], k)[0]:.1e}"
+                                            for k in keys) + ")"
                        for i in bad[:3])
     assert explained.all(), msg + f" — unexplained series {bad}: {detail}"
     assert match.mean() >= min_match, msg

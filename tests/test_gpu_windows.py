@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 import synth
-from test_gpu_parity import assert_fit_parity, faint_states
+from test_gpu_parity import assert_fit_parity, faint_states, ulps_for
 
 NPERTURB = 24  # short windows: more outcomes per series to sample
 
@@ -33,16 +33,30 @@ def oracle_windows(oracle, B, nwindow, fop_rows, state=None, flags=None, ulps=1.
     return np.stack(ref), [np.stack(p) for p in pert]
 
 
-@pytest.mark.parametrize("N,nwindow", [(12000, 1500), (12345, 1500), (4000, 4000)])
-def test_windows_match_oracle(gpu, oracle, N, nwindow):
+@pytest.mark.parametrize("method", ["auto", "exact"])
+@pytest.mark.parametrize("N,nwindow", [(12000, 1500), (12345, 1500), (12250, 1500), (4000, 4000),
+                                      (6000, 200)])
+def test_windows_match_oracle(gpu, oracle, N, nwindow, method):
+    """auto: per-window harmonic moments (k_moments_win) — parity within the oracle's outcomes
+    under 128-ulp χ² noise, as for the whole-exposure harmonic path; windows (and a last
+    window) shorter than 256 samples are fitted exactly; exact: 1-ulp envelope."""
     B = exposure(N, seed=5)
     got, out = gpu.fit_windows(B["t"], B["d"], B["fc"], B["fc_of_pixel"], nwindow,
-                               want_output=True)
-    ref, pert = oracle_windows(oracle, B, nwindow, B["fc_of_pixel"])
+                               want_output=True, method=method)
+    ref, pert = oracle_windows(oracle, B, nwindow, B["fc_of_pixel"], ulps=ulps_for(method))
     assert got.shape == ref.shape == (-(-N // nwindow), 32)
-    assert np.all(got["status"] & gpu.GPD_ST_EXACT)
+    exact = (got["status"] & gpu.GPD_ST_EXACT) != 0
+    if method == "exact" or nwindow < 256:
+        assert np.all(exact)
+    else:
+        spans = np.minimum(nwindow, N - nwindow * np.arange(got.shape[0]))
+        assert np.all(exact[spans < 256])  # short last window: exact fallback
+        assert np.mean(~exact[spans >= 256]) > 0.9  # harmonic fits
+    # few-hundred-sample windows: the oracle's own outcomes under ulp noise spread beyond
+    # NEWUOA's rhoend (1e-3), so the bound on any landing point is relaxed there
     print(assert_fit_parity(got.reshape(-1), ref.reshape(-1), [p.reshape(-1) for p in pert],
-                            label=f"windows N={N} w={nwindow}"))
+                            label=f"windows {method} N={N} w={nwindow}",
+                            max_dev=1e-3 if min(nwindow, N % nwindow or nwindow) >= 500 else 1e-2))
     # output rows of window w use window w's parameters (src/GPPupilDemodulation.jl:207)
     for w in range(ref.shape[0]):
         I = slice(w * nwindow, min(N, (w + 1) * nwindow))
@@ -52,8 +66,9 @@ def test_windows_match_oracle(gpu, oracle, N, nwindow):
         assert np.max(np.abs(out[same][:, I] - refout[same])) <= 1e-9 * np.abs(B["d"]).max()
 
 
+@pytest.mark.parametrize("method", ["auto", "exact"])
 @pytest.mark.parametrize("onlyhigh", [False, True])
-def test_windows_faint(gpu, oracle, onlyhigh):
+def test_windows_faint(gpu, oracle, onlyhigh, method):
     """Per-window compute_mean_var_power on state[I] (faint mode, :205)."""
     N, nwindow = 9000, 3000
     B = exposure(N, seed=23)
@@ -61,11 +76,12 @@ def test_windows_faint(gpu, oracle, onlyhigh):
     power = np.where(st == 3, 1.1, np.where(st == 1, 0.3, 0.6))
     B["d"] = B["d"] * power[None, :]
     got = gpu.fit_windows(B["t"], B["d"], B["fc"], B["fc_of_pixel"], nwindow, state=st,
-                          onlyhigh=onlyhigh)
+                          onlyhigh=onlyhigh, method=method)
     flags = oracle.RECENTER | (oracle.ONLY_HIGH if onlyhigh else 0)
-    ref, pert = oracle_windows(oracle, B, nwindow, B["fc_of_pixel"], state=st, flags=flags)
+    ref, pert = oracle_windows(oracle, B, nwindow, B["fc_of_pixel"], state=st, flags=flags,
+                               ulps=ulps_for(method))
     print(assert_fit_parity(got.reshape(-1), ref.reshape(-1), [p.reshape(-1) for p in pert],
-                            label=f"faint windows onlyhigh={onlyhigh}"))
+                            label=f"faint windows {method} onlyhigh={onlyhigh}"))
 
 
 def test_windows_offsets_and_multi_gpu_split(gpu, oracle):
@@ -82,6 +98,13 @@ def test_windows_offsets_and_multi_gpu_split(gpu, oracle):
     # ulp noise, so the strict-match floor is lowered accordingly
     print(assert_fit_parity(got.reshape(-1), ref.reshape(-1), [p.reshape(-1) for p in pert],
                             label="offsets windows", min_match=0.5))
+
+
+def test_windows_harmonic_offsets_rejected(gpu):
+    B = synth.make_batch(2000, 4, seed=2)
+    with pytest.raises(gpu.GpdError):
+        gpu.fit_windows(B["t"], B["d"], B["fc"], B["fc_of_pixel"], 500, fitoffsets=True,
+                        method="harmonic")
 
 
 def test_demodulate_windows_api(gpu, oracle):
