@@ -46,6 +46,9 @@ def parse():
                     help="series in the CPU-oracle baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--storage", default="c64", choices=["c64", "c32"],
+                    help="c32: series/FC kept as ComplexF32 in HBM (FITS VOLT precision, "
+                         "gpd_fit_batch_c32_dev; arithmetic stays fp64)")
     return ap.parse_args()
 
 
@@ -82,26 +85,47 @@ def main():
     G = P // 4
     offset = shard.weak_offset(P, rank)
     # --- device-resident synthetic batch (untimed setup) -----------------------------------
+    c32 = args.storage == "c32"
     t = torch.empty(N, dtype=torch.float64, device=dev)
-    d = torch.empty((P, N, 2), dtype=torch.float64, device=dev)
-    fc = torch.empty((G, N, 2), dtype=torch.float64, device=dev)
     fcop = torch.empty(P, dtype=torch.int32, device=dev)
     truth = torch.empty((P, 64), dtype=torch.uint8, device=dev)
     params = torch.empty((P, 64), dtype=torch.uint8, device=dev)
-    rc = L.gpd_synth_fill_dev(N, P, offset, args.seed, args.t0, 0.002, 0.1, 0, gpd.M_2PI,
-                              t.data_ptr(), d.data_ptr(), N, fc.data_ptr(), N, fcop.data_ptr(),
-                              truth.data_ptr(), local, sptr)
-    gpd._lib.check(rc)
+    if not c32:
+        d = torch.empty((P, N, 2), dtype=torch.float64, device=dev)
+        fc = torch.empty((G, N, 2), dtype=torch.float64, device=dev)
+        rc = L.gpd_synth_fill_dev(N, P, offset, args.seed, args.t0, 0.002, 0.1, 0, gpd.M_2PI,
+                                  t.data_ptr(), d.data_ptr(), N, fc.data_ptr(), N,
+                                  fcop.data_ptr(), truth.data_ptr(), local, sptr)
+        gpd._lib.check(rc)
+    else:
+        # the same series generated in Float64 blocks of whole FC groups, rounded to ComplexF32
+        d = torch.empty((P, N, 2), dtype=torch.float32, device=dev)
+        fc = torch.empty((G, N, 2), dtype=torch.float32, device=dev)
+        blk = min(P, 8192)
+        d64 = torch.empty((blk, N, 2), dtype=torch.float64, device=dev)
+        f64 = torch.empty((blk // 4, N, 2), dtype=torch.float64, device=dev)
+        for c0 in range(0, P, blk):
+            nb = min(blk, P - c0)
+            rc = L.gpd_synth_fill_dev(N, nb, offset + c0, args.seed, args.t0, 0.002, 0.1, 0,
+                                      gpd.M_2PI, t.data_ptr(), d64.data_ptr(), N, f64.data_ptr(),
+                                      N, fcop[c0:].data_ptr(), truth[c0:].data_ptr(), local, sptr)
+            gpd._lib.check(rc)
+            d[c0:c0 + nb].copy_(d64[:nb])
+            fc[c0 // 4:(c0 + nb) // 4].copy_(f64[:nb // 4])
+        del d64, f64
+        fcop.copy_(torch.arange(P, device=dev, dtype=torch.int32) // 4)
     torch.cuda.synchronize(dev)
 
     flags = gpd.GPD_RECENTER | {"auto": 0, "exact": gpd.GPD_METHOD_EXACT,
                                 "harmonic": gpd.GPD_METHOD_HARMONIC}[args.method]
     err = ctypes.create_string_buffer(512)
 
+    fit_dev = L.gpd_fit_batch_c32_dev if c32 else L.gpd_fit_batch_dev
+
     def step():
-        r = L.gpd_fit_batch_dev(N, P, t.data_ptr(), d.data_ptr(), N, fc.data_ptr(), G, N,
-                                fcop.data_ptr(), None, gpd.M_2PI, None, flags, 60,
-                                params.data_ptr(), None, N, local, sptr, err, len(err))
+        r = fit_dev(N, P, t.data_ptr(), d.data_ptr(), N, fc.data_ptr(), G, N,
+                    fcop.data_ptr(), None, gpd.M_2PI, None, flags, 60,
+                    params.data_ptr(), None, N, local, sptr, err, len(err))
         gpd._lib.check(r, err)
         return shard.gather_records(params, world, rank)
 
@@ -139,7 +163,8 @@ def main():
     par = gathered[:P].cpu().numpy().reshape(-1).view(rec) if world > 1 else \
         params.cpu().numpy().reshape(-1).view(rec)
     roofline = None
-    algo_bytes = P * N * (16 + 16 / 4) + 8 * N  # d + FC phasor shared by 4 + t
+    esz = 8 if c32 else 16  # stored bytes per complex sample
+    algo_bytes = P * N * (esz + esz / 4) + 8 * N  # d + FC shared by 4 + t
     mom = kern.get("moments")
     if mom:
         avg_ms = float(np.mean(mom))
@@ -150,7 +175,8 @@ def main():
         tflops = mfma_flops / (avg_ms * 1e-3) / 1e12
         roofline = {"bound": "hbm", "kernel": "k_moments", "achieved": round(achieved, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": traffic_from_profiles(P, N), "algorithmic_bytes": algo_bytes,
+                    "traffic": traffic_from_profiles(P, N, args.storage),
+                    "algorithmic_bytes": algo_bytes,
                     "avg_ms": round(avg_ms, 3),
                     "mfma": {"achieved": round(tflops, 2), "peak": MFMA_F64_PEAK_TFLOPS,
                              "unit": "TFLOP/s", "frac": round(tflops / MFMA_F64_PEAK_TFLOPS, 4),
@@ -175,7 +201,8 @@ def main():
         "data": "synthetic (device-generated, seeded counter RNG; SURVEY §8d model)",
         "config": {"workload": "C3" if (P, N) == (100_000, 100_000) else f"{P}x{N}",
                    "series_per_gpu": P, "samples": N, "total_series": world * P,
-                   "method": args.method, "t0": args.t0, "parallelism": f"series-shard x{world}",
+                   "method": args.method, "t0": args.t0, "storage": args.storage,
+                   "parallelism": f"series-shard x{world}",
                    "gather": "RCCL gather of 64-B records to rank 0" if world > 1 else "none"},
         "roofline": roofline, "cpu_baseline": cpu, "kernels_ms": kernels, "fits": fits,
     }
@@ -184,10 +211,11 @@ def main():
         dist.destroy_process_group()
 
 
-def traffic_from_profiles(P, N):
+def traffic_from_profiles(P, N, storage="c64"):
     """HBM bytes per moment-kernel launch from the committed rocprofv3 PMC summary (FETCH_SIZE
     doubled per MI355X_MICROARCH.md §HBM + WRITE_SIZE), when it was taken on this shape."""
-    path = os.path.join(ROOT, "profiles", "pmc_moments.json")
+    path = os.path.join(ROOT, "profiles", "pmc_moments.json" if storage == "c64"
+                        else f"pmc_moments_{storage}.json")
     try:
         with open(path) as f:
             j = json.load(f)
@@ -208,8 +236,9 @@ def cpu_baseline(gpd, t, d, fc, fcop, par, args, N):
 
     k = min(args.cpu_pixels, d.shape[0]) // 4 * 4
     th = t.cpu().numpy()
-    dd = d[:k].cpu().numpy().view(np.complex128).reshape(k, N)
-    ff = fc[: k // 4].cpu().numpy().view(np.complex128).reshape(k // 4, N)
+    # Float64.(data) of the stored series (c32 storage: the widened ComplexF32 values)
+    dd = d[:k].double().cpu().numpy().view(np.complex128).reshape(k, N)
+    ff = fc[: k // 4].double().cpu().numpy().view(np.complex128).reshape(k // 4, N)
     fo = fcop[:k].cpu().numpy()
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
     t0 = time.perf_counter()

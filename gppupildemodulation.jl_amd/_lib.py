@@ -42,7 +42,8 @@ assert PARAM_DTYPE.itemsize == 64
 EXPORTS = ("gpd_version", "gpd_strerror", "gpd_device_count", "gpd_fit_batch",
            "gpd_fit_batch_dev", "gpd_chi2_batch", "gpd_chi2_batch_dev", "gpd_buildstates",
            "gpd_synth_fill_dev", "gpd_last_timings", "gpd_fit_windows", "gpd_fit_windows_dev",
-           "gpd_process_volt")
+           "gpd_process_volt", "gpd_fit_batch_c32", "gpd_fit_batch_c32_dev", "gpd_fit_windows_c32",
+           "gpd_fit_windows_c32_dev")
 
 
 class GpdError(RuntimeError):
@@ -86,6 +87,13 @@ def load():
     L.gpd_fit_windows.argtypes = win + [I32, ctypes.c_char_p, ctypes.c_size_t]
     L.gpd_fit_windows_dev.restype = ctypes.c_int
     L.gpd_fit_windows_dev.argtypes = win + [ctypes.c_int, V, ctypes.c_char_p, ctypes.c_size_t]
+    # Float32-storage variants: same argument lists (d / fc are ComplexF32 arrays)
+    for name, base in (("gpd_fit_batch_c32", "gpd_fit_batch"),
+                       ("gpd_fit_batch_c32_dev", "gpd_fit_batch_dev"),
+                       ("gpd_fit_windows_c32", "gpd_fit_windows"),
+                       ("gpd_fit_windows_c32_dev", "gpd_fit_windows_dev")):
+        getattr(L, name).restype = ctypes.c_int
+        getattr(L, name).argtypes = getattr(L, base).argtypes
     L.gpd_process_volt.restype = ctypes.c_int
     L.gpd_process_volt.argtypes = [I64, V, V, I64, V, V, D, V, U32, I32, I64, V, V, I64,
                                    ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]

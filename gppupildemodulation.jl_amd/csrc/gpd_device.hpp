@@ -19,6 +19,15 @@ struct c64 {
     double re, im;
 };
 
+// Julia ComplexF32 — FITS VOLT precision.  Series stored this way are widened to Float64 on
+// load (exact), so every evaluation sees the same values as Float64.(data).
+struct c32 {
+    float re, im;
+};
+
+__device__ __forceinline__ c64 widen(c32 z) { return {(double)z.re, (double)z.im}; }
+__device__ __forceinline__ c64 widen(c64 z) { return z; }
+
 __device__ __forceinline__ c64 cmul(c64 x, c64 y) {  // Base.:*(::ComplexF64, ::ComplexF64)
     return {x.re * y.re - x.im * y.im, x.re * y.im + x.im * y.re};
 }

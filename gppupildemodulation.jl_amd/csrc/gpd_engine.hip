@@ -24,6 +24,7 @@ using namespace gpd;
 
 static_assert(sizeof(Param) == sizeof(gpd_param), "gpd_param layout");
 static_assert(sizeof(c64) == sizeof(gpd_c64), "gpd_c64 layout");
+static_assert(sizeof(c32) == sizeof(gpd_c32), "gpd_c32 layout");
 
 namespace {
 
@@ -164,13 +165,14 @@ int gpd_device_count(void) {
 
 // Whole device pipeline.  bphi == nullptr: fit (gpd_fit_batch_dev); else evaluate χ² at
 // (bphi[2k], bphi[2k+1]) for every series (gpd_chi2_batch_dev).
-static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, const gpd_c64 *d,
-                        int64_t ldd, const gpd_c64 *fc, int64_t n_fc, int64_t ldfc,
+// is_c32: d and fc hold ComplexF32 elements (gpd_c32), widened to Float64 on load.
+static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, const void *d,
+                        int64_t ldd, const void *fc, int64_t n_fc, int64_t ldfc,
                         const int32_t *fc_of_pixel, const int8_t *state, double omega,
                         const double *xinit, uint32_t flags, int32_t maxfun,
                         gpd_param *out_params, gpd_c64 *out_demod, int64_t ldo,
                         const double *bphi, int device, void *stream_, char *errbuf,
-                        size_t errlen, int64_t window = 0) {
+                        size_t errlen, int64_t window = 0, bool is_c32 = false) {
     if (window < 0 || (window > 0 && bphi)) {
         set_err(errbuf, errlen, "gpd_fit_windows: window must be >= 0 (and fits only)");
         return GPD_E_ARG;
@@ -208,14 +210,15 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     const char *mk = getenv("GPD_MOMENTS");
     // buffer descriptors of the MFMA kernels address 128 series rows / the cos-sin table
     // with 32-bit offsets
+    const double esz = is_c32 ? 8.0 : 16.0;  // bytes per stored complex element
     const bool use_mfma = !(mk && std::string(mk) == "valu") &&
-                          (double)MM_PIX * (double)ldd * 16.0 < 2147483648.0 &&
+                          (double)MM_PIX * (double)ldd * esz < 2147483648.0 &&
                           (double)n_samples * KH * 16.0 < 2147483648.0;
     // Harmonic fitoffsets (non-faint, on request): the χ² of the 2×2 system needs the moments
     // G_n of the FC phasors (producer/consumer kernel in UNIT mode over the FC columns) and Σ d
     // per series.  METHOD_EXACT uses the exact evaluator; so do windows with fitoffsets.
     const bool harm_offs_ok =
-        !faint && use_mfma && (double)MM_PIX * (double)ldfc * 16.0 < 2147483648.0;
+        !faint && use_mfma && (double)MM_PIX * (double)ldfc * esz < 2147483648.0;
     // Offsets default to the exact evaluator: the 2×2 system is ill-conditioned for small b and
     // the flat landscape turns the expansion's ~1e-14 χ² rounding into ~1e-10 moves of NEWUOA's
     // iterate; METHOD_HARMONIC asks for the fast path anyway (parity ~1e-9).
@@ -279,9 +282,11 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     pb.N = N;
     pb.P = P;
     pb.t = t;
-    pb.d = (const c64 *)d;
+    pb.d = is_c32 ? nullptr : (const c64 *)d;
+    pb.d32 = is_c32 ? (const c32 *)d : nullptr;
     pb.ldd = ldd;
-    pb.fc = (const c64 *)fc;
+    pb.fc = is_c32 ? nullptr : (const c64 *)fc;
+    pb.fc32 = is_c32 ? (const c32 *)fc : nullptr;
     pb.ldfc = ldfc;
     pb.n_fc = n_fc;
     pb.fcop = fc_of_pixel;
@@ -331,8 +336,12 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             mark("moments_win");
         } else if (use_mfma) {
             dim3 g((unsigned)((P + MM_PIX - 1) / MM_PIX), (unsigned)L.nch);
-            if (faint)
+            if (faint && is_c32)
+                k_moments_mfma<true, c32><<<g, 256, 0, stream>>>(pb, tab, fstat, L.chunk, part);
+            else if (faint)
                 k_moments_mfma<true><<<g, 256, 0, stream>>>(pb, tab, fstat, L.chunk, part);
+            else if (is_c32)  // Float32 storage: the producer/consumer kernel on 8-B elements
+                k_moments_ws<0, false, c32><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
             else if (mk && std::string(mk) == "mfma1")  // single-role kernel (A/B runs)
                 k_moments_mfma<false><<<g, 256, 0, stream>>>(pb, tab, fstat, L.chunk, part);
             else if (mk && std::string(mk) == "ws_nomfma")  // timing experiments only
@@ -379,14 +388,18 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             k_iota<<<(unsigned)((n_fc + 255) / 256), 256, 0, stream>>>(fcid, n_fc);
             Problem pg = pb;
             pg.P = n_fc;
-            pg.d = (const c64 *)fc;
+            pg.d = pb.fc;
+            pg.d32 = pb.fc32;
             pg.ldd = ldfc;
             pg.fcop = fcid;
             pg.win = 0;
             pg.ncol = n_fc;
             double *partG = (double *)(ws + L.partG), *auxG = (double *)(ws + L.auxG);
             dim3 gG((unsigned)((n_fc + MM_PIX - 1) / MM_PIX), (unsigned)L.nch);
-            k_moments_ws<0, true><<<gG, 512, 0, stream>>>(pg, tab, L.chunk, partG);
+            if (is_c32)
+                k_moments_ws<0, true, c32><<<gG, 512, 0, stream>>>(pg, tab, L.chunk, partG);
+            else
+                k_moments_ws<0, true><<<gG, 512, 0, stream>>>(pg, tab, L.chunk, partG);
             dim3 grG((unsigned)((n_fc + 255) / 256), (unsigned)NMOM);
             k_reduce_moments<<<grG, 256, 0, stream>>>(partG, L.nch, n_fc, info, nullptr, 0, momG, auxG);
             k_series_sum<<<(unsigned)P, 256, 0, stream>>>(pb, d0);
@@ -441,7 +454,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     } else {
         if (phbuf) {
             dim3 g((unsigned)std::min<long long>((N + 255) / 256, 256), (unsigned)n_fc);
-            k_phasor<<<g, 256, 0, stream>>>((const c64 *)fc, ldfc, n_fc, N, ph);
+            k_phasor<<<g, 256, 0, stream>>>(pb, ph);
             mark("phasor");
         }
 #define GPD_LAUNCH_EXACT(FA, OF, PH)                                                                 \
@@ -519,6 +532,32 @@ int gpd_fit_windows_dev(int64_t n_samples, int64_t window, int64_t n_cols, const
                         errbuf, errlen, window);
 }
 
+int gpd_fit_batch_c32_dev(int64_t n_samples, int64_t n_pixels, const double *t, const gpd_c32 *d,
+                          int64_t ldd, const gpd_c32 *fc, int64_t n_fc, int64_t ldfc,
+                          const int32_t *fc_of_pixel, const int8_t *state, double omega,
+                          const double *xinit, uint32_t flags, int32_t maxfun,
+                          gpd_param *out_params, gpd_c64 *out_demod, int64_t ldo, int device,
+                          void *stream, char *errbuf, size_t errlen) {
+    return pipeline_dev(n_samples, n_pixels, t, d, ldd, fc, n_fc, ldfc, fc_of_pixel, state, omega,
+                        xinit, flags, maxfun, out_params, out_demod, ldo, nullptr, device, stream,
+                        errbuf, errlen, 0, true);
+}
+
+int gpd_fit_windows_c32_dev(int64_t n_samples, int64_t window, int64_t n_cols, const double *t,
+                            const gpd_c32 *d, int64_t ldd, const gpd_c32 *fc, int64_t n_fc,
+                            int64_t ldfc, const int32_t *fc_of_col, const int8_t *state,
+                            double omega, const double *xinit, uint32_t flags, int32_t maxfun,
+                            gpd_param *out_params, gpd_c64 *out_demod, int64_t ldo, int device,
+                            void *stream, char *errbuf, size_t errlen) {
+    if (window < 1) {
+        set_err(errbuf, errlen, "gpd_fit_windows_c32_dev: window must be >= 1");
+        return GPD_E_ARG;
+    }
+    return pipeline_dev(n_samples, n_cols, t, d, ldd, fc, n_fc, ldfc, fc_of_col, state, omega,
+                        xinit, flags, maxfun, out_params, out_demod, ldo, nullptr, device, stream,
+                        errbuf, errlen, window, true);
+}
+
 int gpd_last_timings(int device, const char **names, double *ms, int cap) {
     if (device < 0 || device >= gpd_device_count()) return 0;
     DevCtx *cx = ctx_for(device);
@@ -540,12 +579,14 @@ int gpd_last_timings(int device, const char **names, double *ms, int cap) {
 
 // Host-pointer driver: shard series over devices (one host thread per device), copy in, run the
 // device pipeline, copy out.  bphi (host, 2 per series) selects χ²-evaluation mode.
-static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, const gpd_c64 *d,
-                      int64_t ldd, const gpd_c64 *fc, int64_t n_fc, int64_t ldfc,
+static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, const void *d_,
+                      int64_t ldd, const void *fc_, int64_t n_fc, int64_t ldfc,
                       const int32_t *fc_of_pixel, const int8_t *state, double omega,
                       const double *xinit, uint32_t flags, int32_t maxfun, gpd_param *out_params,
                       gpd_c64 *out_demod, int64_t ldo, const double *bphi, int32_t n_gpus,
-                      char *errbuf, size_t errlen, int64_t window = 0) {
+                      char *errbuf, size_t errlen, int64_t window = 0, bool is_c32 = false) {
+    const size_t esz = is_c32 ? sizeof(gpd_c32) : sizeof(gpd_c64);  // stored element bytes
+    const char *d = (const char *)d_, *fc = (const char *)fc_;
     if (n_samples < 2 || n_pixels < 1 || !t || !d || !fc || !fc_of_pixel || !out_params ||
         ldd < n_samples || ldfc < n_samples || n_fc < 1 || (out_demod && ldo < n_samples) ||
         window < 0) {
@@ -597,7 +638,8 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
             return fail(GPD_E_HIP);
         }
         double *dt = nullptr;
-        c64 *dd = nullptr, *dfc = nullptr, *dout = nullptr;
+        char *dd = nullptr, *dfc = nullptr;
+        c64 *dout = nullptr;
         int32_t *dfcop = nullptr;
         int8_t *dst = nullptr;
         Param *dpar = nullptr;
@@ -633,8 +675,8 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
         for (auto &c : fcop_l) c -= cmin;
         bool ok = chk(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate") &&
                   chk(hipMalloc(&dt, N * sizeof(double)), "hipMalloc t") &&
-                  chk(hipMalloc(&dd, (size_t)P * N * sizeof(c64)), "hipMalloc d") &&
-                  chk(hipMalloc(&dfc, (size_t)nfc * N * sizeof(c64)), "hipMalloc fc") &&
+                  chk(hipMalloc(&dd, (size_t)P * N * esz), "hipMalloc d") &&
+                  chk(hipMalloc(&dfc, (size_t)nfc * N * esz), "hipMalloc fc") &&
                   chk(hipMalloc(&dfcop, P * sizeof(int32_t)), "hipMalloc fcop") &&
                   chk(hipMalloc(&dpar, nrec * sizeof(Param)), "hipMalloc params") &&
                   (!state || chk(hipMalloc(&dst, N), "hipMalloc state")) &&
@@ -646,11 +688,10 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
             return fail(GPD_E_OOM);
         }
         ok = chk(hipMemcpyAsync(dt, t + s0, N * sizeof(double), hipMemcpyHostToDevice, s), "H2D t") &&
-             chk(hipMemcpy2DAsync(dd, N * sizeof(c64), d + p0 * ldd + s0, ldd * sizeof(gpd_c64),
-                                  N * sizeof(c64), P, hipMemcpyHostToDevice, s), "H2D d") &&
-             chk(hipMemcpy2DAsync(dfc, N * sizeof(c64), fc + (int64_t)cmin * ldfc + s0,
-                                  ldfc * sizeof(gpd_c64), N * sizeof(c64), nfc,
-                                  hipMemcpyHostToDevice, s), "H2D fc") &&
+             chk(hipMemcpy2DAsync(dd, N * esz, d + (p0 * ldd + s0) * esz, ldd * esz, N * esz, P,
+                                  hipMemcpyHostToDevice, s), "H2D d") &&
+             chk(hipMemcpy2DAsync(dfc, N * esz, fc + ((int64_t)cmin * ldfc + s0) * esz,
+                                  ldfc * esz, N * esz, nfc, hipMemcpyHostToDevice, s), "H2D fc") &&
              chk(hipMemcpyAsync(dfcop, fcop_l.data(), P * sizeof(int32_t), hipMemcpyHostToDevice, s),
                  "H2D fcop") &&
              (!state || chk(hipMemcpyAsync(dst, state + s0, N, hipMemcpyHostToDevice, s), "H2D state")) &&
@@ -660,9 +701,9 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
             cleanup();
             return fail(GPD_E_HIP);
         }
-        int r = pipeline_dev(N, P, dt, (const gpd_c64 *)dd, N, (const gpd_c64 *)dfc, nfc, N, dfcop,
-                             dst, omega, xinit, flags, maxfun, (gpd_param *)dpar, (gpd_c64 *)dout, N,
-                             dbphi, g, s, errbuf_l, errlen_l, window);
+        int r = pipeline_dev(N, P, dt, dd, N, dfc, nfc, N, dfcop, dst, omega, xinit, flags, maxfun,
+                             (gpd_param *)dpar, (gpd_c64 *)dout, N, dbphi, g, s, errbuf_l,
+                             errlen_l, window, is_c32);
         if (r != GPD_OK) {
             cleanup();
             return fail(r);
@@ -730,6 +771,32 @@ int gpd_fit_windows(int64_t n_samples, int64_t window, int64_t n_cols, const dou
     return host_batch(n_samples, n_cols, t, d, ldd, fc, n_fc, ldfc, fc_of_col, state, omega,
                       xinit, flags, maxfun, out_params, out_demod, ldo, nullptr, n_gpus, errbuf,
                       errlen, window);
+}
+
+int gpd_fit_batch_c32(int64_t n_samples, int64_t n_pixels, const double *t, const gpd_c32 *d,
+                      int64_t ldd, const gpd_c32 *fc, int64_t n_fc, int64_t ldfc,
+                      const int32_t *fc_of_pixel, const int8_t *state, double omega,
+                      const double *xinit, uint32_t flags, int32_t maxfun, gpd_param *out_params,
+                      gpd_c64 *out_demod, int64_t ldo, int32_t n_gpus, char *errbuf,
+                      size_t errlen) {
+    return host_batch(n_samples, n_pixels, t, d, ldd, fc, n_fc, ldfc, fc_of_pixel, state, omega,
+                      xinit, flags, maxfun, out_params, out_demod, ldo, nullptr, n_gpus, errbuf,
+                      errlen, 0, true);
+}
+
+int gpd_fit_windows_c32(int64_t n_samples, int64_t window, int64_t n_cols, const double *t,
+                        const gpd_c32 *d, int64_t ldd, const gpd_c32 *fc, int64_t n_fc,
+                        int64_t ldfc, const int32_t *fc_of_col, const int8_t *state, double omega,
+                        const double *xinit, uint32_t flags, int32_t maxfun,
+                        gpd_param *out_params, gpd_c64 *out_demod, int64_t ldo, int32_t n_gpus,
+                        char *errbuf, size_t errlen) {
+    if (window < 1) {
+        set_err(errbuf, errlen, "gpd_fit_windows_c32: window must be >= 1");
+        return GPD_E_ARG;
+    }
+    return host_batch(n_samples, n_cols, t, d, ldd, fc, n_fc, ldfc, fc_of_col, state, omega,
+                      xinit, flags, maxfun, out_params, out_demod, ldo, nullptr, n_gpus, errbuf,
+                      errlen, window, true);
 }
 
 int gpd_process_volt(int64_t n_samples, const double *t, const float *volt, int64_t ldv,

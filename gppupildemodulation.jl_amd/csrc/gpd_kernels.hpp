@@ -55,9 +55,13 @@ struct Info {
 struct Problem {
     long long N, P;
     const double *__restrict__ t;
+    // series and FC columns: Float64 complex (d, fc) or Float32 complex as stored in the FITS
+    // VOLT column (d32, fc32; the other pointer is null); ldd / ldfc count elements
     const c64 *__restrict__ d;
+    const c32 *__restrict__ d32;
     long long ldd;
     const c64 *__restrict__ fc;
+    const c32 *__restrict__ fc32;
     long long ldfc, n_fc;
     const int32_t *__restrict__ fcop;
     const int8_t *__restrict__ state;  // nullptr: non-faint
@@ -81,6 +85,25 @@ __device__ __forceinline__ Span span_of(const Problem &pb, long long k) {
     const long long w = k / pb.ncol;
     const long long s0 = w * pb.win;
     return {k - w * pb.ncol, s0, s0 + pb.win < pb.N ? s0 + pb.win : pb.N};
+}
+
+// Element `off` of the series / FC storage, widened to Float64 (uniform branch on the type).
+__device__ __forceinline__ c64 d_at(const Problem &pb, long long off) {
+    return pb.d32 ? widen(pb.d32[off]) : pb.d[off];
+}
+__device__ __forceinline__ c64 fc_at(const Problem &pb, long long off) {
+    return pb.fc32 ? widen(pb.fc32[off]) : pb.fc[off];
+}
+// Typed base pointers for the kernels instantiated per storage type TS (c64 or c32).
+template <class TS>
+__device__ __forceinline__ const TS *d_base(const Problem &pb) {
+    if constexpr (sizeof(TS) == 8) return pb.d32;
+    else return pb.d;
+}
+template <class TS>
+__device__ __forceinline__ const TS *fc_base(const Problem &pb) {
+    if constexpr (sizeof(TS) == 8) return pb.fc32;
+    else return pb.fc;
 }
 
 __device__ __forceinline__ bool sample_valid(const Problem &pb, long long i, int &st) {
@@ -256,14 +279,14 @@ __global__ __launch_bounds__(256) void k_faint_stats(Problem pb, double *__restr
     __shared__ double lds[4 * 15];
     const long long k = blockIdx.x;
     const Span sp = span_of(pb, k);  // per window: compute_mean_var_power on state[I] (:205)
-    const c64 *d = pb.d + sp.col * pb.ldd;
+    const long long doff = sp.col * pb.ldd;
     double v[15];
 #pragma unroll
     for (int q = 0; q < 15; ++q) v[q] = 0.0;
     for (long long i = sp.s0 + threadIdx.x; i < sp.s1; i += 256) {
         int st;
         if (!sample_valid(pb, i, st)) continue;
-        const c64 z = d[i];
+        const c64 z = d_at(pb, doff + i);
         const double ad = hypot(z.re, z.im);
         const double d2 = z.re * z.re + z.im * z.im;
 #pragma unroll
@@ -282,7 +305,7 @@ __global__ __launch_bounds__(256) void k_faint_stats(Problem pb, double *__restr
     for (long long i = sp.s0 + threadIdx.x; i < sp.s1; i += 256) {
         int st;
         if (!sample_valid(pb, i, st)) continue;
-        const c64 z = d[i];
+        const c64 z = d_at(pb, doff + i);
         const double ad = hypot(z.re, z.im);
 #pragma unroll
         for (int q = 0; q < 5; ++q)
@@ -313,11 +336,10 @@ __global__ __launch_bounds__(256) void k_faint_stats(Problem pb, double *__restr
 
 // ---------------------------------------------------------------------------------------
 // k_phasor: FC phasor buffer for the exact evaluator (only when it fits the workspace).
-__global__ __launch_bounds__(256) void k_phasor(const c64 *__restrict__ fc, long long ldfc,
-                                                long long n_fc, long long N, c64 *__restrict__ ph) {
-    const long long g = blockIdx.y;
+__global__ __launch_bounds__(256) void k_phasor(Problem pb, c64 *__restrict__ ph) {
+    const long long g = blockIdx.y, N = pb.N;
     for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < N; i += (long long)gridDim.x * 256)
-        ph[g * N + i] = fc_phasor(fc[g * ldfc + i]);
+        ph[g * N + i] = fc_phasor(fc_at(pb, g * pb.ldfc + i));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -358,8 +380,8 @@ __global__ __launch_bounds__(64) void k_moments(Problem pb, const double *__rest
             const int prow = lp + r * (64 / MOM_TS);
             c64 dv = {0.0, 0.0}, pv = {0.0, 0.0};
             if (pp < pb.P && ss < s_end) {
-                dv = pb.d[pp * pb.ldd + ss];
-                const c64 z = pb.fc[(long long)pb.fcop[pp] * pb.ldfc + ss];
+                dv = d_at(pb, pp * pb.ldd + ss);
+                const c64 z = fc_at(pb, (long long)pb.fcop[pp] * pb.ldfc + ss);
                 const double r2 = z.re * z.re + z.im * z.im;
                 if (r2 > 0.0) {
                     const double inv = 1.0 / sqrt(r2);
@@ -457,7 +479,17 @@ constexpr int MM_GRP = MM_PIX / 4; // FC groups per workgroup
 
 __device__ __forceinline__ int mm_phys(int p, int s) { return s * MM_ROW + (p ^ ((s & 1) << 3)); }
 
-template <bool FAINT>
+// One complex element of storage type TS (c64: 16 B, c32: 8 B) through a buffer descriptor;
+// kept in its storage type until staged (widening at the load would wait on it there).
+template <class TS>
+__device__ __forceinline__ TS buf_ld(__amdgpu_buffer_rsrc_t rs, int voff) {
+    if constexpr (sizeof(TS) == 16)
+        return __builtin_bit_cast(TS, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0));
+    else
+        return __builtin_bit_cast(TS, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, 0, 0));
+}
+
+template <bool FAINT, class TS = c64>
 __global__ __launch_bounds__(256, 2) void k_moments_mfma(Problem pb, const double *__restrict__ tab,
                                                          const double *__restrict__ fstat,
                                                          long long chunk_len,
@@ -498,14 +530,15 @@ __global__ __launch_bounds__(256, 2) void k_moments_mfma(Problem pb, const doubl
     // series rows of this workgroup through one buffer descriptor (wave-uniform base and size,
     // T8/T20): per-thread voffset + per-load scalar soffset, out-of-range rows read as 0.
     const long long nrows = (pb.P - p0) < MM_PIX ? (pb.P - p0) : MM_PIX;
-    const unsigned dbytes = __builtin_amdgcn_readfirstlane((unsigned)(nrows * ldd * 16));
+    constexpr int ES = (int)sizeof(TS);
+    const unsigned dbytes = __builtin_amdgcn_readfirstlane((unsigned)(nrows * ldd * ES));
     const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
-        uniform_ptr(pb.d + p0 * ldd), (short)0, (int)dbytes, 0x00020000);
-    const int dvoff = (int)((4 * gq * ldd + ss) * 16);
-    const int ldd16 = __builtin_amdgcn_readfirstlane((int)(ldd * 16));
-    const c64 *fcp[4];
+        uniform_ptr(d_base<TS>(pb) + p0 * ldd), (short)0, (int)dbytes, 0x00020000);
+    const int dvoff = (int)((4 * gq * ldd + ss) * ES);
+    const int ldd16 = __builtin_amdgcn_readfirstlane((int)(ldd * ES));
+    const TS *fcp[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) fcp[r] = pb.fc + (long long)gcol[r] * ldfc + ss;
+    for (int r = 0; r < 4; ++r) fcp[r] = fc_base<TS>(pb) + (long long)gcol[r] * ldfc + ss;
     // ---- MFMA role
     const int fi = lane & 15, fk = lane >> 4, comp = fi & 1, ppair = fi >> 1;
     v4d acc[4][3];
@@ -516,21 +549,17 @@ __global__ __launch_bounds__(256, 2) void k_moments_mfma(Problem pb, const doubl
         for (int n = 0; n < 3; ++n) acc[m][n] = (v4d){0.0, 0.0, 0.0, 0.0};
 
     // ---- prefetch registers (one tile ahead)
-    c64 rd[4][4], rf[4];
+    TS rd[4][4], rf[4];
     double2 rt[3];
     auto issue = [&](long long s0) {
         const bool in = s0 + ss < s_end;
-        const int s016 = (int)(s0 * 16);
+        const int s016 = (int)(s0 * ES);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            rf[r] = in ? fcp[r][s0] : c64{0.0, 0.0};
+            rf[r] = in ? fcp[r][s0] : TS{0, 0};
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                // every offset part in voffset: the range check ignores soffset
-                const auto v = __builtin_amdgcn_raw_buffer_load_b128(
-                    drs, dvoff + (32 * r + j) * ldd16 + s016, 0, 0);
-                rd[r][j] = __builtin_bit_cast(c64, v);
-            }
+            for (int j = 0; j < 4; ++j)  // every offset part in voffset: the range check ignores soffset
+                rd[r][j] = buf_ld<TS>(drs, dvoff + (32 * r + j) * ldd16 + s016);
         }
         // cos/sin rows: MM_TS × 48 doubles = 768 double2, 3 per thread
         const double2 *trow = (const double2 *)tab + s0 * KH;
@@ -548,7 +577,7 @@ __global__ __launch_bounds__(256, 2) void k_moments_mfma(Problem pb, const doubl
         const bool sok = (s < s_end) && sample_valid(pb, s, st);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const c64 z = rf[r];
+            const c64 z = widen(rf[r]);
             const double r2 = z.re * z.re + z.im * z.im;
             c64 ph = {1.0, 0.0};  // angle(0) = 0
             if (r2 > 0.0) {
@@ -560,7 +589,7 @@ __global__ __launch_bounds__(256, 2) void k_moments_mfma(Problem pb, const doubl
                 const int pl = 4 * (gq + 8 * r) + j;  // series within the workgroup
                 c64 pj = ph;
                 if (ownmask & (1u << (4 * r + j))) {  // general fc_of_pixel: own FC column
-                    const c64 zz = pb.fc[(long long)fcl[pl] * ldfc + s];
+                    const c64 zz = fc_at(pb, (long long)fcl[pl] * ldfc + s);
                     const double rr = zz.re * zz.re + zz.im * zz.im;
                     pj = {1.0, 0.0};
                     if (rr > 0.0) {
@@ -568,7 +597,7 @@ __global__ __launch_bounds__(256, 2) void k_moments_mfma(Problem pb, const doubl
                         pj = {zz.re * iv, zz.im * iv};
                     }
                 }
-                const c64 dv = rd[r][j];
+                const c64 dv = widen(rd[r][j]);
                 c64 q;
                 q.re = fma(pj.re, dv.re, pj.im * dv.im);
                 q.im = fma(pj.re, dv.im, -(pj.im * dv.re));
@@ -659,15 +688,16 @@ struct BoolTag {
     static constexpr bool value = B;
 };
 
+template <class TS>
 struct WsRegs {
-    c64 d[4][4], f[4];
+    TS d[4][4], f[4];
 };
 
 // DBG (timing experiments only, results invalid): 1 = consumers skip the MFMA phase,
 // 2 = producers skip the global loads, 5 = producers only keep the barrier cadence.
 // UNIT: the series are FC columns and d ≡ 1, i.e. the moments G_n = Σ p̄ e^{-jnx} of the
 // unit phasors (harmonic fitoffsets: Σ w m = conj(Σ_n J_n(b) e^{-jnϕ} G_n)).
-template <int DBG = 0, bool UNIT = false>
+template <int DBG = 0, bool UNIT = false, class TS = c64>
 __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double *__restrict__ tab,
                                                        long long chunk_len,
                                                        double *__restrict__ part) {
@@ -700,14 +730,15 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
         const int ss = ptid & 31, gq = ptid >> 5;
         const long long ldd = pb.ldd, ldfc = pb.ldfc, Nm1 = pb.N - 1;
         const long long nrows = (pb.P - p0) < MM_PIX ? (pb.P - p0) : MM_PIX;
-        const unsigned dbytes = __builtin_amdgcn_readfirstlane((unsigned)(nrows * ldd * 16));
+        constexpr int ES = (int)sizeof(TS);
+        const unsigned dbytes = __builtin_amdgcn_readfirstlane((unsigned)(nrows * ldd * ES));
         const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
-            uniform_ptr(pb.d + p0 * ldd), (short)0, (int)dbytes, 0x00020000);
-        const int dvoff = (int)((4 * gq * ldd + ss) * 16);
-        const int ldd16 = __builtin_amdgcn_readfirstlane((int)(ldd * 16));
-        const c64 *fcb[4];
+            uniform_ptr(d_base<TS>(pb) + p0 * ldd), (short)0, (int)dbytes, 0x00020000);
+        const int dvoff = (int)((4 * gq * ldd + ss) * ES);
+        const int ldd16 = __builtin_amdgcn_readfirstlane((int)(ldd * ES));
+        const TS *fcb[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) fcb[r] = pb.fc + (long long)fcl[4 * (gq + 8 * r)] * ldfc;
+        for (int r = 0; r < 4; ++r) fcb[r] = fc_base<TS>(pb) + (long long)fcl[4 * (gq + 8 * r)] * ldfc;
         // cos/sin tile: MM_TS rows × KH double2; this thread's slots e = ptid + 256 u, read
         // through a buffer descriptor (rows ≥ N read as 0; keeps the loads where they are issued
         // — plain loads of the read-only table would be sunk to their use past the barrier)
@@ -716,18 +747,18 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             0x00020000);
         const int tvoff = ptid * 16;  // slot e = ptid + 256 u of a tile starting at row s0
 
-        auto issue = [&](WsRegs &R, int it) {
+        auto issue = [&](WsRegs<TS> &R, int it) {
             if constexpr (DBG == 2 || DBG == 5) {
                 for (int r = 0; r < 4; ++r) {
-                    R.f[r] = c64{1.0 + it, 0.0};
-                    for (int j = 0; j < 4; ++j) R.d[r][j] = c64{0.5 * it, 1.0};
+                    R.f[r] = TS{1.0f + it, 0};
+                    for (int j = 0; j < 4; ++j) R.d[r][j] = TS{0.5f * it, 1};
                 }
                 return;
             }
             it = it < ntiles ? it : ntiles - 1;
             const long long s0 = s_begin + (long long)it * MM_TS;
             const long long sl = (s0 + ss) < Nm1 ? (s0 + ss) : Nm1;
-            const int s016 = (int)(s0 * 16);
+            const int s016 = (int)(s0 * ES);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 R.f[r] = fcb[r][sl];
@@ -736,9 +767,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
                     if constexpr (UNIT) continue;
                     // all offset parts in voffset (the range check ignores soffset): rows
                     // beyond P and samples beyond the last row read as 0
-                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(
-                        drs, dvoff + (32 * r + j) * ldd16 + s016, 0, 0);
-                    R.d[r][j] = __builtin_bit_cast(c64, v);
+                    R.d[r][j] = buf_ld<TS>(drs, dvoff + (32 * r + j) * ldd16 + s016);
                 }
             }
         };
@@ -757,21 +786,21 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             T2 = __builtin_bit_cast(double2,
                                     __builtin_amdgcn_raw_buffer_load_b128(trs, vo + 8192, 0, 0));
         };
-        auto stage_q = [&](const WsRegs &R, int it, auto gen, auto partial) {
+        auto stage_q = [&](const WsRegs<TS> &R, int it, auto gen, auto partial) {
             const long long s = s_begin + (long long)it * MM_TS + ss;
             const bool sok = s < s_end;
             const long long sl = s < Nm1 ? s : Nm1;
             c64 *q_out = qs[it & 1];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const c64 ph = unit_phasor(R.f[r]);
+                const c64 ph = unit_phasor(widen(R.f[r]));
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int pl = 4 * (gq + 8 * r) + j;
                     c64 pj = ph;
                     if (decltype(gen)::value)  // general layout: the series' own FC column
-                        pj = unit_phasor(pb.fc[(long long)fcl[pl] * ldfc + sl]);
-                    const c64 dv = UNIT ? c64{1.0, 0.0} : R.d[r][j];
+                        pj = unit_phasor(fc_at(pb, (long long)fcl[pl] * ldfc + sl));
+                    const c64 dv = UNIT ? c64{1.0, 0.0} : widen(R.d[r][j]);
                     c64 q;
                     q.re = fma(pj.re, dv.re, pj.im * dv.im);
                     q.im = fma(pj.re, dv.im, -(pj.im * dv.re));
@@ -783,7 +812,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
                 }
             }
         };
-        auto stage = [&](const WsRegs &R, int it, auto gen) {
+        auto stage = [&](const WsRegs<TS> &R, int it, auto gen) {
             if (it >= ntiles) return;
             if constexpr (DBG == 5) return;
             // only a chunk's last tile can be partial (chunks are whole tiles, N may not be)
@@ -806,7 +835,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             return 0;
         };
         auto run = [&](auto gen) {
-            WsRegs R0, R1;
+            WsRegs<TS> R0, R1;
             issue(R0, 0);
             issue_t(0);
             issue(R1, 1);
@@ -988,8 +1017,7 @@ __global__ __launch_bounds__(256) void k_moments_win(Problem pb, const double *_
     const Span sp = span_of(pb, k);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int hg = wave * 2 + (lane >> 5), sl = lane & 31;  // hg 0..7 → harmonics 3hg+1..3hg+3
-    const c64 *d = pb.d + sp.col * pb.ldd;
-    const c64 *fcol = pb.fc + (long long)pb.fcop[sp.col] * pb.ldfc;
+    const long long doff = sp.col * pb.ldd, foff = (long long)pb.fcop[sp.col] * pb.ldfc;
     double wm[5] = {0, 0, 0, 0, 0};
     if (FAINT) {
 #pragma unroll
@@ -1001,8 +1029,8 @@ __global__ __launch_bounds__(256) void k_moments_win(Problem pb, const double *_
     for (long long i = sp.s0 + sl; i < sp.s1; i += 32) {
         int st = 0;
         if (FAINT && !sample_valid(pb, i, st)) continue;
-        const c64 ph = unit_phasor(fcol[i]);
-        const c64 dv = d[i];
+        const c64 ph = unit_phasor(fc_at(pb, foff + i));
+        const c64 dv = d_at(pb, doff + i);
         double qr = fma(ph.re, dv.re, ph.im * dv.im);  // q = w m p̄ d
         double qi = fma(ph.re, dv.im, -(ph.im * dv.re));
         if (FAINT) {
@@ -1240,8 +1268,8 @@ __global__ __launch_bounds__(64) void k_fit_harmonic(Problem pb, const Info *__r
 template <bool FAINT, bool OFFS, bool PHBUF>
 struct ExactChi2 {
     const Problem *pb;
-    const c64 *__restrict__ d;
-    const c64 *__restrict__ src;  // PHBUF: phasor column; else raw FC column (setup_exact)
+    long long doff, foff;         // series column / raw FC column offsets (setup_exact)
+    const c64 *__restrict__ src;  // PHBUF: phasor column
     double *lds;
     double m5[5], w5[5];
     double nvalid;
@@ -1252,7 +1280,7 @@ struct ExactChi2 {
     __device__ __forceinline__ bool load(long long i, c64 &p, double &w) const {
         int st;
         if (!sample_valid(*pb, i, st)) return false;
-        const c64 ph = PHBUF ? src[i] : fc_phasor(src[i]);
+        const c64 ph = PHBUF ? src[i] : fc_phasor(fc_at(*pb, foff + i));
         if (FAINT) {
             double m = m5[0], ww = w5[0];
 #pragma unroll
@@ -1285,7 +1313,7 @@ struct ExactChi2 {
                 double w;
                 if (!load(i, p, w)) continue;
                 const c64 m = model(i, p, b, phi);
-                const c64 dd = d[i];
+                const c64 dd = d_at(*pb, doff + i);
                 v[0] += w;
                 v[1] += w * m.re;
                 v[2] += w * m.im;
@@ -1318,7 +1346,7 @@ struct ExactChi2 {
                 if (!load(i, p, w)) continue;
                 const c64 m = model(i, p, b, phi);
                 const c64 mwc = {m.re * w, -(m.im * w)};  // conj(model .* weight)
-                const c64 xx = cmul(mwc, d[i]);
+                const c64 xx = cmul(mwc, d_at(*pb, doff + i));
                 const c64 yy = cmul(mwc, m);
                 v[0] += xx.re;
                 v[1] += xx.im;
@@ -1343,7 +1371,7 @@ struct ExactChi2 {
                 mm.re = c_re + mm.re;
                 mm.im = c_im + mm.im;
             }
-            const c64 dd = d[i];
+            const c64 dd = d_at(*pb, doff + i);
             const double rr = mm.re - dd.re, ri = mm.im - dd.im;
             s[0] += w * (rr * rr + ri * ri);
         }
@@ -1360,9 +1388,10 @@ __device__ __forceinline__ void setup_exact(F &f, const Problem &pb, long long k
                                             double nvalid_all) {
     const Span sp = span_of(pb, k);
     f.pb = &pb;
-    f.d = pb.d + sp.col * pb.ldd;
+    f.doff = sp.col * pb.ldd;
     const long long g = pb.fcop[sp.col];
-    f.src = phbuf ? phbuf + g * pb.N : pb.fc + g * pb.ldfc;
+    f.foff = g * pb.ldfc;
+    f.src = phbuf ? phbuf + g * pb.N : nullptr;
     f.lds = lds;
     f.s0 = sp.s0;
     f.s1 = sp.s1;
@@ -1531,13 +1560,14 @@ __global__ __launch_bounds__(256) void k_series_sum(Problem pb, double *__restri
     __shared__ double lds[4 * 2];
     const long long k = blockIdx.x;
     const Span sp = span_of(pb, k);
-    const c64 *d = pb.d + sp.col * pb.ldd;
+    const long long doff = sp.col * pb.ldd;
     double v[2] = {0.0, 0.0};
     for (long long i = sp.s0 + threadIdx.x; i < sp.s1; i += 256) {
         int st;
         if (!sample_valid(pb, i, st)) continue;
-        v[0] += d[i].re;
-        v[1] += d[i].im;
+        const c64 z = d_at(pb, doff + i);
+        v[0] += z.re;
+        v[1] += z.im;
     }
     block_sum<256, 2>(v, lds);
     if (threadIdx.x == 0) {
@@ -1556,13 +1586,13 @@ __global__ __launch_bounds__(256) void k_output(Problem pb, const Param *__restr
     const double arga = atan2(pk.a_im, pk.a_re);
     const c64 aa = {pk.a_re, pk.a_im};
     const bool offs = (pb.flags & F_OFFSETS) != 0;
-    const c64 *d = pb.d + sp.col * pb.ldd;
+    const long long doff = sp.col * pb.ldd;
     c64 *o = outd + sp.col * ldo;
     for (long long i = sp.s0 + (long long)blockIdx.x * 256 + threadIdx.x; i < sp.s1;
          i += (long long)gridDim.x * 256) {
         double th = pb.omega * pb.t[i];
         th = th + phi;
-        c64 dd = d[i];
+        c64 dd = d_at(pb, doff + i);
         if (pb.flags & F_RECENTER) {
             double ph = b * sin(th);  // getphase (src/Modulation.jl:66-69)
             ph = ph + arga;

@@ -124,19 +124,31 @@ def _method_flags(method: str) -> int:
     raise ValueError(f"method must be auto|exact|harmonic, got {method!r}")
 
 
+def _storage(d, fc):
+    """Series and FC rows in their stored precision: both complex64 (Matrix{ComplexF32}, the
+    FITS VOLT precision) → the Float32-storage entry points, which widen on load and compute in
+    Float64; anything else → complex128."""
+    d = np.asarray(d)
+    fc = np.asarray(fc)
+    if d.dtype == np.complex64 and fc.dtype == np.complex64:
+        return np.ascontiguousarray(d), np.ascontiguousarray(fc), True
+    return (np.ascontiguousarray(d, dtype=np.complex128),
+            np.ascontiguousarray(fc, dtype=np.complex128), False)
+
+
 def fit_batch(t, d, fc, fc_of_pixel, *, state=None, omega=M_2PI, xinit=None, recenter=True,
               fitoffsets=False, onlyhigh=False, maxfun=60, want_output=False, method="auto",
               n_gpus=1):
     """Batch fit of P series on the GPU.
 
-    t: (N,) float64; d: (P, N) complex128 (row k = series k); fc: (G, N) complex128 raw FC
-    columns; fc_of_pixel: (P,) int (0-based row of fc).  Returns a PARAM_DTYPE record array
-    (and the (P, N) demodulated series when want_output).
+    t: (N,) float64; d: (P, N) complex (row k = series k); fc: (G, N) complex raw FC
+    columns; fc_of_pixel: (P,) int (0-based row of fc).  complex64 d and fc are kept in Float32
+    in device memory (gpd_fit_batch_c32), anything else is taken as complex128.  Returns a
+    PARAM_DTYPE record array (and the (P, N) complex128 demodulated series when want_output).
     """
     L = load()
     t = np.ascontiguousarray(t, dtype=np.float64)
-    d = np.ascontiguousarray(d, dtype=np.complex128)
-    fc = np.ascontiguousarray(fc, dtype=np.complex128)
+    d, fc, c32 = _storage(d, fc)
     fop = np.ascontiguousarray(fc_of_pixel, dtype=np.int32)
     if d.ndim != 2 or fc.ndim != 2 or d.shape[1] != t.size or fc.shape[1] != t.size:
         raise ValueError("voltage and time must have the same number of lines")  # src/Modulation.jl:258
@@ -163,9 +175,9 @@ def fit_batch(t, d, fc, fc_of_pixel, *, state=None, omega=M_2PI, xinit=None, rec
     params = np.zeros(P, dtype=PARAM_DTYPE)
     out = np.zeros((P, N), dtype=np.complex128) if want_output else None
     err = ctypes.create_string_buffer(512)
-    rc = L.gpd_fit_batch(N, P, ptr(t), ptr(d), N, ptr(fc), fc.shape[0], N, ptr(fop), ptr(st),
-                         float(omega), ptr(xi), flags, int(maxfun), ptr(params), ptr(out), N,
-                         int(n_gpus), err, len(err))
+    fn = L.gpd_fit_batch_c32 if c32 else L.gpd_fit_batch
+    rc = fn(N, P, ptr(t), ptr(d), N, ptr(fc), fc.shape[0], N, ptr(fop), ptr(st), float(omega),
+            ptr(xi), flags, int(maxfun), ptr(params), ptr(out), N, int(n_gpus), err, len(err))
     check(rc, err)
     return (params, out) if want_output else params
 
@@ -209,7 +221,8 @@ def demodulateall(timestamp, data, *, init="auto", recenter=True, faintparam=Non
     data = np.asarray(data)
     if not np.iscomplexobj(data):
         raise TypeError("data must be a complex matrix (AbstractMatrix{Complex{T}})")
-    data = data.astype(np.complex128, copy=False)
+    if data.dtype != np.complex64:  # Matrix{ComplexF32} stays Float32 in device memory
+        data = data.astype(np.complex128, copy=False)
     if data.ndim != 2 or data.shape[1] != 40:
         raise ValueError("data must be N×40 (32 diodes + 8 FC columns)")
     N = data.shape[0]
@@ -232,7 +245,8 @@ def demodulateall(timestamp, data, *, init="auto", recenter=True, faintparam=Non
     params, out = fit_batch(t, cols[:32], cols, fop, state=state, xinit=xinit, recenter=recenter,
                             fitoffsets=fitoffsets, onlyhigh=onlyhigh, want_output=True,
                             method=method, n_gpus=n_gpus)
-    output = data.copy()  # output = copy(data): FC columns pass through (src/Modulation.jl:353)
+    # output = copy(data): FC columns pass through, eltype of data (src/Modulation.jl:353)
+    output = data.copy()
     output[:, :32] = out.T
     param = []
     for p in params:
@@ -251,13 +265,13 @@ def fit_windows(t, d, fc, fc_of_col, nwindow, *, state=None, omega=M_2PI, xinit=
     """Every window of `nwindow` samples (Iterators.partition, the last one shorter) fitted as its
     own demodulateall call (src/GPPupilDemodulation.jl:204-205), all windows in one GPU call.
 
-    t: (N,); d: (C, N) complex (row k = column k); fc: (G, N) raw FC rows; fc_of_col: (C,).
+    t: (N,); d: (C, N) complex (row k = column k); fc: (G, N) raw FC rows; fc_of_col: (C,);
+    complex64 d and fc stay Float32 in device memory (gpd_fit_windows_c32).
     method: "auto" (harmonic moments per window; exact with fitoffsets), "exact", "harmonic".
     Returns params shaped (n_windows, C) (and the (C, N) demodulated rows when want_output)."""
     L = load()
     t = np.ascontiguousarray(t, dtype=np.float64)
-    d = np.ascontiguousarray(d, dtype=np.complex128)
-    fc = np.ascontiguousarray(fc, dtype=np.complex128)
+    d, fc, c32 = _storage(d, fc)
     fop = np.ascontiguousarray(fc_of_col, dtype=np.int32)
     if d.ndim != 2 or fc.ndim != 2 or d.shape[1] != t.size or fc.shape[1] != t.size:
         raise ValueError("voltage and time must have the same number of lines")
@@ -277,9 +291,10 @@ def fit_windows(t, d, fc, fc_of_col, nwindow, *, state=None, omega=M_2PI, xinit=
     params = np.zeros(nwin * C, dtype=PARAM_DTYPE)
     out = np.zeros((C, N), dtype=np.complex128) if want_output else None
     err = ctypes.create_string_buffer(512)
-    rc = L.gpd_fit_windows(N, nwindow, C, ptr(t), ptr(d), N, ptr(fc), fc.shape[0], N, ptr(fop),
-                           ptr(st), float(omega), ptr(xi), flags, int(maxfun), ptr(params),
-                           ptr(out), N, int(n_gpus), err, len(err))
+    fn = L.gpd_fit_windows_c32 if c32 else L.gpd_fit_windows
+    rc = fn(N, nwindow, C, ptr(t), ptr(d), N, ptr(fc), fc.shape[0], N, ptr(fop), ptr(st),
+            float(omega), ptr(xi), flags, int(maxfun), ptr(params), ptr(out), N, int(n_gpus), err,
+            len(err))
     check(rc, err)
     params = params.reshape(nwin, C)
     return (params, out) if want_output else params
@@ -301,7 +316,9 @@ def demodulate_windows(timestamp, data, window, *, faintparam=None, onlyhigh=Fal
     per-sample Float32 parameter columns ABSA, ARGA, B, PHI (and X0, Y0 with fitoffsets),
     each (32, N) in idx() order, as the reference writes them (:209-224, :239-244)."""
     t = np.asarray(timestamp, dtype=np.float64)
-    data = np.asarray(data).astype(np.complex128, copy=False)
+    data = np.asarray(data)
+    if data.dtype != np.complex64:
+        data = data.astype(np.complex128, copy=False)
     if data.ndim != 2 or data.shape[1] != 40 or data.shape[0] != t.size:
         raise ValueError("data must be N×40 with one row per timestamp")
     N = t.size

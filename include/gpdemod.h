@@ -31,6 +31,11 @@ typedef struct {
     double re, im;
 } gpd_c64;
 
+/* Julia ComplexF32: interleaved (re, im), 8 bytes — the precision of the FITS VOLT column. */
+typedef struct {
+    float re, im;
+} gpd_c32;
+
 /* One fitted series = the reference's Modulation record (src/Modulation.jl:24-39:
  * ModulationWithOffsets{c,a,b,ϕ,ω} / ModulationNoOffsets{a,b,ϕ,ω}) plus the likelihood
  * (src/Modulation.jl:359,416) and bookkeeping.  64 bytes.  c == 0 without GPD_FIT_OFFSETS.
@@ -181,6 +186,44 @@ int gpd_process_volt(int64_t n_samples, const double *t, const float *volt, int6
                      const double *xinit, uint32_t flags, int32_t maxfun, int64_t window,
                      gpd_param *out_params, float *out_volt, int64_t ldov, int device,
                      char *errbuf, size_t errlen);
+
+/*
+ * Float32-storage variants (BASELINE config 5; the VOLT column is Float32 on disk,
+ * src/GPPupilDemodulation.jl:147): d and fc are ComplexF32 columns (ldd, ldfc in elements),
+ * widened to Float64 as they are loaded, so every χ² evaluation and the fit run in Float64 on
+ * exactly the values Float64.(data) would hold — results equal gpd_fit_batch / gpd_fit_windows
+ * on the widened arrays, with half the HBM traffic of the series pass.  Same arguments,
+ * flags, outputs (complex128 out_demod) and errors as the Float64 entry points.
+ * The reference's demodulateall(::Vector{T}, ::Matrix{Complex{T}}) is generic in T
+ * (src/Modulation.jl:344); with T = Float32 it would also compute in Float32 — this engine keeps
+ * Float64 arithmetic (the reference's own Float32 path cannot run: binit is Float64, :403).
+ */
+int gpd_fit_batch_c32(int64_t n_samples, int64_t n_pixels, const double *t, const gpd_c32 *d,
+                      int64_t ldd, const gpd_c32 *fc, int64_t n_fc, int64_t ldfc,
+                      const int32_t *fc_of_pixel, const int8_t *state, double omega,
+                      const double *xinit, uint32_t flags, int32_t maxfun, gpd_param *out_params,
+                      gpd_c64 *out_demod, int64_t ldo, int32_t n_gpus, char *errbuf, size_t errlen);
+
+int gpd_fit_batch_c32_dev(int64_t n_samples, int64_t n_pixels, const double *t, const gpd_c32 *d,
+                          int64_t ldd, const gpd_c32 *fc, int64_t n_fc, int64_t ldfc,
+                          const int32_t *fc_of_pixel, const int8_t *state, double omega,
+                          const double *xinit, uint32_t flags, int32_t maxfun,
+                          gpd_param *out_params, gpd_c64 *out_demod, int64_t ldo, int device,
+                          void *stream, char *errbuf, size_t errlen);
+
+int gpd_fit_windows_c32(int64_t n_samples, int64_t window, int64_t n_cols, const double *t,
+                        const gpd_c32 *d, int64_t ldd, const gpd_c32 *fc, int64_t n_fc,
+                        int64_t ldfc, const int32_t *fc_of_col, const int8_t *state, double omega,
+                        const double *xinit, uint32_t flags, int32_t maxfun,
+                        gpd_param *out_params, gpd_c64 *out_demod, int64_t ldo, int32_t n_gpus,
+                        char *errbuf, size_t errlen);
+
+int gpd_fit_windows_c32_dev(int64_t n_samples, int64_t window, int64_t n_cols, const double *t,
+                            const gpd_c32 *d, int64_t ldd, const gpd_c32 *fc, int64_t n_fc,
+                            int64_t ldfc, const int32_t *fc_of_col, const int8_t *state,
+                            double omega, const double *xinit, uint32_t flags, int32_t maxfun,
+                            gpd_param *out_params, gpd_c64 *out_demod, int64_t ldo, int device,
+                            void *stream, char *errbuf, size_t errlen);
 
 /*
  * buildstates (src/Faint.jl:21-73): two-timer faint state machine on the host.
