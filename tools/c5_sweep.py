@@ -1,0 +1,169 @@
+#!/usr/bin/env python3
+"""BASELINE config 5: faint-mode (src/Faint.jl) state-switched demodulation, Float32 vs Float64
+tolerance sweep.  Runs on one MI355X (gpurun); writes one JSON summary.
+
+Workload: N = 1e5 samples at 2 ms (relative timestamps, t0 = 0), seed 11;
+states NORMAL for the first and last 8 s, then 1 s HIGH per 11 s, LOW otherwise, TRANSIENT
+after each switch per preswitchdelay / postwitchdelay = 0.01 / 0.3 s (buildstates,
+src/Faint.jl:21-73); signal power HIGH : NORMAL : LOW = 1.1 : 0.1 : 0.01 on top of a
+constant detector noise.  P synthetic series (4 per FC column) with the §8d truth model.
+
+Precisions compared (the engine always computes in Float64; "fp32" is the data):
+  f64      ComplexF64 series / FC (gpd_fit_batch_dev)             — the reference outcome
+  c32      the same series rounded to ComplexF32 (the FITS VOLT precision) and kept in Float32 in
+           HBM (gpd_fit_batch_c32_dev)
+for both evaluators (harmonic = default, exact = reference arithmetic), plus f64 harmonic vs f64
+exact as the scale of evaluator-level differences.  For each pair: per-series deviation of b
+(relative), ϕ and arg a (absolute, radians, mod 2π), |a| (relative), and the fraction of series
+within each tolerance 1e-3 … 1e-8.  A fully Float32 arithmetic path is not built (DESIGN.md
+§12): the reference's own Float32 path cannot run (binit is Float64, src/Modulation.jl:403).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+TOLS = [1e-3, 1e-4, 1e-5, 1e-6, 1e-7, 1e-8]
+POWER = {3: 1.1, 2: 0.1, 1: 0.01, -1: 0.1, 0: 0.0}  # HIGH, NORMAL, LOW, TRANSIENT, OFF
+
+
+def c5_states(gpd, t):
+    """HIGH switches at 8 + 11k s, LOW switches at 9 + 11k s, NORMAL again for the last 8 s."""
+    import numpy as np
+
+    T = t[-1] - t[0]
+    highs = np.arange(8.0, T - 8.0, 11.0)
+    lows = highs + 1.0
+    fs = gpd.FaintStates.make(highs, lows, 1.0, 2.0)  # higher voltage = LOW timer (Faint.jl:12-19)
+    st = gpd.buildstates(fs, t, preswitchdelay=0.01, postwitchdelay=0.3)
+    st[t >= T - 8.0] = gpd.MetState.NORMAL
+    return st
+
+
+def deviations(x, r):
+    import numpy as np
+
+    def wrap(a):
+        return np.abs((a + np.pi) % (2 * np.pi) - np.pi)
+
+    return {"b": np.abs(x["b"] - r["b"]) / np.abs(r["b"]),
+            "phi": wrap(x["phi"] - r["phi"]),
+            "abs_a": np.abs(np.abs(x["a"]) - np.abs(r["a"])) / np.abs(r["a"]),
+            "arg_a": wrap(np.angle(x["a"]) - np.angle(r["a"]))}
+
+
+def summarise(x, r):
+    import numpy as np
+
+    dv = deviations(x, r)
+    out = {}
+    for k, v in dv.items():
+        v = v[np.isfinite(v)]
+        out[k] = {"max": float(v.max()), "median": float(np.median(v)),
+                  "within": {f"{t:g}": round(float((v <= t).mean()), 4) for t in TOLS}}
+    worst = np.max(np.stack([dv[k] for k in dv]), axis=0)
+    out["all_params"] = {"within": {f"{t:g}": round(float((worst <= t).mean()), 4) for t in TOLS},
+                         "max": float(np.nanmax(worst))}
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--series", type=int, default=4096)
+    ap.add_argument("--samples", type=int, default=100_000)
+    ap.add_argument("--seed", type=int, default=11)
+    ap.add_argument("--noise", type=float, default=0.02)
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "c5_sweep.json"))
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+
+    import gpdemod_loader
+
+    gpd = gpdemod_loader.load()
+    L = gpd.load()
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    sptr = ctypes.c_void_p(stream.cuda_stream)
+    P, N = args.series - args.series % 4, args.samples
+    G = P // 4
+    t = torch.empty(N, dtype=torch.float64, device=dev)
+    d = torch.empty((P, N, 2), dtype=torch.float64, device=dev)
+    fc = torch.empty((G, N, 2), dtype=torch.float64, device=dev)
+    fcop = torch.empty(P, dtype=torch.int32, device=dev)
+    truth = torch.empty((P, 64), dtype=torch.uint8, device=dev)
+    gpd._lib.check(L.gpd_synth_fill_dev(N, P, 0, args.seed, 0.0, 0.002, 0.0, 0, gpd.M_2PI,
+                                        t.data_ptr(), d.data_ptr(), N, fc.data_ptr(), N,
+                                        fcop.data_ptr(), truth.data_ptr(), 0, sptr))
+    th = t.cpu().numpy()
+    st = c5_states(gpd, th)
+    power = torch.tensor([POWER[int(s)] for s in st], dtype=torch.float64, device=dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(args.seed)
+    d.mul_(power[None, :, None])
+    d.add_(torch.randn(d.shape, generator=gen, dtype=torch.float64, device=dev),
+           alpha=args.noise / np.sqrt(2.0))
+    d32 = d.float()
+    fc32 = fc.float()
+    std = torch.from_numpy(st).to(dev)
+    counts = {name: int((st == code).sum()) for name, code in
+              (("HIGH", 3), ("NORMAL", 2), ("LOW", 1), ("TRANSIENT", -1))}
+
+    params = torch.empty((P, 64), dtype=torch.uint8, device=dev)
+    err = ctypes.create_string_buffer(512)
+    rec = gpd.PARAM_DTYPE
+
+    def run(c32, method):
+        flags = gpd.GPD_RECENTER | {"harmonic": gpd.GPD_METHOD_HARMONIC,
+                                    "exact": gpd.GPD_METHOD_EXACT}[method]
+        fn = L.gpd_fit_batch_c32_dev if c32 else L.gpd_fit_batch_dev
+        dd, ff = (d32, fc32) if c32 else (d, fc)
+        best = None
+        for _ in range(2):  # second call timed (workspace already sized)
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            gpd._lib.check(fn(N, P, t.data_ptr(), dd.data_ptr(), N, ff.data_ptr(), G, N,
+                              fcop.data_ptr(), std.data_ptr(), gpd.M_2PI, None, flags, 60,
+                              params.data_ptr(), None, N, 0, sptr, err, len(err)), err)
+            torch.cuda.synchronize(dev)
+            best = time.perf_counter() - t0
+        kern = {k: round(v, 3) for k, v in gpd.timings(0).items()}
+        par = params.cpu().numpy().reshape(-1).view(rec).copy()
+        return par, {"wall_ms": round(best * 1e3, 3), "kernels_ms": kern,
+                     "samples_per_s": P * N / best,
+                     "nan": int(np.count_nonzero(par["status"] & gpd.GPD_ST_NAN)),
+                     "fallback": int(np.count_nonzero(par["status"] & gpd.GPD_ST_FALLBACK))}
+
+    runs = {}
+    res = {}
+    for c32 in (False, True):
+        for method in ("harmonic", "exact"):
+            key = f"{'c32' if c32 else 'f64'}_{method}"
+            res[key], runs[key] = run(c32, method)
+    tr = truth.cpu().numpy().reshape(-1).view(rec)
+    out = {
+        "config": "C5", "series": P, "samples": N, "seed": args.seed, "dt": 0.002, "t0": 0.0,
+        "noise_sigma": args.noise, "power": {"HIGH": 1.1, "NORMAL": 0.1, "LOW": 0.01},
+        "state_counts": counts, "preswitchdelay": 0.01, "postwitchdelay": 0.3,
+        "runs": runs,
+        "c32_vs_f64": {m: summarise(res[f"c32_{m}"], res[f"f64_{m}"])
+                       for m in ("harmonic", "exact")},
+        "harmonic_vs_exact_f64": summarise(res["f64_harmonic"], res["f64_exact"]),
+        "f64_exact_vs_truth_median_abs_b": float(np.median(np.abs(res["f64_exact"]["b"] - tr["b"]))),
+        "tolerances": TOLS,
+    }
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    with open(args.out, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps({k: out[k] for k in ("c32_vs_f64", "harmonic_vs_exact_f64")}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
