@@ -43,7 +43,7 @@ EXPORTS = ("gpd_version", "gpd_strerror", "gpd_device_count", "gpd_fit_batch",
            "gpd_fit_batch_dev", "gpd_chi2_batch", "gpd_chi2_batch_dev", "gpd_buildstates",
            "gpd_synth_fill_dev", "gpd_last_timings", "gpd_fit_windows", "gpd_fit_windows_dev",
            "gpd_process_volt", "gpd_fit_batch_c32", "gpd_fit_batch_c32_dev", "gpd_fit_windows_c32",
-           "gpd_fit_windows_c32_dev")
+           "gpd_fit_windows_c32_dev", "gpd_buildstates_dev")
 
 
 class GpdError(RuntimeError):
@@ -99,6 +99,8 @@ def load():
                                    ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]
     L.gpd_buildstates.restype = ctypes.c_int
     L.gpd_buildstates.argtypes = [I64, V, I64, V, I64, V, D, D, V]
+    L.gpd_buildstates_dev.restype = ctypes.c_int
+    L.gpd_buildstates_dev.argtypes = [I64, V, I64, V, I64, V, I64, D, D, V, ctypes.c_int, V]
     L.gpd_synth_fill_dev.restype = ctypes.c_int
     L.gpd_synth_fill_dev.argtypes = [I64, I64, I64, ctypes.c_uint64, D, D, D, ctypes.c_int, D, V, V,
                                      I64, V, I64, V, V, ctypes.c_int, V]

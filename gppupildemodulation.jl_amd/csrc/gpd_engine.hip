@@ -19,6 +19,7 @@
 
 #include "../../include/gpdemod.h"
 #include "gpd_kernels.hpp"
+#include "gpd_states.hpp"
 
 using namespace gpd;
 
@@ -59,6 +60,9 @@ struct DevCtx {
     int ntimers = 0;
     bool have_timers = false;
     int n_cu = 0;  // compute units (wave-quantisation of the moment grid)
+    // gpd_buildstates_dev: pinned staging of the timer lists, reused once its copy has run
+    double *bs_pinned = nullptr;
+    hipEvent_t bs_done = nullptr;
 };
 
 std::mutex g_mu;
@@ -924,6 +928,57 @@ int gpd_synth_fill_dev(int64_t n_samples, int64_t n_pixels, int64_t pixel_offset
                                ldfc, (c64 *)d, ldd, fc_of_pixel);
     HIP_TRY(hipGetLastError());
     if (tmp) HIP_TRY(hipFreeAsync(tmp, s));
+    return GPD_OK;
+}
+
+int gpd_buildstates_dev(int64_t n, const double *t, int64_t n1, const double *timer1, int64_t n2,
+                        const double *timer2, int64_t lag, double preswitchdelay,
+                        double postwitchdelay, int8_t *states, int device, void *stream_) {
+    // src/Faint.jl:21-73 on device (gpd_states.hpp): t and states are device arrays, the timer
+    // lists (FITS header values, buildfaintparameters) host arrays, shifted here by lag·Δt.
+    char *errbuf = nullptr;
+    size_t errlen = 0;
+    if (n < 2 || n1 < 1 || n2 < 1 || n1 > BS_MAX_TIMER || n2 > BS_MAX_TIMER || !t || !timer1 ||
+        !timer2 || !states)
+        return GPD_E_ARG;
+    const int ndev = gpd_device_count();
+    if (ndev <= 0) return GPD_E_NODEV;
+    if (device < 0 || device >= ndev) return GPD_E_ARG;
+    HIP_TRY(hipSetDevice(device));
+    hipStream_t s = (hipStream_t)stream_;
+    const long long nt = n1 + n2, cap = nt + n + 1;
+    DevCtx *cx = ctx_for(device);
+    std::lock_guard<std::mutex> lk(cx->mu);
+    if (!cx->bs_pinned) {
+        HIP_TRY(hipHostMalloc((void **)&cx->bs_pinned, 2 * BS_MAX_TIMER * sizeof(double),
+                              hipHostMallocDefault));
+        HIP_TRY(hipEventCreateWithFlags(&cx->bs_done, hipEventDisableTiming));
+    } else {
+        HIP_TRY(hipEventSynchronize(cx->bs_done));  // the previous call's copy has consumed it
+    }
+    std::memcpy(cx->bs_pinned, timer1, n1 * sizeof(double));
+    std::memcpy(cx->bs_pinned + n1, timer2, n2 * sizeof(double));
+    const size_t o_lb = align_up(nt * sizeof(double)), o_ctl = o_lb + align_up(nt * sizeof(long long)),
+                 o_evk = o_ctl + align_up(sizeof(BsCtl)), o_evf = o_evk + align_up(cap * sizeof(long long)),
+                 o_evs = o_evf + align_up(cap * sizeof(long long)), total = o_evs + align_up(cap);
+    char *w = nullptr;
+    HIP_TRY(hipMallocAsync((void **)&w, total, s));
+    double *tim = (double *)w;
+    long long *lb = (long long *)(w + o_lb), *evk = (long long *)(w + o_evk),
+              *evf = (long long *)(w + o_evf);
+    BsCtl *ctl = (BsCtl *)(w + o_ctl);
+    int8_t *evs = (int8_t *)(w + o_evs);
+    HIP_TRY(hipMemcpyAsync(tim, cx->bs_pinned, nt * sizeof(double), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipEventRecord(cx->bs_done, s));
+    HIP_TRY(hipMemsetAsync(ctl, 0, sizeof(BsCtl), s));
+    const long long np = std::max<long long>(n - 1, nt);
+    k_bs_prep<<<(unsigned)((np + 255) / 256), 256, 0, s>>>(t, n, tim, n1, n2, lag, preswitchdelay,
+                                                         postwitchdelay, lb, ctl);
+    k_bs_events<<<1, 256, 0, s>>>(t, n, tim, n1, n2, lb, ctl, evk, evs, evf);
+    k_bs_fill<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(n, ctl, evk, evs, evf, states);
+    k_bs_serial<<<1, 64, 0, s>>>(t, n, tim, n1, n2, ctl, states);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipFreeAsync(w, s));
     return GPD_OK;
 }
 

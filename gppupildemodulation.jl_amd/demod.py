@@ -96,6 +96,28 @@ class FaintStates:  # src/Faint.jl:3-19
         return cls(t1, t2, voltage1, voltage2, MetState.HIGH, MetState.LOW)
 
 
+MJD_1970_1_1 = 40587.0  # src/GPPupilDemodulation.jl:15
+DAY_TO_SEC = 24 * 60 * 60  # :16
+
+
+def buildfaintparameters(hdr) -> FaintStates:
+    """FaintStates from the exposure header (src/GPPupilDemodulation.jl:64-81): timer_i =
+    TIMERi + MJD(1970-01-01)·86400 + RATEi·(0:REPEATi-1), ordered by VOLTAGEi.  `hdr` is any
+    mapping with the ESO keywords (e.g. a FITS header read elsewhere; FITS I/O is out of scope)."""
+    timers = []
+    for i in (1, 2):
+        start = hdr[f"ESO INS ANLO3 TIMER{i}"] + MJD_1970_1_1 * DAY_TO_SEC
+        rate = hdr[f"ESO INS ANLO3 RATE{i}"]
+        timers.append(start + rate * np.arange(int(hdr[f"ESO INS ANLO3 REPEAT{i}"])))
+    return FaintStates.make(timers[0], timers[1], hdr["ESO INS ANLO3 VOLTAGE1"],
+                            hdr["ESO INS ANLO3 VOLTAGE2"])
+
+
+def metrology_times(time_us, mjd_obs):
+    """Float64.(table["TIME"]) .* 1e-6 .+ DAY_TO_SEC * mjd (src/GPPupilDemodulation.jl:139)."""
+    return np.asarray(time_us).astype(np.float64) * 1e-6 + (DAY_TO_SEC * float(mjd_obs))
+
+
 def buildstates(faintstates: FaintStates, timestamp, lag: int = 0, preswitchdelay=0.0,
                 postwitchdelay=0.0) -> np.ndarray:
     """src/Faint.jl:21-73 → int8 MetState codes (host C++ in libgpdemod)."""

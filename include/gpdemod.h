@@ -235,6 +235,18 @@ int gpd_buildstates(int64_t n_samples, const double *t, int64_t n1, const double
                     double postwitchdelay, int8_t *states);
 
 /*
+ * buildstates on device (same semantics, src/Faint.jl:21-73): t [n_samples] and states
+ * [n_samples] are device arrays of device `device`, timer1 [n1] / timer2 [n2] host arrays of the
+ * unshifted switch times (buildfaintparameters, src/GPPupilDemodulation.jl:64-81), shifted on
+ * device by lag·(t[1] − t[0]) as src/Faint.jl:25-26.  Enqueued on `stream`; the timer lists may
+ * be released when the call returns.  n1, n2 ≤ 4096.  Non-decreasing timestamps: firing samples
+ * by binary search and a parallel fill; otherwise the reference loop on one lane.
+ */
+int gpd_buildstates_dev(int64_t n_samples, const double *t, int64_t n1, const double *timer1,
+                        int64_t n2, const double *timer2, int64_t lag, double preswitchdelay,
+                        double postwitchdelay, int8_t *states, int device, void *stream);
+
+/*
  * Synthetic GRAVITY-like metrology batch generated ON DEVICE (benchmarks):
  * d[k][i] = p_i(c_k + a_k exp(j b_k sin(ω t_i + ϕ_k))) + σ CN(0,1), FC column g = 1.3 exp(jΦ_g),
  * Φ a random walk (σ 1e-3 rad/step), 4 series per FC column, counter-based RNG keyed by

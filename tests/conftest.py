@@ -5,6 +5,10 @@ import sys
 import numpy as np
 import pytest
 
+# torch (used by the device-pointer tests) before libgpdemod: torch ships its own HIP runtime,
+# and loading it after the system one our library links makes torch see no device
+import torch  # noqa: F401
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
     if p not in sys.path:

@@ -82,3 +82,19 @@ def test_process_volt_argument_checks(gpd):
         gpd.process_volt(t, np.zeros((100, 79), np.float32))
     with pytest.raises(NotImplementedError):
         gpd.process_volt(t, np.zeros((100, 80), np.float32), offsets=True)
+
+
+def test_buildfaintparameters_from_header(gpd):
+    """src/GPPupilDemodulation.jl:64-81: timers from TIMERi/RATEi/REPEATi, ordered by voltage."""
+    hdr = {"MJD-OBS": 60000.5, "ESO INS ANLO3 RATE1": 11.0, "ESO INS ANLO3 RATE2": 11.0,
+           "ESO INS ANLO3 REPEAT1": 5, "ESO INS ANLO3 REPEAT2": 4,
+           "ESO INS ANLO3 TIMER1": 1.7e9, "ESO INS ANLO3 TIMER2": 1.7e9 + 1.0,
+           "ESO INS ANLO3 VOLTAGE1": 4.5, "ESO INS ANLO3 VOLTAGE2": 1.0}
+    fs = gpd.buildfaintparameters(hdr)
+    off = 40587.0 * 86400
+    # voltage1 > voltage2: timer1 is the LOW one, so the structure swaps them (src/Faint.jl:14-16)
+    np.testing.assert_array_equal(fs.timer1, 1.7e9 + 1.0 + off + 11.0 * np.arange(4))
+    np.testing.assert_array_equal(fs.timer2, 1.7e9 + off + 11.0 * np.arange(5))
+    assert (fs.voltage1, fs.voltage2) == (1.0, 4.5)
+    t = gpd.metrology_times(np.array([0, 2000, 4000], dtype=np.int64), 60000.5)
+    np.testing.assert_array_equal(t, np.array([0, 2000, 4000]) * 1e-6 + 86400 * 60000.5)

@@ -165,3 +165,85 @@ def test_golden_fixtures_reproduce(oracle):
             np.testing.assert_allclose(got[key], case["expect"][key], rtol=1e-12, atol=1e-14,
                                        err_msg=f"{case['spec']['name']}:{key}")
         np.testing.assert_array_equal(got["nfev"], case["expect"]["nfev"])
+
+
+def event_buildstates(t, t1, t2, pre, post):
+    """The firing-list formulation of gpd_states.hpp (k_bs_prep / k_bs_events / k_bs_fill) in
+    Python: checks the reduction itself against the line-by-line transcription on CPU."""
+    n, n1, n2 = t.size, len(t1), len(t2)
+    step = t[1] - t[0]
+    premax, postmax = math.ceil(pre / step), math.ceil(post / step)
+    tl = t[-1]
+    lb = np.searchsorted(t, np.concatenate([t1, t2]), side="left")
+    lbT = int(np.searchsorted(t, tl, side="left"))
+    last = np.concatenate([t1, t2]) == tl
+    c1 = c2 = 0
+    l1 = l2 = -1
+    cur = 2
+    ev = []
+    while True:
+        k1 = max(l1 + 1, lb[c1] if c1 < n1 else lbT)
+        k2 = max(l2 + 1, lb[n1 + c2] if c2 < n2 else lbT)
+        k1, k2 = (k1 if k1 < n else n), (k2 if k2 < n else n)
+        k = min(k1, k2)
+        if k >= n:
+            break
+        fg = 0
+        if k1 == k:
+            cur, fg = 3, premax
+            if c1 >= n1 - 1:
+                c1 = n1
+                if c2 >= n2 or last[n1 + c2]:
+                    cur = 2
+            else:
+                c1 += 1
+            l1 = k
+        if k2 == k:
+            cur, fg = 1, postmax
+            if c2 >= n2 - 1:
+                c2 = n2
+                if c1 >= n1 or last[c1]:
+                    cur = 2
+            else:
+                c2 += 1
+            l2 = k
+        ev.append((k, cur, fg))
+    out = np.full(n, 2, dtype=np.int8)
+    ks = np.array([e[0] for e in ev], dtype=np.int64)
+    for k in range(n):
+        j = np.searchsorted(ks, k, side="right") - 1
+        if j >= 0:
+            ek, es, ef = ev[j]
+            out[k] = -1 if k - ek < ef else es
+    return out
+
+
+def random_timer_case(rng):
+    """Edge cases of src/Faint.jl:21-73: entries closer than Δt (the one-pop-per-sample lag),
+    before t[0], after and exactly at t[N-1], repeated final timestamps, single entries."""
+    n = int(rng.integers(2, 400))
+    t = 10.0 + np.arange(n) * 0.002
+    if rng.random() < 0.3:
+        t[-int(rng.integers(1, 4)):] = t[-1] if n > 4 else t[-1]
+        t = np.maximum.accumulate(t)
+    span = t[-1] - t[0]
+
+    def timer():
+        m = int(rng.integers(1, 8))
+        x = t[0] + rng.uniform(-0.1, 1.1, m) * span
+        if rng.random() < 0.3:
+            x = np.concatenate([x, x[:1] + rng.uniform(0, 0.003, 2)])  # within one interval
+        if rng.random() < 0.2:
+            x[rng.integers(0, x.size)] = t[-1]
+        return np.sort(x)
+
+    pre, post = (0.0, 0.0) if rng.random() < 0.3 else (rng.uniform(0, 0.05), rng.uniform(0, 0.2))
+    return t, timer(), timer(), pre, post
+
+
+def test_event_formulation_equals_reference_loop():
+    rng = np.random.default_rng(5)
+    for _ in range(400):
+        t, t1, t2, pre, post = random_timer_case(rng)
+        np.testing.assert_array_equal(event_buildstates(t, t1, t2, pre, post),
+                                      py_buildstates(t, t1, t2, pre, post))
