@@ -448,3 +448,69 @@ def process_volt(timestamp, volt, *, offsets=None, window=None, faintparam=None,
         params = params.reshape(-1, 32)
         return out, params, window_tables(params, N, nwindow, fitoffsets=fitoffsets)
     return out, params, None
+
+
+def _diode_order():
+    """(side, telescope, diode) in the order of Iterators.product((D1,D2,D3,D4), 1:4, (FT,SC))
+    (src/GPPupilDemodulation.jl:171,212): diode fastest, then telescope, then side."""
+    return [(side, tel, diode) for side in (Side.FT, Side.SC) for tel in range(1, 5)
+            for diode in (Diode.D1, Diode.D2, Diode.D3, Diode.D4)]
+
+
+def processmetrology(table, header, *, window=None, faintparam=None, keepraw=False,
+                     onlyhigh=False, offsets=None, method="auto", device=0):
+    """processmetrology (src/GPPupilDemodulation.jl:128-255) on the GPU, minus FITS I/O.
+
+    table: mapping of the METROLOGY columns with at least "TIME" (µs, N) and "VOLT" (N×80
+    Float32 rows); header: mapping of its header (the "MJD-OBS" key gives mjd, :139).  faintparam:
+    FaintStates (e.g. buildfaintparameters(primary header)).  offsets: (40,) complex centres, or
+    False → fitoffsets (a circle fit, offsets=True, is not restated).
+    Returns (table, header) as new dicts: VOLT replaced by the Float32 demodulated rows (80 per
+    row, or 144 with keepraw: raw rows then the 32 demodulated columns), in window mode the
+    per-sample Float32 columns ABSA, ARGA, B, PHI (+ X0, Y0) as (N, 32) rows and STATE (Int8) with
+    faint states; otherwise the header gains the per-diode DEMODULATION keywords (:172-189);
+    PROCSOFT = "GPPupilDemodulation.jl" in both modes (:253)."""
+    mjd = float(header["MJD-OBS"])
+    times = metrology_times(table["TIME"], mjd)
+    state = None
+    if faintparam is not None:
+        state = buildstates(faintparam, times)  # default delays of buildstates (:144)
+    volt = np.ascontiguousarray(table["VOLT"], dtype=np.float32)
+    if offsets is True:
+        raise NotImplementedError("compute_offsets (circle fit) is outside the hot path")
+    fitoffsets = offsets is False
+    vout, params, tabs = process_volt(times, volt, offsets=None if fitoffsets else offsets,
+                                      window=window, faintparam=state, onlyhigh=onlyhigh,
+                                      method=method, device=device)
+    tab = dict(table)
+    hdr = dict(header)
+    N = times.size
+    if keepraw:  # s[1:80,:] = volt; s[81:2:end,:] = real(output[:,1:32])' … (:162-167, :228-233)
+        s = np.empty((N, 144), dtype=np.float32)
+        s[:, :80] = volt
+        s[:, 80:] = vout[:, :64]
+        vout = s
+    if window is None:
+        for side, tel, diode in _diode_order():
+            p = params[idx(side, tel, diode) - 1]
+            b, phi = float(p["b"]), float(p["phi"])
+            if b < 0:  # rem2pi(ϕ+π, RoundNearest) (:175-178; b ≥ 0 already, :427-430)
+                b = -b
+                phi = float(np.remainder(phi + np.pi + np.pi, 2 * np.pi) - np.pi)
+            name = f"{side.name} T{tel} {diode.name}"
+            if fitoffsets:
+                hdr[f"DEMODULATION CENTER X0 {name}"] = float(p["c"].real)
+                hdr[f"DEMODULATION CENTER Y0 {name}"] = float(p["c"].imag)
+            hdr[f"DEMODULATION AMPLITUDE ABS {name}"] = float(abs(p["a"]))
+            hdr[f"DEMODULATION AMPLITUDE ARG {name}"] = float(np.angle(p["a"]))
+            hdr[f"DEMODULATION SIN AMPLITUDE {name}"] = b
+            hdr[f"DEMODULATION SIN PHASE {name}"] = phi
+    else:
+        order = ["X0", "Y0"] if fitoffsets else []
+        for key in order + ["ABSA", "ARGA", "B", "PHI"]:
+            tab[key] = np.ascontiguousarray(tabs[key].T)  # (N, 32): Julia's 32×N column per row
+        if state is not None:
+            tab["STATE"] = state.astype(np.int8)
+    hdr["PROCSOFT"] = "GPPupilDemodulation.jl"
+    tab["VOLT"] = vout
+    return tab, hdr

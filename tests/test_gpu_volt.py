@@ -65,3 +65,39 @@ def test_process_volt_fitoffsets_without_centring(gpu, oracle):
     print(assert_fit_parity(params, ref, perturbed_runs(oracle, B, ulps=4.0, fitoffsets=True),
                             label="volt offsets", min_match=0.5))
     assert np.max(np.abs(params["c"] - ref["c"])[np.abs(params["b"] - ref["b"]) <= 1e-10]) <= 1e-9
+
+
+def test_processmetrology_table_and_header(gpu):
+    """processmetrology (src/GPPupilDemodulation.jl:128-255) outputs: header keywords in the
+    reference's order and names, VOLT rows (80, or 144 with keepraw), window-mode columns."""
+    t, volt, centres, cplx, fop = volt_exposure(gpu, 6000, seed=37)
+    table = {"TIME": np.round((t - t[0]) * 1e6).astype(np.int64), "VOLT": volt,
+             "OTHER": np.arange(t.size)}
+    header = {"MJD-OBS": 60123.25, "EXTNAME": "METROLOGY"}
+    tab, hdr = gpu.processmetrology(table, header, offsets=centres)
+    times = gpu.metrology_times(table["TIME"], 60123.25)
+    out, params, _ = gpu.process_volt(times, volt, offsets=centres)
+    np.testing.assert_array_equal(tab["VOLT"], out)
+    assert tab["OTHER"] is table["OTHER"] and hdr["PROCSOFT"] == "GPPupilDemodulation.jl"
+    keys = [k for k in hdr if k.startswith("DEMODULATION")]
+    assert len(keys) == 4 * 32 and keys[:5] == [
+        "DEMODULATION AMPLITUDE ABS FT T1 D1", "DEMODULATION AMPLITUDE ARG FT T1 D1",
+        "DEMODULATION SIN AMPLITUDE FT T1 D1", "DEMODULATION SIN PHASE FT T1 D1",
+        "DEMODULATION AMPLITUDE ABS FT T1 D2"]
+    k = gpu.idx(gpu.Side.SC, 3, gpu.Diode.D2) - 1
+    assert hdr["DEMODULATION SIN AMPLITUDE SC T3 D2"] == params["b"][k]
+    assert hdr["DEMODULATION AMPLITUDE ARG SC T3 D2"] == np.angle(params["a"][k])
+    # keepraw: raw rows first, then the 32 demodulated columns
+    tab2, _ = gpu.processmetrology(table, header, offsets=centres, keepraw=True)
+    assert tab2["VOLT"].shape == (t.size, 144)
+    np.testing.assert_array_equal(tab2["VOLT"][:, :80], volt)
+    np.testing.assert_array_equal(tab2["VOLT"][:, 80:], out[:, :64])
+    # fitoffsets keywords, window columns + STATE
+    _, hdr3 = gpu.processmetrology(table, header, offsets=False)
+    assert "DEMODULATION CENTER X0 FT T1 D1" in hdr3
+    highs = times[0] + np.array([2.0, 7.0])
+    fs = gpu.FaintStates.make(highs, highs + 1.0, 1.0, 2.0)
+    tab4, hdr4 = gpu.processmetrology(table, header, offsets=centres, window=4.0, faintparam=fs)
+    assert not any(k.startswith("DEMODULATION") for k in hdr4)
+    assert tab4["B"].shape == (t.size, 32) and tab4["B"].dtype == np.float32
+    assert tab4["STATE"].dtype == np.int8 and set(np.unique(tab4["STATE"])) <= {-1, 1, 2, 3}
