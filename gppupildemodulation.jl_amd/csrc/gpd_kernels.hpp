@@ -481,12 +481,13 @@ __device__ __forceinline__ int mm_phys(int p, int s) { return s * MM_ROW + (p ^ 
 
 // One complex element of storage type TS (c64: 16 B, c32: 8 B) through a buffer descriptor;
 // kept in its storage type until staged (widening at the load would wait on it there).
-template <class TS>
+// POL: cache policy bits of the load (0 default, 2 = nt: streamed once, no MALL allocation).
+template <class TS, int POL = 0>
 __device__ __forceinline__ TS buf_ld(__amdgpu_buffer_rsrc_t rs, int voff) {
     if constexpr (sizeof(TS) == 16)
-        return __builtin_bit_cast(TS, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0));
+        return __builtin_bit_cast(TS, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, POL));
     else
-        return __builtin_bit_cast(TS, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, 0, 0));
+        return __builtin_bit_cast(TS, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, 0, POL));
 }
 
 template <bool FAINT, class TS = c64>
@@ -697,7 +698,7 @@ struct WsRegs {
 // 2 = producers skip the global loads, 5 = producers only keep the barrier cadence.
 // UNIT: the series are FC columns and d ≡ 1, i.e. the moments G_n = Σ p̄ e^{-jnx} of the
 // unit phasors (harmonic fitoffsets: Σ w m = conj(Σ_n J_n(b) e^{-jnϕ} G_n)).
-template <int DBG = 0, bool UNIT = false, class TS = c64>
+template <int DBG = 0, bool UNIT = false, class TS = c64, int POL = 0>
 __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double *__restrict__ tab,
                                                        long long chunk_len,
                                                        double *__restrict__ part) {
@@ -767,7 +768,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
                     if constexpr (UNIT) continue;
                     // all offset parts in voffset (the range check ignores soffset): rows
                     // beyond P and samples beyond the last row read as 0
-                    R.d[r][j] = buf_ld<TS>(drs, dvoff + (32 * r + j) * ldd16 + s016);
+                    R.d[r][j] = buf_ld<TS, POL>(drs, dvoff + (32 * r + j) * ldd16 + s016);
                 }
             }
         };
