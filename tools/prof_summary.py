@@ -47,9 +47,11 @@ def main(tag, src=None):
         "bench": bench,
     }
     json.dump(summary, open(os.path.join(dst, "summary.json"), "w"), indent=1)
+    storage = cfg.get("storage", "c64")
+    name = "pmc_moments.json" if storage == "c64" else f"pmc_moments_{storage}.json"
     json.dump({k: summary[k] for k in ("tag", "pixels", "samples", "hbm_bytes_per_launch",
                                        "FETCH_SIZE_kB", "WRITE_SIZE_kB")},
-              open(os.path.join(ROOT, "profiles", "pmc_moments.json"), "w"), indent=1)
+              open(os.path.join(ROOT, "profiles", name), "w"), indent=1)
     print(json.dumps({k: v for k, v in summary.items() if k != "bench"}, indent=1))
 
 
