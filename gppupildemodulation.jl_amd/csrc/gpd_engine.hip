@@ -351,7 +351,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                 k_moments_ws<0, false, c32, 2><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
             else if (is_c32)
                 k_moments_ws<0, false, c32><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
-            else if (nt_loads)
+            else if (!(mk && *mk) && nt_loads)  // the production kernel
                 k_moments_ws<0, false, c64, 2><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
             else if (mk && std::string(mk) == "mfma1")  // single-role kernel (A/B runs)
                 k_moments_mfma<false><<<g, 256, 0, stream>>>(pb, tab, fstat, L.chunk, part);
@@ -359,6 +359,10 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                 k_moments_ws<1><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
             else if (mk && std::string(mk) == "ws_noload")
                 k_moments_ws<2><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
+            else if (mk && std::string(mk) == "ws_nof0")
+                k_moments_ws<7><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
+            else if (mk && std::string(mk) == "ws_noq")
+                k_moments_ws<8><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
             else if (mk && std::string(mk) == "ws_mfmaonly")
                 k_moments_ws<5><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
             else if (mk && std::string(mk) == "ws_prof") {  // cycle split per role (stderr)
@@ -375,6 +379,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                         "consumer mfma %.3g barrier %.3g\n",
                         z[0] / pw, z[1] / pw, z[2] / pw, z[3] / cw, z[4] / cw);
             }
+            else if (nt_loads)
+                k_moments_ws<0, false, c64, 2><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
             else
                 k_moments_ws<0><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
         } else {

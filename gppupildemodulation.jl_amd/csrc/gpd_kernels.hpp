@@ -695,6 +695,7 @@ struct WsRegs {
 };
 
 // DBG (timing experiments only, results invalid): 1 = consumers skip the MFMA phase,
+// 7 = consumers skip the F0/Σ|q|² VALU, 8 = producers stage d without forming q = p̄ d,
 // 2 = producers skip the global loads, 5 = producers only keep the barrier cadence.
 // UNIT: the series are FC columns and d ≡ 1, i.e. the moments G_n = Σ p̄ e^{-jnx} of the
 // unit phasors (harmonic fitoffsets: Σ w m = conj(Σ_n J_n(b) e^{-jnϕ} G_n)).
@@ -803,8 +804,12 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
                         pj = unit_phasor(fc_at(pb, (long long)fcl[pl] * ldfc + sl));
                     const c64 dv = UNIT ? c64{1.0, 0.0} : widen(R.d[r][j]);
                     c64 q;
-                    q.re = fma(pj.re, dv.re, pj.im * dv.im);
-                    q.im = fma(pj.re, dv.im, -(pj.im * dv.re));
+                    if constexpr (DBG == 8) {
+                        q = dv;
+                    } else {
+                        q.re = fma(pj.re, dv.re, pj.im * dv.im);
+                        q.im = fma(pj.re, dv.im, -(pj.im * dv.re));
+                    }
                     if (decltype(partial)::value) {  // rows beyond P read as 0 already
                         q.re = sok ? q.re : 0.0;
                         q.im = sok ? q.im : 0.0;
@@ -915,10 +920,12 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
 #pragma unroll
                 for (int n = 0; n < 3; ++n)
                     acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b[n], acc[m][n], 0, 0, 0);
+            if constexpr (DBG != 7) {
 #pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                f0[m] += a[m];
-                q2[m] = fma(a[m], a[m], q2[m]);
+                for (int m = 0; m < 4; ++m) {
+                    f0[m] += a[m];
+                    q2[m] = fma(a[m], a[m], q2[m]);
+                }
             }
         };
         unsigned long long c0 = 0;
