@@ -169,9 +169,11 @@ def main():
     if mom:
         avg_ms = float(np.mean(mom))
         achieved = algo_bytes / (avg_ms * 1e-3) / 1e9
-        # the same kernel against the dense fp64 MFMA peak: 4 real MACs per harmonic
-        # (K = 24) per complex sample — the pipe it actually saturates
-        mfma_flops = 2.0 * 4 * 24 * P * N
+        # the same kernel against the dense fp64 MFMA peak: 4 real MACs per harmonic per
+        # complex sample for the harmonics 1..16 on the f64 MFMAs (17..24 run on split-bf16
+        # MFMAs; GPD_MIX=0: all 24 on f64)
+        n_f64 = 24 if os.environ.get("GPD_MIX") == "0" else 16
+        mfma_flops = 2.0 * 4 * n_f64 * P * N
         tflops = mfma_flops / (avg_ms * 1e-3) / 1e12
         roofline = {"bound": "hbm", "kernel": "k_moments", "achieved": round(achieved, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -180,7 +182,8 @@ def main():
                     "avg_ms": round(avg_ms, 3),
                     "mfma": {"achieved": round(tflops, 2), "peak": MFMA_F64_PEAK_TFLOPS,
                              "unit": "TFLOP/s", "frac": round(tflops / MFMA_F64_PEAK_TFLOPS, 4),
-                             "algorithmic_flops": mfma_flops}}
+                             "algorithmic_flops": mfma_flops,
+                             "harmonics_f64": n_f64, "harmonics_bf16x3": 24 - n_f64}}
     kernels = {k: round(float(np.mean(v)), 3) for k, v in kern.items()}
     status = par["status"]
     fits = {"fallback_exact": int(np.count_nonzero(status & gpd.GPD_ST_FALLBACK)),

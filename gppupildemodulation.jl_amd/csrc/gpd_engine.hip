@@ -126,7 +126,8 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     L.nch = (int)nch;
     L.chunk = chunk;
     L.info = take(sizeof(Info));
-    L.tab = take(harmonic ? (size_t)N * 2 * KH * sizeof(double) : 0);
+    // cos/sin table, padded to whole MM_TS-sample tiles (k_table_mix fills the padding)
+    L.tab = take(harmonic ? (size_t)((N + MM_TS - 1) / MM_TS * MM_TS) * 2 * KH * sizeof(double) : 0);
     // windowed series: k_moments_win writes mom directly (no partial moments)
     L.part = take(harmonic && !windowed ? (size_t)nch * NMOM * P * sizeof(double) : 0);
     L.mom = take(harmonic ? (size_t)NMOM * P * sizeof(double) : 0);
@@ -220,7 +221,11 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     const double esz = is_c32 ? 8.0 : 16.0;  // bytes per stored complex element
     const bool use_mfma = !(mk && std::string(mk) == "valu") &&
                           (double)MM_PIX * (double)ldd * esz < 2147483648.0 &&
-                          (double)n_samples * KH * 16.0 < 2147483648.0;
+                          (double)(n_samples + MM_TS) * KH * 16.0 < 2147483648.0;
+    // mixed-precision moment kernel (harmonics 17..24 on split-bf16 MFMAs);
+    // GPD_MIX=0 keeps all harmonics on the f64 MFMAs (A/B runs and precision checks; read per
+    // call so a test can switch it)
+    const bool mix = !(getenv("GPD_MIX") && std::string(getenv("GPD_MIX")) == "0");
     // Harmonic fitoffsets (non-faint, on request): the χ² of the 2×2 system needs the moments
     // G_n of the FC phasors (producer/consumer kernel in UNIT mode over the FC columns) and Σ d
     // per series.  METHOD_EXACT uses the exact evaluator; so do windows with fitoffsets.
@@ -332,8 +337,18 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         mark("faint_stats");
     }
     const unsigned exact_grid = (unsigned)std::min<long long>(P, 1024);
+    bool tmix = false;  // the table holds the k_table_mix layout
     if (harmonic) {
-        k_table<<<(unsigned)((N + 255) / 256), 256, 0, stream>>>(t, N, omega, tab);
+        // the producer/consumer kernel (non-faint whole-exposure series, also the UNIT pass
+        // of harmonic fitoffsets) reads the k_table_mix layout when mixing; every other
+        // moment kernel the plain rows
+        const bool ws_kernel = use_mfma && window == 0 && !faint && !(mk && std::string(mk) == "mfma1");
+        tmix = mix && ws_kernel;
+        if (tmix)
+            k_table_mix<<<(unsigned)((N + MM_TS - 1) / MM_TS * MM_TS / 256 + 1), 256, 0, stream>>>(
+                t, N, omega, tab);
+        else
+            k_table<<<(unsigned)((N + 255) / 256), 256, 0, stream>>>(t, N, omega, tab);
         mark("table");
         if (window > 0) {
             if (faint)
@@ -347,14 +362,18 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                 k_moments_mfma<true, c32><<<g, 256, 0, stream>>>(pb, tab, fstat, L.chunk, part);
             else if (faint)
                 k_moments_mfma<true><<<g, 256, 0, stream>>>(pb, tab, fstat, L.chunk, part);
+            else if (mk && std::string(mk) == "mfma1")  // single-role kernel (A/B runs)
+                k_moments_mfma<false><<<g, 256, 0, stream>>>(pb, tab, fstat, L.chunk, part);
+            else if (!tmix && is_c32)  // all-f64 MFMA variants (GPD_MIX=0)
+                k_moments_ws<0, false, c32, 2, false><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
+            else if (!tmix)
+                k_moments_ws<0, false, c64, 2, false><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
             else if (is_c32 && nt_loads)  // Float32 storage: the producer/consumer kernel on 8-B elements
                 k_moments_ws<0, false, c32, 2><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
             else if (is_c32)
                 k_moments_ws<0, false, c32><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
             else if (!(mk && *mk) && nt_loads)  // the production kernel
                 k_moments_ws<0, false, c64, 2><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
-            else if (mk && std::string(mk) == "mfma1")  // single-role kernel (A/B runs)
-                k_moments_mfma<false><<<g, 256, 0, stream>>>(pb, tab, fstat, L.chunk, part);
             else if (mk && std::string(mk) == "ws_nomfma")  // timing experiments only
                 k_moments_ws<1><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
             else if (mk && std::string(mk) == "ws_noload")
@@ -413,10 +432,14 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             pg.ncol = n_fc;
             double *partG = (double *)(ws + L.partG), *auxG = (double *)(ws + L.auxG);
             dim3 gG((unsigned)((n_fc + MM_PIX - 1) / MM_PIX), (unsigned)L.nch);
-            if (is_c32)
+            if (is_c32 && tmix)
                 k_moments_ws<0, true, c32><<<gG, 512, 0, stream>>>(pg, tab, L.chunk, partG);
-            else
+            else if (tmix)
                 k_moments_ws<0, true><<<gG, 512, 0, stream>>>(pg, tab, L.chunk, partG);
+            else if (is_c32)
+                k_moments_ws<0, true, c32, 0, false><<<gG, 512, 0, stream>>>(pg, tab, L.chunk, partG);
+            else
+                k_moments_ws<0, true, c64, 0, false><<<gG, 512, 0, stream>>>(pg, tab, L.chunk, partG);
             dim3 grG((unsigned)((n_fc + 255) / 256), (unsigned)NMOM);
             k_reduce_moments<<<grG, 256, 0, stream>>>(partG, L.nch, n_fc, info, nullptr, 0, momG, auxG);
             k_series_sum<<<(unsigned)P, 256, 0, stream>>>(pb, d0);

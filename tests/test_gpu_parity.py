@@ -276,3 +276,34 @@ def test_demodulateall_one_exposure_full_size(gpu, oracle):
     np.testing.assert_array_equal(output[:, 32:], data[:, 32:])  # FC columns pass through
     same = np.abs(got["b"] - ref["b"]) <= TOL * ref["b"]
     assert np.max(np.abs(output[:, :32][:, same] - refout[same].T)) <= 1e-9 * np.abs(data).max()
+
+
+@pytest.mark.parametrize("n_samples", [6000, 100000])
+def test_mixed_precision_moments(gpu, monkeypatch, n_samples):
+    """Harmonics 17..24 of the production moment kernel run on split-bf16 MFMAs.
+    Worst case for them: series whose true b is large (2.8..3.8, past the synthetic 0.3..2.5, near
+    up to NEWUOA's largest probes), evaluated near their optimum, where |S| is large and χ² is
+    small, so an error in S shows in χ² undamped.  There the all-f64 expansion itself is ~2e-13
+    from the exact χ² (cancellation in W2 − |S|²/DEN); the split-bf16 harmonics must add no more
+    than a fraction of that (measured: 3e-14 at N = 6000, 6e-14 at N = 1e5, against 1.8e-13 and
+    4.1e-13 for the all-f64 expansion) and stay as close to the exact evaluator as it."""
+    B = synth.make_batch(n_samples, 64, seed=5, b_range=(2.8, 3.8))
+    rng = np.random.default_rng(11)
+    tr = B["truth"]
+    bphi = np.stack([tr["b"] + rng.normal(0, 1e-3, 64), tr["phi"] + rng.normal(0, 1e-3, 64)], 1)
+    args = (B["t"], B["d"], B["fc"], B["fc_of_pixel"], bphi)
+    mixed = gpu.chi2_batch(*args, method="harmonic")
+    monkeypatch.setenv("GPD_MIX", "0")
+    f64 = gpu.chi2_batch(*args, method="harmonic")
+    monkeypatch.delenv("GPD_MIX")
+    ex = gpu.chi2_batch(*args, method="exact")
+    assert not ((mixed["status"] | f64["status"]) & 0x18).any()  # no exact fallback: harmonic
+    d_mix = np.abs(mixed["chi2"] - f64["chi2"]) / f64["chi2"]
+    e_mix = np.abs(mixed["chi2"] - ex["chi2"]) / ex["chi2"]
+    e_f64 = np.abs(f64["chi2"] - ex["chi2"]) / ex["chi2"]
+    d_a = np.abs(mixed["a"] - f64["a"]) / np.abs(f64["a"])
+    print(f"N={n_samples}: chi2 mixed vs f64 max {d_mix.max():.2e} (median {np.median(d_mix):.2e});"
+          f" vs exact: mixed {e_mix.max():.2e}, f64 {e_f64.max():.2e}; a {d_a.max():.2e}")
+    assert d_mix.max() <= max(0.25 * e_f64.max(), 2e-14)
+    assert e_mix.max() <= max(1.25 * e_f64.max(), 1e-13)
+    assert d_a.max() <= 1e-13
