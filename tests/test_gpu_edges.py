@@ -60,11 +60,12 @@ def test_two_samples(gpu, oracle):
     np.testing.assert_allclose(got["chi2"], ref["chi2"], rtol=1e-10, atol=1e-300)
 
 
-@pytest.mark.parametrize("kernel", ["valu", "mfma1"])
+@pytest.mark.parametrize("kernel", ["valu", "mfma1", "ws_f64"])
 @pytest.mark.parametrize("faint", [False, True])
 def test_alternative_moment_kernels(gpu, oracle, monkeypatch, kernel, faint):
     """The single-role MFMA kernel and the VALU kernel (used when a series row or the cos/sin
-    table exceeds the producer/consumer kernel's 32-bit buffer offsets) give the same fits."""
+    table exceeds the producer/consumer kernel's 32-bit buffer offsets) give the same fits, and so
+    does the producer/consumer kernel with every harmonic on the f64 MFMAs (GPD_MIX=0)."""
     from test_gpu_parity import faint_states
     N, P = 3000, 40
     B = synth.make_batch(N, P, seed=77)
@@ -73,7 +74,10 @@ def test_alternative_moment_kernels(gpu, oracle, monkeypatch, kernel, faint):
     if faint:
         st = faint_states(N, seed=5)
         B["d"] = B["d"] * np.where(st == 3, 1.1, np.where(st == 1, 0.3, 0.6))[None, :]
-    monkeypatch.setenv("GPD_MOMENTS", kernel)
+    if kernel == "ws_f64":
+        monkeypatch.setenv("GPD_MIX", "0")
+    else:
+        monkeypatch.setenv("GPD_MOMENTS", kernel)
     got = gpu.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], state=st, method="harmonic")
     ref = oracle.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], state=st, flags=flags)
     pert = [oracle.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], state=st, flags=flags,
