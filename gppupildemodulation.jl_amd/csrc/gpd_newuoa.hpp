@@ -66,6 +66,40 @@ GPD_HD void wrc(double (&a)[R][C], int r, int c, double v) {
 }
 
 constexpr double kTwoPi = 6.283185307179586476925286766559;  // 8·atan(1)
+// cos/sin of the fixed trial angles i·dang, dang = kTwoPi/50, of the three angle searches
+// (TRSAPP, BIGLAG, BIGDEN: 49 angles each), exactly as the oracle's libm computes them
+// (oracle/tools/angle_table.py).  Read by uniform index (scalar loads) instead of 98 fp64
+// sin/cos evaluations per search — the bulk of the device NEWUOA's vector instructions.
+constexpr double kAngCos[50] = {
+    0x1.0000000000000p+0, 0x1.fbf675480d903p-1, 0x1.efea21d101ee0p-1, 0x1.dc0ba9def5ae4p-1,
+    0x1.c0ab44e81c059p-1, 0x1.9e3779b97f4a8p-1, 0x1.753b603d2b816p-1, 0x1.465c6feb501bbp-1,
+    0x1.1257e3c182b50p-1, 0x1.b3ff7c925819cp-2, 0x1.3c6ef372fe950p-2, 0x1.7fc1c65037a75p-3,
+    0x1.0130a1be09374p-4, -0x1.0130a1be0937bp-4, -0x1.7fc1c65037a80p-3, -0x1.3c6ef372fe952p-2,
+    -0x1.b3ff7c925819dp-2, -0x1.1257e3c182b53p-1, -0x1.465c6feb501bcp-1, -0x1.753b603d2b817p-1,
+    -0x1.9e3779b97f4a7p-1, -0x1.c0ab44e81c059p-1, -0x1.dc0ba9def5ae5p-1, -0x1.efea21d101ee0p-1,
+    -0x1.fbf675480d903p-1, -0x1.0000000000000p+0, -0x1.fbf675480d903p-1, -0x1.efea21d101ee0p-1,
+    -0x1.dc0ba9def5ae3p-1, -0x1.c0ab44e81c058p-1, -0x1.9e3779b97f4a6p-1, -0x1.753b603d2b816p-1,
+    -0x1.465c6feb501bap-1, -0x1.1257e3c182b4ep-1, -0x1.b3ff7c9258193p-2, -0x1.3c6ef372fe952p-2,
+    -0x1.7fc1c65037a79p-3, -0x1.0130a1be0936dp-4, 0x1.0130a1be09392p-4, 0x1.7fc1c65037a8bp-3,
+    0x1.3c6ef372fe94cp-2, 0x1.b3ff7c925819bp-2, 0x1.1257e3c182b52p-1, 0x1.465c6feb501bep-1,
+    0x1.753b603d2b819p-1, 0x1.9e3779b97f4abp-1, 0x1.c0ab44e81c059p-1, 0x1.dc0ba9def5ae5p-1,
+    0x1.efea21d101ee1p-1, 0x1.fbf675480d903p-1,
+};
+constexpr double kAngSin[50] = {
+    0x0.0p+0, 0x1.00aeb5da15be0p-3, 0x1.fd511fa1c0796p-3, 0x1.78f5a48a8a919p-2,
+    0x1.ed50d5cbfa952p-2, 0x1.2cf2304755a5ep-1, 0x1.5e7cf55112014p-1, 0x1.8a80b635b6beap-1,
+    0x1.b04bbff642e86p-1, 0x1.cf457dcdc158cp-1, 0x1.e6f0e134454ffp-1, 0x1.f6ee5ac2509ffp-1,
+    0x1.fefd5bfe443fep-1, 0x1.fefd5bfe443fep-1, 0x1.f6ee5ac2509fep-1, 0x1.e6f0e134454ffp-1,
+    0x1.cf457dcdc158bp-1, 0x1.b04bbff642e85p-1, 0x1.8a80b635b6beap-1, 0x1.5e7cf55112012p-1,
+    0x1.2cf2304755a5fp-1, 0x1.ed50d5cbfa950p-2, 0x1.78f5a48a8a915p-2, 0x1.fd511fa1c0797p-3,
+    0x1.00aeb5da15bdap-3, -0x1.72cece675d1fdp-52, -0x1.00aeb5da15be1p-3, -0x1.fd511fa1c079ep-3,
+    -0x1.78f5a48a8a91fp-2, -0x1.ed50d5cbfa953p-2, -0x1.2cf2304755a60p-1, -0x1.5e7cf55112014p-1,
+    -0x1.8a80b635b6bebp-1, -0x1.b04bbff642e88p-1, -0x1.cf457dcdc158ep-1, -0x1.e6f0e134454ffp-1,
+    -0x1.f6ee5ac2509ffp-1, -0x1.fefd5bfe443fep-1, -0x1.fefd5bfe443fep-1, -0x1.f6ee5ac2509fep-1,
+    -0x1.e6f0e13445500p-1, -0x1.cf457dcdc158cp-1, -0x1.b04bbff642e85p-1, -0x1.8a80b635b6be8p-1,
+    -0x1.5e7cf55112010p-1, -0x1.2cf2304755a59p-1, -0x1.ed50d5cbfa952p-2, -0x1.78f5a48a8a917p-2,
+    -0x1.fd511fa1c078bp-3, -0x1.00aeb5da15bcfp-3,
+};
 
 // DIRECT = true: the object lives in LDS (one per lane, k_fit_harmonic), so runtime indices
 // address it directly; false: per-thread objects held in registers, runtime indices become
@@ -241,8 +275,7 @@ struct Newuoa {
             const int iu = 49;
             const double dang = kTwoPi / (double)(iu + 1);
             for (int i = 1; i <= iu; ++i) {
-                const double ang = (double)i * dang;
-                const double cth = cos(ang), sth = sin(ang);
+                const double cth = kAngCos[i], sth = kAngSin[i];
                 qnew = (sg + cf * cth) * cth + (dg + dhs * cth) * sth;
                 if (qnew < qmin) {
                     qmin = qnew;
@@ -385,8 +418,7 @@ struct Newuoa {
             const int iu = 49;
             const double dang = kTwoPi / (double)(iu + 1);
             for (int i = 1; i <= iu; ++i) {
-                const double ang = (double)i * dang;
-                const double cth = cos(ang), sth = sin(ang);
+                const double cth = kAngCos[i], sth = kAngSin[i];
                 tau = cf1 + (cf2 + cf4 * cth) * cth + (cf3 + cf5 * cth) * sth;
                 if (fabs(tau) > fabs(taumax)) {
                     taumax = tau;
@@ -611,9 +643,8 @@ struct Newuoa {
             const double dang = kTwoPi / (double)(iu + 1);
             par[0] = 1.0;
             for (int i = 1; i <= iu; ++i) {
-                const double ang = (double)i * dang;
-                par[1] = cos(ang);
-                par[2] = sin(ang);
+                par[1] = kAngCos[i];
+                par[2] = kAngSin[i];
 #pragma unroll
                 for (int j = 3; j <= 7; j += 2) {
                     par[j] = par[1] * par[j - 2] - par[2] * par[j - 1];
