@@ -43,7 +43,7 @@ EXPORTS = ("gpd_version", "gpd_strerror", "gpd_device_count", "gpd_fit_batch",
            "gpd_fit_batch_dev", "gpd_chi2_batch", "gpd_chi2_batch_dev", "gpd_buildstates",
            "gpd_synth_fill_dev", "gpd_last_timings", "gpd_fit_windows", "gpd_fit_windows_dev",
            "gpd_process_volt", "gpd_fit_batch_c32", "gpd_fit_batch_c32_dev", "gpd_fit_windows_c32",
-           "gpd_fit_windows_c32_dev", "gpd_buildstates_dev")
+           "gpd_fit_windows_c32_dev", "gpd_buildstates_dev", "gpd_release")
 
 
 class GpdError(RuntimeError):
@@ -72,6 +72,8 @@ def load():
     L.gpd_strerror.argtypes = [ctypes.c_int]
     L.gpd_device_count.restype = ctypes.c_int
     L.gpd_device_count.argtypes = []
+    L.gpd_release.restype = ctypes.c_int
+    L.gpd_release.argtypes = [ctypes.c_int]
     common = [I64, I64, V, V, I64, V, I64, I64, V, V, D, V, U32, I32, V, V, I64]
     L.gpd_fit_batch.restype = ctypes.c_int
     L.gpd_fit_batch.argtypes = common + [I32, ctypes.c_char_p, ctypes.c_size_t]

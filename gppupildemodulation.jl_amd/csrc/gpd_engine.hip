@@ -63,6 +63,13 @@ struct DevCtx {
     // gpd_buildstates_dev: pinned staging of the timer lists, reused once its copy has run
     double *bs_pinned = nullptr;
     hipEvent_t bs_done = nullptr;
+    // host-buffer entry points (gpd_fit_batch & co.): device copies of the caller's arrays in
+    // one grow-only arena and one stream, reused across calls (no hipMalloc/hipFree per
+    // exposure); hmu serialises host calls on this device for the duration of a call
+    std::mutex hmu;
+    char *harena = nullptr;
+    size_t harena_cap = 0;
+    hipStream_t hstream = nullptr;
 };
 
 std::mutex g_mu;
@@ -164,6 +171,21 @@ int gpd_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
     return n;
+}
+
+int gpd_release(int device) {
+    if (device < 0 || device >= gpd_device_count()) return GPD_E_ARG;
+    DevCtx *cx = ctx_for(device);
+    std::lock_guard<std::mutex> hlk(cx->hmu);
+    std::lock_guard<std::mutex> lk(cx->mu);
+    if (hipSetDevice(device) != hipSuccess) return GPD_E_HIP;
+    if (cx->hstream) (void)hipStreamSynchronize(cx->hstream);
+    if (cx->done) (void)hipEventSynchronize(cx->done);
+    (void)hipFree(cx->ws);
+    (void)hipFree(cx->harena);
+    cx->ws = cx->harena = nullptr;
+    cx->ws_cap = cx->harena_cap = 0;
+    return GPD_OK;
 }
 
 }  // extern "C"
@@ -677,25 +699,6 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
             set_err(errbuf_l, errlen_l, "hipSetDevice(%d) failed", g);
             return fail(GPD_E_HIP);
         }
-        double *dt = nullptr;
-        char *dd = nullptr, *dfc = nullptr;
-        c64 *dout = nullptr;
-        int32_t *dfcop = nullptr;
-        int8_t *dst = nullptr;
-        Param *dpar = nullptr;
-        double *dbphi = nullptr;
-        hipStream_t s = nullptr;
-        auto cleanup = [&]() {
-            if (s) (void)hipStreamDestroy(s);
-            (void)hipFree(dt);
-            (void)hipFree(dd);
-            (void)hipFree(dfc);
-            (void)hipFree(dout);
-            (void)hipFree(dfcop);
-            (void)hipFree(dst);
-            (void)hipFree(dpar);
-            (void)hipFree(dbphi);
-        };
         auto chk = [&](hipError_t e, const char *what) {
             if (e != hipSuccess) {
                 set_err(errbuf_l, errlen_l, "%s: %s", what, hipGetErrorString(e));
@@ -703,6 +706,7 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
             }
             return true;
         };
+        auto cleanup = [&]() {};
         // only the FC columns this shard references travel (e.g. 8 of the 40 columns of an
         // exposure matrix passed whole as `fc`)
         int32_t cmin = INT32_MAX, cmax = 0;
@@ -713,21 +717,46 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
         const int64_t nfc = (int64_t)cmax - cmin + 1;
         std::vector<int32_t> fcop_l(fc_of_pixel + p0, fc_of_pixel + p1);
         for (auto &c : fcop_l) c -= cmin;
-        bool ok = chk(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate") &&
-                  chk(hipMalloc(&dt, N * sizeof(double)), "hipMalloc t") &&
-                  chk(hipMalloc(&dd, (size_t)P * N * esz), "hipMalloc d") &&
-                  chk(hipMalloc(&dfc, (size_t)nfc * N * esz), "hipMalloc fc") &&
-                  chk(hipMalloc(&dfcop, P * sizeof(int32_t)), "hipMalloc fcop") &&
-                  chk(hipMalloc(&dpar, nrec * sizeof(Param)), "hipMalloc params") &&
-                  (!state || chk(hipMalloc(&dst, N), "hipMalloc state")) &&
-                  (!bphi || chk(hipMalloc(&dbphi, 2 * P * sizeof(double)), "hipMalloc bphi")) &&
-                  (!out_demod || chk(hipMalloc(&dout, (size_t)P * N * sizeof(c64)), "hipMalloc out"));
-        if (!ok) {
-            cleanup();
-            (void)hipGetLastError();
-            return fail(GPD_E_OOM);
+        DevCtx *cx = ctx_for(g);
+        std::lock_guard<std::mutex> hlk(cx->hmu);
+        size_t off = 0;
+        auto take = [&](size_t bytes) {
+            const size_t o = off;
+            off += align_up(bytes);
+            return o;
+        };
+        const size_t o_t = take(N * sizeof(double)), o_d = take((size_t)P * N * esz),
+                     o_fc = take((size_t)nfc * N * esz), o_fcop = take(P * sizeof(int32_t)),
+                     o_par = take(nrec * sizeof(Param)), o_st = take(state ? N : 0),
+                     o_bphi = take(bphi ? 2 * P * sizeof(double) : 0),
+                     o_out = take(out_demod ? (size_t)P * N * sizeof(c64) : 0);
+        if (!cx->hstream && !chk(hipStreamCreateWithFlags(&cx->hstream, hipStreamNonBlocking),
+                                 "hipStreamCreate"))
+            return fail(GPD_E_HIP);
+        hipStream_t s = cx->hstream;
+        if (cx->harena_cap < off) {
+            if (cx->harena) {
+                (void)hipStreamSynchronize(s);
+                (void)hipFree(cx->harena);
+                cx->harena = nullptr;
+                cx->harena_cap = 0;
+            }
+            if (hipMalloc(&cx->harena, off) != hipSuccess) {
+                (void)hipGetLastError();
+                set_err(errbuf_l, errlen_l, "device arena of %zu bytes: out of device memory", off);
+                return fail(GPD_E_OOM);
+            }
+            cx->harena_cap = off;
         }
-        ok = chk(hipMemcpyAsync(dt, t + s0, N * sizeof(double), hipMemcpyHostToDevice, s), "H2D t") &&
+        char *A = cx->harena;
+        double *dt = (double *)(A + o_t);
+        char *dd = A + o_d, *dfc = A + o_fc;
+        int32_t *dfcop = (int32_t *)(A + o_fcop);
+        Param *dpar = (Param *)(A + o_par);
+        int8_t *dst = state ? (int8_t *)(A + o_st) : nullptr;
+        double *dbphi = bphi ? (double *)(A + o_bphi) : nullptr;
+        c64 *dout = out_demod ? (c64 *)(A + o_out) : nullptr;
+        bool ok = chk(hipMemcpyAsync(dt, t + s0, N * sizeof(double), hipMemcpyHostToDevice, s), "H2D t") &&
              chk(hipMemcpy2DAsync(dd, N * esz, d + (p0 * ldd + s0) * esz, ldd * esz, N * esz, P,
                                   hipMemcpyHostToDevice, s), "H2D d") &&
              chk(hipMemcpy2DAsync(dfc, N * esz, fc + ((int64_t)cmin * ldfc + s0) * esz,

@@ -83,6 +83,11 @@ typedef struct {
 int gpd_version(void);                /* = GPD_ABI_VERSION                            */
 const char *gpd_strerror(int code);   /* static string                                */
 int gpd_device_count(void);           /* visible HIP devices (0 if none)              */
+/* Free the library's cached device memory on `device` (fit workspace and the arena holding
+ * device copies of host-buffer calls; both grow to the largest call and are reused).  Waits
+ * for that device's pending library work.  0 = ok, GPD_E_ARG for a bad device.  No reference
+ * counterpart (Julia frees through its GC); call it after a one-off very large batch. */
+int gpd_release(int device);
 
 /*
  * Fit (and optionally demodulate) a batch of series.  Replaces the diode loop of

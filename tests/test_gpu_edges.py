@@ -89,3 +89,18 @@ def test_alternative_moment_kernels(gpu, oracle, monkeypatch, kernel, faint):
     pert = [oracle.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], state=st, flags=flags,
                              perturb_seed=s, perturb_ulps=128.0) for s in range(1, 13)]
     print(assert_fit_parity(got, ref, pert, label=f"{kernel}/faint={faint}"))
+
+
+def test_release_and_reuse(gpu, oracle):
+    """Host-buffer calls reuse a cached device arena; gpd_release frees it (and the fit
+    workspace) and the next call re-allocates: identical results across the three calls."""
+    B = synth.make_batch(3000, 16, seed=12)
+    args = (B["t"], B["d"], B["fc"], B["fc_of_pixel"])
+    a = gpu.fit_batch(*args, want_output=True)
+    b = gpu.fit_batch(*args, want_output=True)
+    assert gpu.load().gpd_release(0) == 0
+    assert gpu.load().gpd_release(999) == gpu._lib.GPD_E_ARG
+    c = gpu.fit_batch(*args, want_output=True)
+    for x in (b, c):
+        np.testing.assert_array_equal(x[0], a[0])
+        np.testing.assert_array_equal(x[1], a[1])
