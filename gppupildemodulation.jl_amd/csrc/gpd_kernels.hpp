@@ -1239,11 +1239,17 @@ struct HarmChi2 {
 
     // Σ_n J_n(b) e^{-jnϕ} M_n for moments M in the layout of k_moments (F0 re/im at rows 0-1,
     // (A,B,C,D)_n at rows 3+4(n-1)..)
-    __device__ __forceinline__ void combine(const double *__restrict__ m, long long ld, long long col,
+    // The moments are read through a global-address-space pointer: reached through this
+    // out-of-line functor, a plain pointer is generic, and flat loads both cost more and make
+    // every wait drain all outstanding loads (flat counts on vmcnt and lgkmcnt).
+    typedef const __attribute__((address_space(1))) double gdouble;
+    __device__ __forceinline__ void combine(const double *__restrict__ m_, long long ld, long long col,
                                             const double (&J)[KH + 2], double cph, double sph,
                                             double &Sr, double &Si) const {
-        Sr = J[0] * m[0 * ld + col];
-        Si = J[0] * m[1 * ld + col];
+        gdouble *p = (gdouble *)m_ + col;  // row r of this series at p[r·ld]
+        Sr = J[0] * p[0];
+        Si = J[0] * p[ld];
+        p += 3 * ld;
         double cn = 1.0, sn = 0.0;
 #pragma unroll
         for (int n = 1; n <= KH; ++n) {
@@ -1251,10 +1257,15 @@ struct HarmChi2 {
             const double s2 = sn * cph + cn * sph;
             cn = c2;
             sn = s2;
-            const double A = m[(long long)(3 + 4 * (n - 1) + 0) * ld + col];
-            const double B = m[(long long)(3 + 4 * (n - 1) + 1) * ld + col];
-            const double C = m[(long long)(3 + 4 * (n - 1) + 2) * ld + col];
-            const double D = m[(long long)(3 + 4 * (n - 1) + 3) * ld + col];
+            gdouble *q = p;
+            const double A = *q;
+            q += ld;
+            const double B = *q;
+            q += ld;
+            const double C = *q;
+            q += ld;
+            const double D = *q;
+            p = q + ld;
             double tr, ti;
             if ((n & 1) == 0) {
                 tr = fma(A, cn, -(D * sn));
@@ -1275,10 +1286,10 @@ struct HarmChi2 {
     bool prof;
 
     __device__ __attribute__((noinline)) double operator()(const double (&x)[2]) {
-        if (!prof) return eval(x);
-        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        // one inlined copy of eval (the cycle split only brackets it)
+        const unsigned long long t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
         const double r = eval(x);
-        prof_cycles += __builtin_amdgcn_s_memtime() - t0;
+        if (prof) prof_cycles += __builtin_amdgcn_s_memtime() - t0;
         return r;
     }
     __device__ __forceinline__ double eval(const double (&x)[2]) {
