@@ -121,8 +121,10 @@ __host__ __device__ __forceinline__ void bessel_j(double b, double (&J)[KP + 1])
 // ---------------------------------------------------------------------------------------
 // Deterministic sum over a workgroup of WG threads (WG multiple of 64) of NV doubles.
 // lds must hold (WG/64)*NV doubles.  On return every thread holds the same totals.
-template <int WG, int NV>
-__device__ __forceinline__ void block_sum(double (&v)[NV], double *lds) {
+// PT: double* or an LDS-qualified pointer (out-of-line callers pass the latter so that the
+// partials go through ds_ instructions, not flat ones)
+template <int WG, int NV, class PT = double *>
+__device__ __forceinline__ void block_sum(double (&v)[NV], PT lds) {
     constexpr int NW = WG / 64;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll

@@ -1421,10 +1421,56 @@ struct ExactChi2 {
     long long s0, s1;  // sample range (the series' window)
     int nfev;
 
-    __device__ __forceinline__ bool load(long long i, c64 &p, double &w) const {
+    // Global-address-space views of the problem's arrays, taken once per evaluation: this
+    // functor runs out of line, where plain pointers are generic and every flat load's wait
+    // drains all outstanding loads.
+    typedef const __attribute__((address_space(1))) double gdouble;
+    typedef const __attribute__((address_space(1))) c64 gc64;
+    typedef const __attribute__((address_space(1))) c32 gc32;
+    typedef const __attribute__((address_space(1))) int8_t gi8;
+    typedef __attribute__((address_space(3))) double ldouble;
+    struct View {
+        gdouble *t;
+        gc64 *d, *fc, *src;
+        gc32 *d32, *fc32;
+        gi8 *state;
+        double omega;
+        bool only_high;
+    };
+    __device__ __forceinline__ View view() const {
+        View v;
+        v.t = (gdouble *)pb->t;
+        v.d = (gc64 *)pb->d;
+        v.d32 = (gc32 *)pb->d32;
+        v.fc = (gc64 *)pb->fc;
+        v.fc32 = (gc32 *)pb->fc32;
+        v.src = (gc64 *)src;
+        v.state = (gi8 *)pb->state;
+        v.omega = pb->omega;
+        v.only_high = (pb->flags & F_ONLY_HIGH) != 0;
+        return v;
+    }
+    static __device__ __forceinline__ c64 ld(gc64 *p) { return c64{p->re, p->im}; }
+    static __device__ __forceinline__ c64 ld(gc32 *p) { return c64{(double)p->re, (double)p->im}; }
+    __device__ __forceinline__ c64 d_of(const View &v, long long off) const {
+        return v.d32 ? ld(v.d32 + off) : ld(v.d + off);
+    }
+    // sample_valid (TRANSIENT dropped, onlyhigh keeps HIGH ∪ NORMAL), src/Modulation.jl:373-382
+    __device__ __forceinline__ bool valid(const View &v, long long i, int &st) const {
+        if (v.state == nullptr) {
+            st = 0;
+            return true;
+        }
+        st = v.state[i];
+        if (st == -1) return false;
+        if (v.only_high) return st == 3 || st == 2;
+        return true;
+    }
+    __device__ __forceinline__ bool load(const View &v, long long i, c64 &p, double &w) const {
         int st;
-        if (!sample_valid(*pb, i, st)) return false;
-        const c64 ph = PHBUF ? src[i] : fc_phasor(fc_at(*pb, foff + i));
+        if (!valid(v, i, st)) return false;
+        const c64 ph = PHBUF ? ld(v.src + i)
+                             : fc_phasor(v.fc32 ? ld(v.fc32 + foff + i) : ld(v.fc + foff + i));
         if (FAINT) {
             double m = m5[0], ww = w5[0];
 #pragma unroll
@@ -1440,8 +1486,9 @@ struct ExactChi2 {
         }
         return true;
     }
-    __device__ __forceinline__ c64 model(long long i, const c64 &p, double b, double phi) const {
-        double th = pb->omega * pb->t[i];
+    __device__ __forceinline__ c64 model(const View &v, long long i, const c64 &p, double b,
+                                         double phi) const {
+        double th = v.omega * v.t[i];
         th = th + phi;
         const double beta = b * sin(th);
         return cmul(p, cisj(beta));  // power * exp(ȷ b sin(ωt+ϕ)) (src/Modulation.jl:137)
@@ -1450,14 +1497,16 @@ struct ExactChi2 {
     __device__ double operator()(const double (&x)[2]) {
         ++nfev;
         const double b = x[0], phi = x[1];
+        const View V = view();
+        ldouble *lp = (ldouble *)lds;
         if (OFFS) {
             double v[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // a11, a12(2), a22, b1(2), b2(2)
             for (long long i = s0 + threadIdx.x; i < s1; i += EXACT_WG) {
                 c64 p;
                 double w;
-                if (!load(i, p, w)) continue;
-                const c64 m = model(i, p, b, phi);
-                const c64 dd = d_at(*pb, doff + i);
+                if (!load(V, i, p, w)) continue;
+                const c64 m = model(V, i, p, b, phi);
+                const c64 dd = d_of(V, doff + i);
                 v[0] += w;
                 v[1] += w * m.re;
                 v[2] += w * m.im;
@@ -1468,7 +1517,7 @@ struct ExactChi2 {
                 v[6] += pr.re;
                 v[7] += pr.im;
             }
-            block_sum<EXACT_WG, 8>(v, lds);
+            block_sum<EXACT_WG, 8>(v, lp);
             // StaticArrays 2×2 Cramer solve (src/Modulation.jl:189-192)
             const c64 A11 = {v[0], 0.0}, A12 = {v[1], v[2]}, A21 = {v[1], -v[2]}, A22 = {v[3], 0.0};
             const c64 b1 = {v[4], v[5]}, b2 = {v[6], v[7]};
@@ -1487,17 +1536,17 @@ struct ExactChi2 {
             for (long long i = s0 + threadIdx.x; i < s1; i += EXACT_WG) {
                 c64 p;
                 double w;
-                if (!load(i, p, w)) continue;
-                const c64 m = model(i, p, b, phi);
+                if (!load(V, i, p, w)) continue;
+                const c64 m = model(V, i, p, b, phi);
                 const c64 mwc = {m.re * w, -(m.im * w)};  // conj(model .* weight)
-                const c64 xx = cmul(mwc, d_at(*pb, doff + i));
+                const c64 xx = cmul(mwc, d_of(V, doff + i));
                 const c64 yy = cmul(mwc, m);
                 v[0] += xx.re;
                 v[1] += xx.im;
                 v[2] += yy.re;
                 v[3] += yy.im;
             }
-            block_sum<EXACT_WG, 4>(v, lds);
+            block_sum<EXACT_WG, 4>(v, lp);
             const c64 aa = cdiv(c64{v[0], v[1]}, c64{v[2], v[3]});  // (src/Modulation.jl:144)
             c_re = c_im = 0.0;
             a_re = aa.re;
@@ -1509,17 +1558,17 @@ struct ExactChi2 {
         for (long long i = s0 + threadIdx.x; i < s1; i += EXACT_WG) {
             c64 p;
             double w;
-            if (!load(i, p, w)) continue;
-            c64 mm = cmul(aa, model(i, p, b, phi));
+            if (!load(V, i, p, w)) continue;
+            c64 mm = cmul(aa, model(V, i, p, b, phi));
             if (OFFS) {
                 mm.re = c_re + mm.re;
                 mm.im = c_im + mm.im;
             }
-            const c64 dd = d_at(*pb, doff + i);
+            const c64 dd = d_of(V, doff + i);
             const double rr = mm.re - dd.re, ri = mm.im - dd.im;
             s[0] += w * (rr * rr + ri * ri);
         }
-        block_sum<EXACT_WG, 1>(s, lds);
+        block_sum<EXACT_WG, 1>(s, lp);
         return s[0] / nvalid;
     }
 };
