@@ -364,7 +364,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         // the producer/consumer kernel (non-faint whole-exposure series, also the UNIT pass
         // of harmonic fitoffsets) reads the k_table_mix layout when mixing; every other
         // moment kernel the plain rows
-        const bool ws_kernel = use_mfma && window == 0 && !faint && !(mk && std::string(mk) == "mfma1");
+        const bool ws_kernel = use_mfma && window == 0 && !(mk && std::string(mk) == "mfma1");
         tmix = mix && ws_kernel;
         if (tmix)
             k_table_mix<<<(unsigned)((N + MM_TS - 1) / MM_TS * MM_TS / 256 + 1), 256, 0, stream>>>(
@@ -380,12 +380,21 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             mark("moments_win");
         } else if (use_mfma) {
             dim3 g((unsigned)((P + MM_PIX - 1) / MM_PIX), (unsigned)L.nch);
-            if (faint && is_c32)
+            const bool mfma1 = mk && std::string(mk) == "mfma1";  // single-role kernel (A/B runs)
+            if (faint && mfma1 && is_c32)
                 k_moments_mfma<true, c32><<<g, 256, 0, stream>>>(pb, tab, fstat, L.chunk, part);
-            else if (faint)
+            else if (faint && mfma1)
                 k_moments_mfma<true><<<g, 256, 0, stream>>>(pb, tab, fstat, L.chunk, part);
-            else if (mk && std::string(mk) == "mfma1")  // single-role kernel (A/B runs)
+            else if (mfma1)
                 k_moments_mfma<false><<<g, 256, 0, stream>>>(pb, tab, fstat, L.chunk, part);
+            else if (faint && is_c32 && tmix)  // faint series: the producer/consumer kernel, weighted
+                k_moments_ws<0, false, c32, 2, true, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part, fstat);
+            else if (faint && tmix)
+                k_moments_ws<0, false, c64, 2, true, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part, fstat);
+            else if (faint && is_c32)
+                k_moments_ws<0, false, c32, 2, false, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part, fstat);
+            else if (faint)
+                k_moments_ws<0, false, c64, 2, false, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part, fstat);
             else if (!tmix && is_c32)  // all-f64 MFMA variants (GPD_MIX=0)
                 k_moments_ws<0, false, c32, 2, false><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
             else if (!tmix)

@@ -339,36 +339,59 @@ __global__ __launch_bounds__(256) void k_faint_stats(Problem pb, double *__restr
     double v[15];
 #pragma unroll
     for (int q = 0; q < 15; ++q) v[q] = 0.0;
-    for (long long i = sp.s0 + threadIdx.x; i < sp.s1; i += 256) {
-        int st;
-        if (!sample_valid(pb, i, st)) continue;
-        const c64 z = d_at(pb, doff + i);
-        const double ad = hypot(z.re, z.im);
-        const double d2 = z.re * z.re + z.im * z.im;
+    // each thread's samples i, i+256, … are summed in that order (the oracle's partials); the
+    // loads of U consecutive ones are issued together (U in flight instead of one)
+    constexpr int U = 4;
+    auto fetch = [&](long long i0, c64 (&z)[U], int (&st)[U], bool (&ok)[U]) {
 #pragma unroll
-        for (int q = 0; q < 5; ++q)
-            if (st + 1 == q) {
-                v[q] += 1.0;
-                v[5 + q] += ad;
-                v[10 + q] += d2;
-            }
+        for (int u = 0; u < U; ++u) {
+            const long long i = i0 + 256 * u;
+            ok[u] = i < sp.s1;
+            const long long ic = ok[u] ? i : sp.s0;
+            z[u] = d_at(pb, doff + ic);
+            ok[u] = ok[u] && sample_valid(pb, ic, st[u]);
+        }
+    };
+    for (long long i0 = sp.s0 + threadIdx.x; i0 < sp.s1; i0 += 256 * U) {
+        c64 z[U];
+        int st[U];
+        bool ok[U];
+        fetch(i0, z, st, ok);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!ok[u]) continue;
+            const double ad = hypot(z[u].re, z[u].im);
+            const double d2 = z[u].re * z[u].re + z[u].im * z[u].im;
+#pragma unroll
+            for (int q = 0; q < 5; ++q)
+                if (st[u] + 1 == q) {
+                    v[q] += 1.0;
+                    v[5 + q] += ad;
+                    v[10 + q] += d2;
+                }
+        }
     }
     block_sum<256, 15>(v, lds);
     double m[5];
 #pragma unroll
     for (int q = 0; q < 5; ++q) m[q] = v[5 + q] / v[q];
     double s[5] = {0, 0, 0, 0, 0};
-    for (long long i = sp.s0 + threadIdx.x; i < sp.s1; i += 256) {
-        int st;
-        if (!sample_valid(pb, i, st)) continue;
-        const c64 z = d_at(pb, doff + i);
-        const double ad = hypot(z.re, z.im);
+    for (long long i0 = sp.s0 + threadIdx.x; i0 < sp.s1; i0 += 256 * U) {
+        c64 z[U];
+        int st[U];
+        bool ok[U];
+        fetch(i0, z, st, ok);
 #pragma unroll
-        for (int q = 0; q < 5; ++q)
-            if (st + 1 == q) {
-                const double dv = ad - m[q];
-                s[q] += dv * dv;
-            }
+        for (int u = 0; u < U; ++u) {
+            if (!ok[u]) continue;
+            const double ad = hypot(z[u].re, z[u].im);
+#pragma unroll
+            for (int q = 0; q < 5; ++q)
+                if (st[u] + 1 == q) {
+                    const double dv = ad - m[q];
+                    s[q] += dv * dv;
+                }
+        }
     }
     block_sum<256, 5>(s, lds);
     if (threadIdx.x == 0) {
@@ -748,6 +771,7 @@ struct BoolTag {
 template <class TS>
 struct WsRegs {
     TS d[4][4], f[4];
+    int st;  // FAINT: MetState code of the lane's sample
 };
 
 // DBG (timing experiments only, results invalid): 1 = consumers skip the MFMA phase,
@@ -778,13 +802,20 @@ __device__ __forceinline__ void split_bf16x2(float f0, float f1, unsigned &h, un
     l = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf16x2));
 }
 
-template <int DBG = 0, bool UNIT = false, class TS = c64, int POL = 0, bool MIX = true>
+// FAINT: q = w·m p̄ d with the per-series, per-state weight w and power m of
+// compute_mean_var_power (fstat, src/Faint.jl:89-100; src/Modulation.jl:392-396); samples
+// outside the valid mask (TRANSIENT, or not HIGH/NORMAL with onlyhigh: src/Modulation.jl:373-382)
+// contribute 0.  The state byte of each sample is loaded with the tile.
+template <int DBG = 0, bool UNIT = false, class TS = c64, int POL = 0, bool MIX = true,
+          bool FAINT = false>
 __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double *__restrict__ tab,
                                                        long long chunk_len,
-                                                       double *__restrict__ part) {
+                                                       double *__restrict__ part,
+                                                       const double *__restrict__ fstat = nullptr) {
     __shared__ c64 qs[2][MM_TS * MM_ROW];
     __shared__ __attribute__((aligned(16))) double ts[2][MM_TS * 2 * KH];
     __shared__ int fcl[MM_PIX];
+    __shared__ double wml[FAINT ? MM_PIX * 5 : 1];  // FAINT: w·m per series and state
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const long long p0 = (long long)blockIdx.x * MM_PIX;
     const long long s_begin = (long long)blockIdx.y * chunk_len;
@@ -794,6 +825,11 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
     if (tid < MM_PIX) {
         const long long p = p0 + tid;
         fcl[tid] = p < pb.P ? pb.fcop[p] : 0;
+        if constexpr (FAINT) {
+#pragma unroll
+            for (int q = 0; q < 5; ++q)
+                wml[tid * 5 + q] = p < pb.P ? fstat[p * 16 + 5 + q] * fstat[p * 16 + q] : 0.0;
+        }
     }
     __syncthreads();
     // general layout: some series of the workgroup does not use its 4-group's FC column
@@ -842,6 +878,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             const long long s0 = s_begin + (long long)it * MM_TS;
             const long long sl = (s0 + ss) < Nm1 ? (s0 + ss) : Nm1;
             const int s016 = (int)(s0 * ES);
+            if constexpr (FAINT) R.st = pb.state[sl];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 R.f[r] = fcb[r][sl];
@@ -871,9 +908,15 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
         };
         auto stage_q = [&](const WsRegs<TS> &R, int it, auto gen, auto partial) {
             const long long s = s_begin + (long long)it * MM_TS + ss;
-            const bool sok = s < s_end;
+            bool sok = s < s_end;
             const long long sl = s < Nm1 ? s : Nm1;
             c64 *q_out = qs[it & 1];
+            int stc = 0;  // FAINT: index of the sample's state in wml (code + 1)
+            if constexpr (FAINT) {
+                const int st = R.st;
+                sok = sok && st != -1 && (!(pb.flags & F_ONLY_HIGH) || st == 3 || st == 2);
+                stc = st + 1;
+            }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const c64 ph = unit_phasor(widen(R.f[r]));
@@ -891,7 +934,11 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
                         q.re = fma(pj.re, dv.re, pj.im * dv.im);
                         q.im = fma(pj.re, dv.im, -(pj.im * dv.re));
                     }
-                    if (decltype(partial)::value) {  // rows beyond P read as 0 already
+                    if constexpr (FAINT) {
+                        const double f = wml[pl * 5 + stc];
+                        q.re = sok ? q.re * f : 0.0;
+                        q.im = sok ? q.im * f : 0.0;
+                    } else if (decltype(partial)::value) {  // rows beyond P read as 0 already
                         q.re = sok ? q.re : 0.0;
                         q.im = sok ? q.im : 0.0;
                     }
