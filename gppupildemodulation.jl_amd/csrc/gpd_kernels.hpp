@@ -881,7 +881,16 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             if constexpr (FAINT) R.st = pb.state[sl];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                R.f[r] = fcb[r][sl];
+                if constexpr (POL == 2) {  // FC columns are read once per launch too
+                    typedef double nv2d __attribute__((ext_vector_type(2)));
+                    typedef float nv2f __attribute__((ext_vector_type(2)));
+                    if constexpr (sizeof(TS) == 16)
+                        R.f[r] = __builtin_bit_cast(TS, __builtin_nontemporal_load((const nv2d *)&fcb[r][sl]));
+                    else
+                        R.f[r] = __builtin_bit_cast(TS, __builtin_nontemporal_load((const nv2f *)&fcb[r][sl]));
+                } else {
+                    R.f[r] = fcb[r][sl];
+                }
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     if constexpr (UNIT) continue;
