@@ -126,6 +126,7 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
             nch = std::max<long long>(1, (mfma ? 6144 : 8192) / std::max<long long>(npg, 1));
         }
     }
+    if (const char *e = getenv("GPD_NCH")) nch = std::max(1LL, atoll(e));  // A/B sweeps only
     nch = std::min<long long>(nch, std::max<long long>(1, (N + 255) / 256));
     long long chunk = (N + nch - 1) / nch;
     chunk = (chunk + MM_TS - 1) / MM_TS * MM_TS;
