@@ -88,7 +88,8 @@ DevCtx *ctx_for(int dev) {
 size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
 struct Layout {
-    size_t info, tab, part, mom, aux, fstat, raw, list, phbuf, partG, momG, auxG, fcid, d0, total;
+    size_t info, tab, part, mom, aux, fstat, raw, list, phbuf, partG, momG, auxG, fcid, d0, mcache, total;
+    long long mstride;  // model-cache elements per exact-path workgroup (0: no cache)
     int nch;
     long long chunk;
 };
@@ -150,6 +151,11 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     L.auxG = take(harm_offs ? (size_t)4 * n_fc * sizeof(double) : 0);
     L.fcid = take(harm_offs ? (size_t)n_fc * sizeof(int32_t) : 0);
     L.d0 = take(harm_offs ? (size_t)2 * P * sizeof(double) : 0);
+    // exact evaluator: one model-cache slot of N complex per workgroup of the fit grid
+    // (min(P, 1024) workgroups), when that stays below 8 GB
+    const size_t mc_bytes = (size_t)std::min<long long>(P, 1024) * (size_t)N * sizeof(c64);
+    L.mstride = (!harmonic && mc_bytes <= (size_t(8) << 30)) ? N : 0;
+    L.mcache = take(L.mstride ? mc_bytes : 0);
     L.total = off;
     return L;
 }
@@ -535,9 +541,9 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             k_chi2_exact<FA, OF, PH><<<(unsigned)P, EXACT_WG, 0, stream>>>(pb, info, ph, fstat, \
                                                                            bphi, outp);         \
         else                                                                                    \
-            k_fit_exact<FA, OF, PH><<<exact_grid, EXACT_WG, 0, stream>>>(pb, info, ph, fstat,   \
-                                                                         nullptr, nullptr,      \
-                                                                         outp, raw, 0);         \
+            k_fit_exact<FA, OF, PH><<<exact_grid, EXACT_WG, 0, stream>>>(                     \
+                pb, info, ph, fstat, nullptr, nullptr, outp, raw, 0,                            \
+                L.mstride ? (c64 *)(ws + L.mcache) : nullptr, L.mstride);                      \
     } while (0)
         if (faint) {
             if (offs) { if (phbuf) GPD_LAUNCH_EXACT(true, true, true); else GPD_LAUNCH_EXACT(true, true, false); }

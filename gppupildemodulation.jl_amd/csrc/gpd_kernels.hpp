@@ -1476,6 +1476,10 @@ struct ExactChi2 {
     double a_re, a_im, c_re, c_im;
     long long s0, s1;  // sample range (the series' window)
     int nfev;
+    // model cache (nullptr: none): the final pass of each evaluation reads the model the first
+    // pass computed (same values, so the same sums) instead of re-evaluating sin/sincos and the
+    // FC phasor; one slot of s1 − s0 elements per workgroup
+    c64 *mc;
 
     // Global-address-space views of the problem's arrays, taken once per evaluation: this
     // functor runs out of line, where plain pointers are generic and every flat load's wait
@@ -1506,7 +1510,16 @@ struct ExactChi2 {
         v.only_high = (pb->flags & F_ONLY_HIGH) != 0;
         return v;
     }
+    typedef __attribute__((address_space(1))) c64 gmc64;
     static __device__ __forceinline__ c64 ld(gc64 *p) { return c64{p->re, p->im}; }
+    // weight of a valid sample (FAINT: w of its state; the power m is inside the cached model)
+    __device__ __forceinline__ double weight_of(int st) const {
+        if (!FAINT) return 1.0;
+        double ww = w5[0];
+#pragma unroll
+        for (int q = 1; q < 5; ++q) ww = (st + 1 == q) ? w5[q] : ww;
+        return ww;
+    }
     static __device__ __forceinline__ c64 ld(gc32 *p) { return c64{(double)p->re, (double)p->im}; }
     __device__ __forceinline__ c64 d_of(const View &v, long long off) const {
         return v.d32 ? ld(v.d32 + off) : ld(v.d + off);
@@ -1555,6 +1568,7 @@ struct ExactChi2 {
         const double b = x[0], phi = x[1];
         const View V = view();
         ldouble *lp = (ldouble *)lds;
+        gmc64 *mcg = (gmc64 *)mc;
         if (OFFS) {
             double v[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // a11, a12(2), a22, b1(2), b2(2)
             for (long long i = s0 + threadIdx.x; i < s1; i += EXACT_WG) {
@@ -1562,6 +1576,10 @@ struct ExactChi2 {
                 double w;
                 if (!load(V, i, p, w)) continue;
                 const c64 m = model(V, i, p, b, phi);
+                if (mcg) {
+                    mcg[i - s0].re = m.re;
+                    mcg[i - s0].im = m.im;
+                }
                 const c64 dd = d_of(V, doff + i);
                 v[0] += w;
                 v[1] += w * m.re;
@@ -1594,6 +1612,10 @@ struct ExactChi2 {
                 double w;
                 if (!load(V, i, p, w)) continue;
                 const c64 m = model(V, i, p, b, phi);
+                if (mcg) {
+                    mcg[i - s0].re = m.re;
+                    mcg[i - s0].im = m.im;
+                }
                 const c64 mwc = {m.re * w, -(m.im * w)};  // conj(model .* weight)
                 const c64 xx = cmul(mwc, d_of(V, doff + i));
                 const c64 yy = cmul(mwc, m);
@@ -1612,10 +1634,19 @@ struct ExactChi2 {
         double s[1] = {0.0};
         const c64 aa = {a_re, a_im};
         for (long long i = s0 + threadIdx.x; i < s1; i += EXACT_WG) {
-            c64 p;
+            c64 m;
             double w;
-            if (!load(V, i, p, w)) continue;
-            c64 mm = cmul(aa, model(V, i, p, b, phi));
+            if (mcg) {  // the same thread wrote element i in the first pass
+                int st;
+                if (!valid(V, i, st)) continue;
+                w = weight_of(st);
+                m = c64{mcg[i - s0].re, mcg[i - s0].im};
+            } else {
+                c64 p;
+                if (!load(V, i, p, w)) continue;
+                m = model(V, i, p, b, phi);
+            }
+            c64 mm = cmul(aa, m);
             if (OFFS) {
                 mm.re = c_re + mm.re;
                 mm.im = c_im + mm.im;
@@ -1642,6 +1673,7 @@ __device__ __forceinline__ void setup_exact(F &f, const Problem &pb, long long k
     f.foff = g * pb.ldfc;
     f.src = phbuf ? phbuf + g * pb.N : nullptr;
     f.lds = lds;
+    f.mc = nullptr;
     f.s0 = sp.s0;
     f.s1 = sp.s1;
     if (pb.win > 0) {
@@ -1664,7 +1696,9 @@ __global__ __launch_bounds__(EXACT_WG) void k_fit_exact(Problem pb, const Info *
                                                         const int *__restrict__ list,
                                                         const int *__restrict__ count,
                                                         Param *__restrict__ out,
-                                                        double *__restrict__ raw, int extra_status) {
+                                                        double *__restrict__ raw, int extra_status,
+                                                        c64 *__restrict__ mcache = nullptr,
+                                                        long long mstride = 0) {
     __shared__ double lds[(EXACT_WG / 64) * 8];
     const long long total = list ? (long long)(*count) : pb.P;
     const double nvalid = (double)info->nvalid;
@@ -1672,6 +1706,7 @@ __global__ __launch_bounds__(EXACT_WG) void k_fit_exact(Problem pb, const Info *
         const long long k = list ? (long long)list[idx] : idx;
         ExactChi2<FAINT, OFFS, PHBUF> f;
         setup_exact(f, pb, k, PHBUF ? phbuf : nullptr, lds, nvalid);
+        if (mcache) f.mc = mcache + (long long)blockIdx.x * mstride;
         if (FAINT) {
 #pragma unroll
             for (int q = 0; q < 5; ++q) {
