@@ -211,3 +211,20 @@ def test_newuoa_angle_table_is_the_oracles_libm():
         vals = [float.fromhex(v) for v in re.findall(r"-?0x[0-9a-f.]+p[-+]\d+", body)]
         assert len(vals) == 50
         assert vals == [fn(float(i) * dang) for i in range(50)]
+
+
+def _build_c_example(out):
+    lib = os.path.join(ROOT, "gppupildemodulation.jl_amd")
+    subprocess.run(["gcc", "-O2", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "examples", "demod_exposure.c"), "-L", lib, "-lgpdemod",
+                    f"-Wl,-rpath,{lib}", "-lm", "-o", str(out)], check=True)
+    return out
+
+
+def test_c_host_example_builds_against_the_abi(gpd, tmp_path):
+    """A plain C host (examples/demod_exposure.c) compiles and links against include/gpdemod.h
+    and libgpdemod.so — the boundary needs no Python or torch types."""
+    exe = _build_c_example(tmp_path / "demod_exposure")
+    r = subprocess.run([str(exe), "1000"], capture_output=True, text=True, timeout=60)
+    if gpd.load().gpd_device_count() == 0:
+        assert r.returncode == 3 and "no HIP device" in r.stderr

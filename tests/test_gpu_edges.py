@@ -104,3 +104,14 @@ def test_release_and_reuse(gpu, oracle):
     for x in (b, c):
         np.testing.assert_array_equal(x[0], a[0])
         np.testing.assert_array_equal(x[1], a[1])
+
+
+def test_c_host_example_runs(gpu, tmp_path):
+    """examples/demod_exposure.c: one exposure (32 diodes + 8 FC columns) through gpd_fit_batch
+    from plain C recovers every diode's b."""
+    import subprocess
+    from test_abi import _build_c_example
+    exe = _build_c_example(tmp_path / "demod_exposure")
+    r = subprocess.run([str(exe), "20000"], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-1000:]
+    assert "ok: 32/32" in r.stdout
