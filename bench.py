@@ -69,12 +69,18 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
+    # GPD_DIST_BACKEND=gloo: rehearsal of the multi-rank path with several ranks on fewer GPUs
+    # (ranks share devices round-robin, records gathered through host memory); the scaling runs
+    # use the default "nccl" = RCCL over xGMI, one rank per GPU
+    backend = os.environ.get("GPD_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     dist = None
     if world > 1:
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     stream = torch.cuda.current_stream(dev)
@@ -127,6 +133,9 @@ def main():
                     fcop.data_ptr(), None, gpd.M_2PI, None, flags, 60,
                     params.data_ptr(), None, N, local, sptr, err, len(err))
         gpd._lib.check(r, err)
+        if backend != "nccl" and world > 1:
+            g = shard.gather_records(params.cpu(), world, rank)
+            return None if g is None else g.to(dev)
         return shard.gather_records(params, world, rank)
 
     for _ in range(args.warmup):
@@ -147,7 +156,8 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
     if dist:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        e = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 
@@ -206,7 +216,8 @@ def main():
                    "series_per_gpu": P, "samples": N, "total_series": world * P,
                    "method": args.method, "t0": args.t0, "storage": args.storage,
                    "parallelism": f"series-shard x{world}",
-                   "gather": "RCCL gather of 64-B records to rank 0" if world > 1 else "none"},
+                   "gather": ("none" if world == 1 else "RCCL gather of 64-B records to rank 0"
+                              if backend == "nccl" else f"{backend} gather (multi-rank rehearsal)")},
         "roofline": roofline, "cpu_baseline": cpu, "kernels_ms": kernels, "fits": fits,
     }
     print(json.dumps(out))

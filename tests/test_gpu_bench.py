@@ -32,3 +32,21 @@ def test_bench_json_contract():
     cb = out["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0
     assert out["fits"]["nan"] == 0
+
+
+def test_bench_two_ranks_rehearsal():
+    """The multi-rank path of bench.py (torch.distributed.run, barrier, max-over-ranks time,
+    gather of the records to rank 0, one JSON line from rank 0) with two ranks sharing cuda:0
+    under gloo (GPD_DIST_BACKEND) — the scaling runs use RCCL with one rank per GPU."""
+    env = dict(os.environ, GPD_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                        "--master-port", "29517", os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--pixels", "256", "--samples", "4096", "--steps", "2", "--warmup", "1",
+                        "--no-cpu"], capture_output=True, text=True, timeout=110, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["total_series"] == 512
+    assert out["scaling"] == "weak" and out["value"] > 0
