@@ -87,12 +87,29 @@ __device__ __forceinline__ Span span_of(const Problem &pb, long long k) {
     return {k - w * pb.ncol, s0, s0 + pb.win < pb.N ? s0 + pb.win : pb.N};
 }
 
+// Loads through the global address space.  The Problem's pointers arrive inside a by-value
+// struct, where the compiler only sees generic pointers: plain indexing emits flat loads, whose
+// waits drain every outstanding memory operation (flat counts on vmcnt and lgkmcnt).  Every
+// Problem array is device (global) memory.
+__device__ __forceinline__ c64 gld(const c64 *p) {
+    const __attribute__((address_space(1))) c64 *g = (const __attribute__((address_space(1))) c64 *)p;
+    return c64{g->re, g->im};
+}
+__device__ __forceinline__ c32 gld(const c32 *p) {
+    const __attribute__((address_space(1))) c32 *g = (const __attribute__((address_space(1))) c32 *)p;
+    return c32{g->re, g->im};
+}
+template <class T>
+__device__ __forceinline__ T gld(const T *p) {
+    return *(const __attribute__((address_space(1))) T *)p;
+}
+
 // Element `off` of the series / FC storage, widened to Float64 (uniform branch on the type).
 __device__ __forceinline__ c64 d_at(const Problem &pb, long long off) {
-    return pb.d32 ? widen(pb.d32[off]) : pb.d[off];
+    return pb.d32 ? widen(gld(pb.d32 + off)) : gld(pb.d + off);
 }
 __device__ __forceinline__ c64 fc_at(const Problem &pb, long long off) {
-    return pb.fc32 ? widen(pb.fc32[off]) : pb.fc[off];
+    return pb.fc32 ? widen(gld(pb.fc32 + off)) : gld(pb.fc + off);
 }
 // Typed base pointers for the kernels instantiated per storage type TS (c64 or c32).
 template <class TS>
@@ -111,7 +128,7 @@ __device__ __forceinline__ bool sample_valid(const Problem &pb, long long i, int
         st = 0;
         return true;
     }
-    st = pb.state[i];
+    st = gld(pb.state + i);
     if (st == -1) return false;  // TRANSIENT always dropped (src/Modulation.jl:380-382)
     if (pb.flags & F_ONLY_HIGH) return st == 3 || st == 2;  // HIGH ∪ NORMAL (:375-376)
     return true;
@@ -197,7 +214,7 @@ __global__ __launch_bounds__(1024) void k_prepare(Problem pb, Info *info) {
     for (long long i = threadIdx.x; i < pb.N; i += 1024) {
         int st;
         if (!sample_valid(pb, i, st)) continue;
-        const double x = fabs(pb.omega * pb.t[i]);
+        const double x = fabs(pb.omega * gld(pb.t + i));
         cnt += 1.0;
         xmn = fmin(xmn, x);
         xmx = fmax(xmx, x);
@@ -460,7 +477,7 @@ __global__ __launch_bounds__(64) void k_moments(Problem pb, const double *__rest
             c64 dv = {0.0, 0.0}, pv = {0.0, 0.0};
             if (pp < pb.P && ss < s_end) {
                 dv = d_at(pb, pp * pb.ldd + ss);
-                const c64 z = fc_at(pb, (long long)pb.fcop[pp] * pb.ldfc + ss);
+                const c64 z = fc_at(pb, (long long)gld(pb.fcop + pp) * pb.ldfc + ss);
                 const double r2 = z.re * z.re + z.im * z.im;
                 if (r2 > 0.0) {
                     const double inv = 1.0 / sqrt(r2);
@@ -878,7 +895,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             const long long s0 = s_begin + (long long)it * MM_TS;
             const long long sl = (s0 + ss) < Nm1 ? (s0 + ss) : Nm1;
             const int s016 = (int)(s0 * ES);
-            if constexpr (FAINT) R.st = pb.state[sl];
+            if constexpr (FAINT) R.st = gld(pb.state + sl);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 if constexpr (POL == 2) {  // FC columns are read once per launch too
@@ -889,7 +906,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
                     else
                         R.f[r] = __builtin_bit_cast(TS, __builtin_nontemporal_load((const nv2f *)&fcb[r][sl]));
                 } else {
-                    R.f[r] = fcb[r][sl];
+                    R.f[r] = gld(fcb[r] + sl);
                 }
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -1874,7 +1891,7 @@ __global__ __launch_bounds__(256) void k_output(Problem pb, const Param *__restr
     c64 *o = outd + sp.col * ldo;
     for (long long i = sp.s0 + (long long)blockIdx.x * 256 + threadIdx.x; i < sp.s1;
          i += (long long)gridDim.x * 256) {
-        double th = pb.omega * pb.t[i];
+        double th = pb.omega * gld(pb.t + i);
         th = th + phi;
         c64 dd = d_at(pb, doff + i);
         if (pb.flags & F_RECENTER) {
