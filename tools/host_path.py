@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Host-buffer boundary timing (the Julia drop-in hands over host arrays: gpd_fit_batch).
 
+0. C1, one diode × 1e4 samples (BASELINE configs[0]) against the oracle on one thread.
 1. C2, one GRAVITY exposure (32 diodes + 8 FC columns × 1e5 samples, seed 42): wall time of
    the C-ABI call with the demodulated output (what demodulateall does), against the CPU
    oracle on the same exposure (16 OpenMP threads).
@@ -46,13 +47,26 @@ def main():
     gpd = gpdemod_loader.load()
     res = {}
 
+    # ---- 0. C1: one diode × 1e4 samples (BASELINE configs[0]) ---------------------------------
+    import oracle  # checker / CPU baseline only
+    B1 = synth.make_batch(10_000, 1, seed=1)
+    a1 = (B1["t"], B1["d"], B1["fc"], B1["fc_of_pixel"])
+    s1, p1 = timed(lambda: gpd.fit_batch(*a1), a.reps)
+    t0 = time.perf_counter()
+    r1 = oracle.fit_batch(*a1, flags=oracle.RECENTER, nthreads=1)
+    c1 = time.perf_counter() - t0
+    res["C1"] = {"series": 1, "samples": 10_000, "host_call_ms": 1e3 * s1,
+                 "device_kernels_ms": {k: round(v, 3) for k, v in gpd.timings(0).items()},
+                 "cpu_oracle_ms_1_thread": 1e3 * c1,
+                 "b": float(p1["b"][0]), "b_oracle": float(r1["b"][0]),
+                 "b_truth": float(B1["truth"]["b"][0])}
+
     # ---- 1. C2: one exposure through the host boundary ------------------------------------
     B = synth.make_batch(a.samples, 32, seed=42)
     args = (B["t"], B["d"], B["fc"], B["fc_of_pixel"])
     s_fit, _ = timed(lambda: gpd.fit_batch(*args), a.reps)
     s_out, (par, _) = timed(lambda: gpd.fit_batch(*args, want_output=True), a.reps)
     dev = gpd.timings(0)
-    import oracle  # checker / CPU baseline only
     t0 = time.perf_counter()
     ref = oracle.fit_batch(*args, flags=oracle.RECENTER, nthreads=a.cpu_threads)
     s_cpu = time.perf_counter() - t0
