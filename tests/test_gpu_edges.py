@@ -115,3 +115,18 @@ def test_c_host_example_runs(gpu, tmp_path):
     r = subprocess.run([str(exe), "20000"], capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-1000:]
     assert "ok: 32/32" in r.stdout
+
+
+@pytest.mark.parametrize("N", [5, 20, 33, 95])
+def test_short_series_harmonic_chi2(gpu, N):
+    """Series shorter than one 32-sample tile (and one tile + a few samples): the moment kernel's
+    padded table tile (bf16 fragments in rows 0..15, zero rows past N) and the partial-tile masking
+    give the χ² of the exact evaluator."""
+    B = synth.make_batch(N, 12, seed=N)
+    rng = np.random.default_rng(N)
+    bphi = np.stack([rng.uniform(-3, 3, 12), rng.uniform(-4, 4, 12)], 1)
+    args = (B["t"], B["d"], B["fc"], B["fc_of_pixel"], bphi)
+    h = gpu.chi2_batch(*args, method="harmonic")
+    e = gpu.chi2_batch(*args, method="exact")
+    assert not (h["status"] & 0x18).any()
+    np.testing.assert_allclose(h["chi2"], e["chi2"], rtol=1e-12, atol=0)
