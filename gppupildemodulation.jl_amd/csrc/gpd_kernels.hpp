@@ -767,9 +767,11 @@ __global__ __launch_bounds__(256, 2) void k_moments_mfma(Problem pb, const doubl
     }
 }
 
-// k_moments_ws: the MFMA contraction with producer/consumer wave roles (non-faint series).
+// k_moments_ws: the MFMA contraction with producer/consumer wave roles (every whole-exposure
+// series; faint ones weighted per state).
 //   Workgroup = 8 waves, one workgroup per CU (LDS 157 KB): waves 0-3 (consumers) only run the
-//   MFMA phase of k_moments_mfma (same fragments, same 12 accumulators per wave); waves 4-7
+//   MFMA phase — the f64 fragments of k_moments_mfma for harmonics 1..16 (8 accumulators per
+//   wave) and, with MIX, split-bf16 MFMAs for harmonics 17..24 (4 f32 accumulators); waves 4-7
 //   (producers) stream d / FC / cos-sin rows two tiles ahead in registers, form q = p̄ d and
 //   write the next tile into the other half of a double-buffered LDS tile.  One barrier per
 //   tile: consumers on buffer i&1 while producers fill buffer (i+1)&1, so each SIMD hosts one
