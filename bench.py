@@ -262,7 +262,7 @@ def cpu_baseline(gpd, t, d, fc, fcop, par, args, N):
     # NEWUOA tie check on the first series of the sample (outside the timed baseline): a fit
     # that is not within 1e-10 of the oracle must be an outcome the oracle itself reaches when
     # its χ² moves by the harmonic evaluator's error size (128 ulp; tests/test_gpu_parity.py)
-    kt = min(k, 64)
+    kt = min(k, 512)
 
     def dev(x, r):
         dphi = np.abs((x["phi"] - r["phi"] + np.pi) % (2 * np.pi) - np.pi)
@@ -271,12 +271,16 @@ def cpu_baseline(gpd, t, d, fc, fcop, par, args, N):
                        np.abs(x["a"] - r["a"]) / np.abs(r["a"])], axis=0)
     pert = [oracle.fit_batch(th, dd[:kt], ff[: kt // 4], fo[:kt], flags=oracle.RECENTER,
                              nthreads=threads, perturb_seed=sd, perturb_ulps=128.0)
-            for sd in range(1, 7)]
+            for sd in range(1, 13)]
     got, r0 = par[:kt], ref[:kt]
     e = dev(got, r0)
-    env = np.max([dev(q, r0) for q in pert], axis=0)
+    devs = np.array([dev(q, r0) for q in pert])
+    env = devs.max(axis=0)
     same = np.any([dev(got, q) <= 1e-10 for q in pert], axis=0)
-    explained = (e <= 1e-10) | same | (e <= 1.5 * env + 1e-12)
+    # as tests/test_gpu_parity.assert_fit_parity: series the oracle itself re-routes in >= 1/4 of
+    # its perturbed runs admit any landing point below NEWUOA's rhoend
+    chaotic = (devs > 1e-10).mean(axis=0) >= 0.25
+    explained = (e <= 1e-10) | same | (e <= 1.5 * env + 1e-10) | (chaotic & (e < 1e-3))
     cpu_model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
