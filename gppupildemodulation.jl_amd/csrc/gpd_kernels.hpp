@@ -1719,6 +1719,9 @@ __global__ __launch_bounds__(EXACT_WG) void k_fit_exact(Problem pb, const Info *
                                                         c64 *__restrict__ mcache = nullptr,
                                                         long long mstride = 0) {
     __shared__ double lds[(EXACT_WG / 64) * 8];
+    // NEWUOA state: one copy per wave in LDS (all lanes of a wave run the same iteration and
+    // read/write the same addresses), instead of replicated in every thread's registers
+    __shared__ Newuoa<2, 5, true> nwx[EXACT_WG / 64];
     const long long total = list ? (long long)(*count) : pb.P;
     const double nvalid = (double)info->nvalid;
     for (long long idx = blockIdx.x; idx < total; idx += gridDim.x) {
@@ -1737,7 +1740,7 @@ __global__ __launch_bounds__(EXACT_WG) void k_fit_exact(Problem pb, const Info *
         f.nfev = 0;
         double x[2];
         int status = ST_EXACT | extra_status;
-        drive_fit(f, pb, x, status);
+        drive_fit(f, pb, x, status, nwx[threadIdx.x >> 6]);
         const double chi2 = f(x);
         if (threadIdx.x == 0)
             store_param(out, raw, k, f.c_re, f.c_im, f.a_re, f.a_im, x[0], x[1], chi2, f.nfev, status);
