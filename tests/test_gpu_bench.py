@@ -38,10 +38,14 @@ def test_bench_two_ranks_rehearsal():
     """The multi-rank path of bench.py (torch.distributed.run, barrier, max-over-ranks time,
     gather of the records to rank 0, one JSON line from rank 0) with two ranks sharing cuda:0
     under gloo (GPD_DIST_BACKEND) — the scaling runs use RCCL with one rank per GPU."""
+    import socket
+    with socket.socket() as so:  # a free rendezvous port on this box
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
     env = dict(os.environ, GPD_DIST_BACKEND="gloo")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
-                        "--master-port", "29517", os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2",
                         "--pixels", "256", "--samples", "4096", "--steps", "2", "--warmup", "1",
                         "--no-cpu"], capture_output=True, text=True, timeout=110, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
