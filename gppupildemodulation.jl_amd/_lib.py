@@ -43,7 +43,7 @@ EXPORTS = ("gpd_version", "gpd_strerror", "gpd_device_count", "gpd_fit_batch",
            "gpd_fit_batch_dev", "gpd_chi2_batch", "gpd_chi2_batch_dev", "gpd_buildstates",
            "gpd_synth_fill_dev", "gpd_last_timings", "gpd_fit_windows", "gpd_fit_windows_dev",
            "gpd_process_volt", "gpd_fit_batch_c32", "gpd_fit_batch_c32_dev", "gpd_fit_windows_c32",
-           "gpd_fit_windows_c32_dev", "gpd_buildstates_dev", "gpd_release")
+           "gpd_fit_windows_c32_dev", "gpd_buildstates_dev", "gpd_release", "gpd_libm_eval")
 
 
 class GpdError(RuntimeError):
@@ -106,6 +106,8 @@ def load():
     L.gpd_synth_fill_dev.restype = ctypes.c_int
     L.gpd_synth_fill_dev.argtypes = [I64, I64, I64, ctypes.c_uint64, D, D, D, ctypes.c_int, D, V, V,
                                      I64, V, I64, V, V, ctypes.c_int, V]
+    L.gpd_libm_eval.restype = ctypes.c_int
+    L.gpd_libm_eval.argtypes = [ctypes.c_int, I64, V, V, V, ctypes.c_int]
     L.gpd_last_timings.restype = ctypes.c_int
     L.gpd_last_timings.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                    ctypes.POINTER(ctypes.c_double), ctypes.c_int]
@@ -128,6 +130,21 @@ def check(rc: int, errbuf=None):
         L = load()
         msg = errbuf.value.decode(errors="replace") if errbuf is not None else ""
         raise GpdError(rc, f"{L.gpd_strerror(rc).decode()}: {msg}")
+
+
+LIBM_FN = {"sin": 0, "cos": 1, "sincos": 2, "atan": 3, "atan2": 4, "hypot": 5, "rem_pio2": 6}
+
+
+def libm_eval(fn: str, x, y=None, device: int = 0):
+    """Julia Base's sin/cos/sincos/atan/atan(y,x)/hypot/rem_pio2 as the device evaluates them
+    (gpd_jlmath.h).  sincos → (n, 2) [s, c]; rem_pio2 → (n, 3) [quadrant, hi, lo]."""
+    code = LIBM_FN[fn]
+    x = np.ascontiguousarray(x, dtype=np.float64).ravel()
+    yy = None if y is None else np.ascontiguousarray(y, dtype=np.float64).ravel()
+    width = {2: 2, 6: 3}.get(code, 1)
+    out = np.empty(x.size * width)
+    check(load().gpd_libm_eval(code, x.size, ptr(x), ptr(yy), ptr(out), device))
+    return out.reshape(-1, width) if width > 1 else out
 
 
 def timings(device: int = 0):

@@ -13,6 +13,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "gpd_jlmath.h"  // Julia Base's sin/cos/sincos/atan/hypot, shared with the oracle
+
 namespace gpd {
 
 struct c64 {
@@ -66,11 +68,12 @@ __device__ __forceinline__ c64 cdiv(c64 z, c64 w) {
     return {p * s, q * s};
 }
 
-// exp(Complex(±0, x)) as Julia evaluates it: (cos x, sin x), or (1, x) when x == 0.
+// exp(Complex(±0, x)) as Julia evaluates it: (cos x, sin x) from sincos(x), or (1, x) when
+// x == 0 (base/complex.jl exp; the sincos is Julia Base's, gpd_jlmath.h).
 __device__ __forceinline__ c64 cisj(double x) {
     if (x == 0.0) return {1.0, x};
     double s, c;
-    sincos(x, &s, &c);
+    jl_sincos(x, &s, &c);
     return {c, s};
 }
 

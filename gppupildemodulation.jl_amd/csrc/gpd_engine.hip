@@ -88,14 +88,15 @@ DevCtx *ctx_for(int dev) {
 size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
 struct Layout {
-    size_t info, tab, part, mom, aux, fstat, raw, list, phbuf, partG, momG, auxG, fcid, d0, mcache, total;
+    size_t info, tab, part, mom, aux, fstat, raw, list, phbuf, partG, momG, auxG, fcid, d0, mcache,
+        xtot, xcnt, total;
     long long mstride;  // model-cache elements per exact-path workgroup (0: no cache)
     int nch;
     long long chunk;
 };
 
 Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic, bool phbuf,
-            bool mfma, int n_cu, bool harm_offs, bool windowed = false) {
+            bool mfma, int n_cu, bool harm_offs, bool windowed = false, int exact_g = 1) {
     Layout L{};
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -152,10 +153,16 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     L.fcid = take(harm_offs ? (size_t)n_fc * sizeof(int32_t) : 0);
     L.d0 = take(harm_offs ? (size_t)2 * P * sizeof(double) : 0);
     // exact evaluator: one model-cache slot of N complex per workgroup of the fit grid
-    // (min(P, 1024) workgroups), when that stays below 8 GB
-    const size_t mc_bytes = (size_t)std::min<long long>(P, 1024) * (size_t)N * sizeof(c64);
+    // (min(P, 1024) workgroups), or per series with the multi-workgroup split, when that stays
+    // below 8 GB
+    const long long mc_slots = exact_g > 1 ? P : std::min<long long>(P, 1024);
+    const size_t mc_bytes = (size_t)mc_slots * (size_t)N * sizeof(c64);
     L.mstride = (!harmonic && mc_bytes <= (size_t(8) << 30)) ? N : 0;
     L.mcache = take(L.mstride ? mc_bytes : 0);
+    // multi-workgroup exact fit: per-series block totals (2 slots × 8 blocks × 8 values) and
+    // arrival counters (zeroed per launch)
+    L.xtot = take(exact_g > 1 ? (size_t)P * 2 * CR_BLOCKS * CR_NV * sizeof(double) : 0);
+    L.xcnt = take(exact_g > 1 ? (size_t)(P + 3) / 4 * 16 : 0);
     L.total = off;
     return L;
 }
@@ -283,8 +290,22 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     DevCtx *cx = ctx_for(device);
     std::lock_guard<std::mutex> lk(cx->mu);
     if (cx->n_cu == 0) HIP_TRY(hipDeviceGetAttribute(&cx->n_cu, hipDeviceAttributeMultiprocessorCount, device));
-    const Layout L =
-        plan(N, P, n_fc, faint, harmonic, phbuf, use_mfma, cx->n_cu, harm_offs, window > 0);
+    // Small whole-exposure exact fits (one exposure: 32 series) spread each series over G
+    // workgroups, one per CU (all resident: the per-series barrier needs its G parts on chip);
+    // the canonical reduction order makes the records identical for every G.  GPD_EXACT_G
+    // forces G (tests of that identity).
+    int exact_g = 1;
+    if (want_exact && !bphi && window == 0) {
+        const long long p8 = (P + 7) / 8 * 8;
+        for (int gg = 8; gg >= 2 && exact_g == 1; gg >>= 1)
+            if (p8 * gg <= cx->n_cu) exact_g = gg;
+        if (const char *e = getenv("GPD_EXACT_G")) {
+            const int f = atoi(e);
+            if ((f == 1 || f == 2 || f == 4 || f == 8) && p8 * f <= (long long)cx->n_cu) exact_g = f;
+        }
+    }
+    const Layout L = plan(N, P, n_fc, faint, harmonic, phbuf, use_mfma, cx->n_cu, harm_offs,
+                          window > 0, exact_g);
     if (cx->ws_cap < L.total) {
         if (cx->ws) {
             HIP_TRY(hipDeviceSynchronize());
@@ -535,15 +556,20 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             k_phasor<<<g, 256, 0, stream>>>(pb, ph);
             mark("phasor");
         }
+        if (exact_g > 1)
+            HIP_TRY(hipMemsetAsync(ws + L.xcnt, 0, (size_t)(P + 3) / 4 * 16, stream));
+        const unsigned fit_grid =
+            exact_g > 1 ? (unsigned)((P + 7) / 8 * 8 * exact_g) : exact_grid;
 #define GPD_LAUNCH_EXACT(FA, OF, PH)                                                                 \
     do {                                                                                        \
         if (bphi)                                                                               \
             k_chi2_exact<FA, OF, PH><<<(unsigned)P, EXACT_WG, 0, stream>>>(pb, info, ph, fstat, \
                                                                            bphi, outp);         \
         else                                                                                    \
-            k_fit_exact<FA, OF, PH><<<exact_grid, EXACT_WG, 0, stream>>>(                     \
+            k_fit_exact<FA, OF, PH><<<fit_grid, EXACT_WG, 0, stream>>>(                       \
                 pb, info, ph, fstat, nullptr, nullptr, outp, raw, 0,                            \
-                L.mstride ? (c64 *)(ws + L.mcache) : nullptr, L.mstride);                      \
+                L.mstride ? (c64 *)(ws + L.mcache) : nullptr, L.mstride, exact_g,               \
+                (double *)(ws + L.xtot), (unsigned *)(ws + L.xcnt));                            \
     } while (0)
         if (faint) {
             if (offs) { if (phbuf) GPD_LAUNCH_EXACT(true, true, true); else GPD_LAUNCH_EXACT(true, true, false); }
@@ -981,6 +1007,42 @@ int gpd_process_volt(int64_t n_samples, const double *t, const float *volt, int6
          chk(hipStreamSynchronize(s), "synchronize");
     cleanup();
     return ok ? GPD_OK : GPD_E_HIP;
+}
+
+int gpd_libm_eval(int fn, int64_t n, const double *x, const double *y, double *out, int device) {
+    char *errbuf = nullptr;
+    size_t errlen = 0;
+    if (fn < 0 || fn > 6 || n < 0 || (n > 0 && (!x || !out)) || ((fn == 4 || fn == 5) && n > 0 && !y))
+        return GPD_E_ARG;
+    const int ndev = gpd_device_count();
+    if (ndev <= 0) return GPD_E_NODEV;
+    if (device < 0 || device >= ndev) return GPD_E_ARG;
+    if (n == 0) return GPD_OK;
+    HIP_TRY(hipSetDevice(device));
+    const int width = fn == 2 ? 2 : fn == 6 ? 3 : 1;
+    double *dx = nullptr, *dy = nullptr, *dout = nullptr;
+    auto release = [&]() {
+        (void)hipFree(dx);
+        (void)hipFree(dy);
+        (void)hipFree(dout);
+    };
+    if (hipMalloc(&dx, n * sizeof(double)) != hipSuccess ||
+        hipMalloc(&dy, n * sizeof(double)) != hipSuccess ||
+        hipMalloc(&dout, n * width * sizeof(double)) != hipSuccess) {
+        release();
+        (void)hipGetLastError();
+        return GPD_E_OOM;
+    }
+    hipError_t e = hipMemcpy(dx, x, n * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(dy, y ? y : x, n * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        k_libm<<<(unsigned)((n + 255) / 256), 256>>>(fn, n, dx, dy, dout);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(out, dout, n * width * sizeof(double), hipMemcpyDeviceToHost);
+    release();
+    return e == hipSuccess ? GPD_OK : GPD_E_HIP;
 }
 
 int gpd_synth_fill_dev(int64_t n_samples, int64_t n_pixels, int64_t pixel_offset, uint64_t seed,

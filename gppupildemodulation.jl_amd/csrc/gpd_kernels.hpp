@@ -135,7 +135,7 @@ __device__ __forceinline__ bool sample_valid(const Problem &pb, long long i, int
 }
 
 // FC phasor exp(im·angle(fc)) (src/Modulation.jl:388), Julia arithmetic.
-__device__ __forceinline__ c64 fc_phasor(c64 z) { return cisj(atan2(z.im, z.re)); }
+__device__ __forceinline__ c64 fc_phasor(c64 z) { return cisj(jl_atan2(z.im, z.re)); }
 
 // ---------------------------------------------------------------------------------------
 // Driver shared by both evaluators (src/Modulation.jl:402-416).  F: double operator()(double(&)[2])
@@ -274,7 +274,7 @@ __global__ __launch_bounds__(256) void k_table(const double *__restrict__ t, lon
     if (i >= N) return;
     const double x = omega * t[i];
     double s1, c1;
-    sincos(x, &s1, &c1);
+    jl_sincos(x, &s1, &c1);
     double cn = c1, sn = s1;
     double *row = tab + i * (2 * KH);
 #pragma unroll
@@ -311,7 +311,7 @@ __global__ __launch_bounds__(256) void k_table_mix(const double *__restrict__ t,
     if (i < N) {
         const double x = omega * t[i];
         double s1, c1;
-        sincos(x, &s1, &c1);
+        jl_sincos(x, &s1, &c1);
         double cn = c1, sn = s1;
 #pragma unroll
         for (int n = 1; n <= KH; ++n) {  // the recurrence of k_table, bit for bit
@@ -345,72 +345,82 @@ __global__ __launch_bounds__(256) void k_table_mix(const double *__restrict__ t,
 }
 
 // ---------------------------------------------------------------------------------------
-// k_faint_stats: per series and MetState, m = mean(|d|), w = 1/var(|d|) (src/Faint.jl:89-100)
-// over the valid samples, plus Σ|d|² per state.  One workgroup per series.
-// out[k*16 + ...]: m[5] | w[5] | W2 | DEN | Q2 (state index = code + 1).
+// k_faint_stats: per series and MetState, m = mean(|d|), w = 1/var(|d|; mean=m) (two passes,
+// src/Faint.jl:89-100) over the valid samples, plus Σ|d|² per state.  One workgroup per series;
+// sums in the canonical order CR8 (8 block sweeps of 256 strided slots, the oracle's gsum), so m
+// and w are the oracle's bits.  out[k*16 + ...]: m[5] | w[5] | W2 | DEN | Q2 (state = code + 1).
 __global__ __launch_bounds__(256) void k_faint_stats(Problem pb, double *__restrict__ out) {
     __shared__ double lds[4 * 15];
     const long long k = blockIdx.x;
     const Span sp = span_of(pb, k);  // per window: compute_mean_var_power on state[I] (:205)
     const long long doff = sp.col * pb.ldd;
-    double v[15];
-#pragma unroll
-    for (int q = 0; q < 15; ++q) v[q] = 0.0;
-    // each thread's samples i, i+256, … are summed in that order (the oracle's partials); the
-    // loads of U consecutive ones are issued together (U in flight instead of one)
+    // the loads of U consecutive samples of a slot (2048 apart) are issued together
     constexpr int U = 4;
     auto fetch = [&](long long i0, c64 (&z)[U], int (&st)[U], bool (&ok)[U]) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const long long i = i0 + 256 * u;
+            const long long i = i0 + 2048LL * u;
             ok[u] = i < sp.s1;
             const long long ic = ok[u] ? i : sp.s0;
             z[u] = d_at(pb, doff + ic);
             ok[u] = ok[u] && sample_valid(pb, ic, st[u]);
         }
     };
-    for (long long i0 = sp.s0 + threadIdx.x; i0 < sp.s1; i0 += 256 * U) {
-        c64 z[U];
-        int st[U];
-        bool ok[U];
-        fetch(i0, z, st, ok);
+    double v[15];
+    for (int blk = 0; blk < 8; ++blk) {
+        double a[15];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (!ok[u]) continue;
-            const double ad = hypot(z[u].re, z[u].im);
-            const double d2 = z[u].re * z[u].re + z[u].im * z[u].im;
+        for (int q = 0; q < 15; ++q) a[q] = 0.0;
+        for (long long i0 = sp.s0 + 256 * blk + threadIdx.x; i0 < sp.s1; i0 += 2048LL * U) {
+            c64 z[U];
+            int st[U];
+            bool ok[U];
+            fetch(i0, z, st, ok);
 #pragma unroll
-            for (int q = 0; q < 5; ++q)
-                if (st[u] + 1 == q) {
-                    v[q] += 1.0;
-                    v[5 + q] += ad;
-                    v[10 + q] += d2;
-                }
+            for (int u = 0; u < U; ++u) {
+                if (!ok[u]) continue;
+                const double ad = jl_hypot(z[u].re, z[u].im);
+                const double d2 = z[u].re * z[u].re + z[u].im * z[u].im;
+#pragma unroll
+                for (int q = 0; q < 5; ++q)
+                    if (st[u] + 1 == q) {
+                        a[q] += 1.0;
+                        a[5 + q] += ad;
+                        a[10 + q] += d2;
+                    }
+            }
         }
+        block_sum<256, 15>(a, lds);
+#pragma unroll
+        for (int q = 0; q < 15; ++q) v[q] = blk == 0 ? a[q] : v[q] + a[q];
     }
-    block_sum<256, 15>(v, lds);
     double m[5];
 #pragma unroll
     for (int q = 0; q < 5; ++q) m[q] = v[5 + q] / v[q];
-    double s[5] = {0, 0, 0, 0, 0};
-    for (long long i0 = sp.s0 + threadIdx.x; i0 < sp.s1; i0 += 256 * U) {
-        c64 z[U];
-        int st[U];
-        bool ok[U];
-        fetch(i0, z, st, ok);
+    double s[5];
+    for (int blk = 0; blk < 8; ++blk) {
+        double a[5] = {0, 0, 0, 0, 0};
+        for (long long i0 = sp.s0 + 256 * blk + threadIdx.x; i0 < sp.s1; i0 += 2048LL * U) {
+            c64 z[U];
+            int st[U];
+            bool ok[U];
+            fetch(i0, z, st, ok);
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (!ok[u]) continue;
-            const double ad = hypot(z[u].re, z[u].im);
+            for (int u = 0; u < U; ++u) {
+                if (!ok[u]) continue;
+                const double ad = jl_hypot(z[u].re, z[u].im);
 #pragma unroll
-            for (int q = 0; q < 5; ++q)
-                if (st[u] + 1 == q) {
-                    const double dv = ad - m[q];
-                    s[q] += dv * dv;
-                }
+                for (int q = 0; q < 5; ++q)
+                    if (st[u] + 1 == q) {
+                        const double dv = ad - m[q];
+                        a[q] += dv * dv;
+                    }
+            }
         }
+        block_sum<256, 5>(a, lds);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) s[q] = blk == 0 ? a[q] : s[q] + a[q];
     }
-    block_sum<256, 5>(s, lds);
     if (threadIdx.x == 0) {
         double *o = out + k * 16;
         double W2 = 0.0, DEN = 0.0, Q2 = 0.0;
@@ -1380,7 +1390,7 @@ struct HarmChi2 {
         }
         if (qbase != 0.0) phi = (qbase + phi) - qbase;  // θ = fl(x + ϕ) = x + ϕ_q (one binade)
         double sph, cph;
-        sincos(phi, &sph, &cph);
+        jl_sincos(phi, &sph, &cph);
         double Sr, Si;  // S = Σ w m̄ d
         combine(mom, P, k, J, cph, sph, Sr, Si);
         if (offs) {
@@ -1482,8 +1492,37 @@ __global__ __launch_bounds__(64) void k_fit_harmonic(Problem pb, const Info *__r
 }
 
 // ---------------------------------------------------------------------------------------
-// EXACT PATH — one workgroup per series, NEWUOA replicated on every thread (uniform control
-// flow), χ² as a cooperative pass with the reference arithmetic.
+// EXACT PATH — a series is fitted by G ∈ {1, 2, 4, 8} workgroups of EXACT_WG threads; NEWUOA
+// runs replicated on every thread of every one of them (uniform control flow: every thread
+// obtains bit-identical χ² totals), χ² is a cooperative pass with the reference arithmetic.
+//
+// Canonical reduction order CR8 (the oracle's gsum, oracle/demod_oracle.c): sample i of the
+// series (counted from its first sample) adds into slot i mod 2048; slot s = 256·blk + t is
+// thread t's accumulator during block blk's sweep (samples s0 + 256·blk + t + 2048·m in order);
+// a block total is block_sum's fixed tree (xor butterfly per wave, 4 wave totals left to right);
+// the 8 block totals are added left to right.  One workgroup (G = 1) sweeps the 8 blocks in
+// turn; with G > 1 workgroup g sweeps blocks [g·8/G, (g+1)·8/G), publishes its block totals and
+// every workgroup of the series adds all 8 after a per-series barrier — the same bits for every
+// G, so small batches (one exposure: 32 series) can spread over the chip.
+constexpr int CR_BLOCKS = 8;
+constexpr int CR_SLOTS = CR_BLOCKS * EXACT_WG;  // 2048
+constexpr int CR_NV = 8;                        // values per block total (offsets: 8)
+constexpr int CR_FLAG = (EXACT_WG / 64) * 8;    // LDS word after block_sum's partials
+constexpr int EXACT_LDS = CR_FLAG + 1;          // doubles of LDS per exact-path workgroup
+
+// Per-series exchange of block totals between the G workgroups of a multi-workgroup fit:
+// tot[2 slots][CR_BLOCKS][CR_NV] doubles per series, one arrival counter per series (zeroed
+// before the launch).  Barrier k (k = 1, 2, …) uses slot k & 1 and completes when the counter
+// reaches k·G.  Payload stores are write-through (sc1) and drained before the arrival add,
+// consumers poll the counter relaxed, take one agent acquire, and read the payload with sc1
+// loads (cdna_hip_programming.md Guideline 16, R1; MI355X_MICROARCH.md § visibility).
+struct Xchg {
+    double *tot;
+    unsigned *cnt;
+};
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+
 template <bool FAINT, bool OFFS, bool PHBUF>
 struct ExactChi2 {
     const Problem *pb;
@@ -1497,8 +1536,13 @@ struct ExactChi2 {
     int nfev;
     // model cache (nullptr: none): the final pass of each evaluation reads the model the first
     // pass computed (same values, so the same sums) instead of re-evaluating sin/sincos and the
-    // FC phasor; one slot of s1 − s0 elements per workgroup
+    // FC phasor; element i − s0 of the series' slot
     c64 *mc;
+    // multi-workgroup split: G workgroups per series, this one is g; x: the series' exchange
+    int G, g;
+    Xchg x;
+    unsigned nbar;  // barriers passed
+    bool sync_fail; // a barrier spin gave up (never observed; the series reports NaN)
 
     // Global-address-space views of the problem's arrays, taken once per evaluation: this
     // functor runs out of line, where plain pointers are generic and every flat load's wait
@@ -1578,39 +1622,108 @@ struct ExactChi2 {
                                          double phi) const {
         double th = v.omega * v.t[i];
         th = th + phi;
-        const double beta = b * sin(th);
+        const double beta = b * jl_sin(th);
         return cmul(p, cisj(beta));  // power * exp(ȷ b sin(ωt+ϕ)) (src/Modulation.jl:137)
     }
 
-    __device__ double operator()(const double (&x)[2]) {
-        ++nfev;
-        const double b = x[0], phi = x[1];
-        const View V = view();
+    // Per-series barrier of the G workgroups (G > 1); the caller has issued its payload stores.
+    __device__ __forceinline__ void xbarrier() {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+        __syncthreads();
+        ++nbar;
+        if (threadIdx.x == 0) {
+            __hip_atomic_fetch_add((gu32 *)x.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned target = nbar * (unsigned)G;
+            unsigned spins = 0;
+            while (__hip_atomic_load((gu32 *)x.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                   target) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > (1u << 24)) {  // ~1 s: a sibling is not resident (never expected)
+                    sync_fail = true;
+                    break;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            ((ldouble *)lds)[CR_FLAG] = sync_fail ? 1.0 : 0.0;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        sync_fail = ((ldouble *)lds)[CR_FLAG] != 0.0;  // every thread takes the same branches
+    }
+
+    // Σ over the series' samples of accum(i, acc) in the canonical order CR8; every thread of
+    // every workgroup of the series returns the same NV totals.
+    template <int NV, class A>
+    __device__ __forceinline__ void cr_sum(A &&accum, double (&tot)[NV]) {
         ldouble *lp = (ldouble *)lds;
+        const int nb = CR_BLOCKS / G, b0 = g * nb;
+        for (int blk = b0; blk < b0 + nb; ++blk) {
+            double acc[NV];
+#pragma unroll
+            for (int k = 0; k < NV; ++k) acc[k] = 0.0;
+            for (long long i = s0 + blk * EXACT_WG + threadIdx.x; i < s1; i += CR_SLOTS) accum(i, acc);
+            block_sum<EXACT_WG, NV>(acc, lp);
+            if (G == 1) {
+#pragma unroll
+                for (int k = 0; k < NV; ++k) tot[k] = (blk == 0) ? acc[k] : tot[k] + acc[k];
+            } else if (threadIdx.x < NV) {
+                double v = acc[0];
+#pragma unroll
+                for (int k = 1; k < NV; ++k) v = ((int)threadIdx.x == k) ? acc[k] : v;
+                gu64 *slot = (gu64 *)(x.tot + ((nbar + 1) & 1) * (CR_BLOCKS * CR_NV) +
+                                      blk * CR_NV + threadIdx.x);
+                __hip_atomic_store(slot, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if (G == 1) return;
+        xbarrier();
+        const double *base = x.tot + (nbar & 1) * (CR_BLOCKS * CR_NV);
+#pragma unroll
+        for (int blk = 0; blk < CR_BLOCKS; ++blk) {
+#pragma unroll
+            for (int k = 0; k < NV; ++k) {
+                const double v = __builtin_bit_cast(
+                    double, __hip_atomic_load((gu64 *)(base + blk * CR_NV + k), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT));
+                tot[k] = (blk == 0) ? v : tot[k] + v;
+            }
+        }
+        if (sync_fail) {
+#pragma unroll
+            for (int k = 0; k < NV; ++k) tot[k] = __builtin_nan("");
+        }
+    }
+
+    __device__ double operator()(const double (&xx)[2]) {
+        ++nfev;
+        const double b = xx[0], phi = xx[1];
+        const View V = view();
         gmc64 *mcg = (gmc64 *)mc;
         if (OFFS) {
-            double v[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // a11, a12(2), a22, b1(2), b2(2)
-            for (long long i = s0 + threadIdx.x; i < s1; i += EXACT_WG) {
-                c64 p;
-                double w;
-                if (!load(V, i, p, w)) continue;
-                const c64 m = model(V, i, p, b, phi);
-                if (mcg) {
-                    mcg[i - s0].re = m.re;
-                    mcg[i - s0].im = m.im;
-                }
-                const c64 dd = d_of(V, doff + i);
-                v[0] += w;
-                v[1] += w * m.re;
-                v[2] += w * m.im;
-                v[3] += w * (m.re * m.re + m.im * m.im);
-                v[4] += w * dd.re;
-                v[5] += w * dd.im;
-                const c64 pr = cmul(c64{w * m.re, w * (-m.im)}, dd);
-                v[6] += pr.re;
-                v[7] += pr.im;
-            }
-            block_sum<EXACT_WG, 8>(v, lp);
+            double v[8];  // a11, a12(2), a22, b1(2), b2(2)
+            cr_sum<8>(
+                [&](long long i, double (&a)[8]) {
+                    c64 p;
+                    double w;
+                    if (!load(V, i, p, w)) return;
+                    const c64 m = model(V, i, p, b, phi);
+                    if (mcg) {
+                        mcg[i - s0].re = m.re;
+                        mcg[i - s0].im = m.im;
+                    }
+                    const c64 dd = d_of(V, doff + i);
+                    a[0] += w;
+                    a[1] += w * m.re;
+                    a[2] += w * m.im;
+                    a[3] += w * (m.re * m.re + m.im * m.im);
+                    a[4] += w * dd.re;
+                    a[5] += w * dd.im;
+                    const c64 pr = cmul(c64{w * m.re, w * (-m.im)}, dd);
+                    a[6] += pr.re;
+                    a[7] += pr.im;
+                },
+                v);
             // StaticArrays 2×2 Cramer solve (src/Modulation.jl:189-192)
             const c64 A11 = {v[0], 0.0}, A12 = {v[1], v[2]}, A21 = {v[1], -v[2]}, A22 = {v[3], 0.0};
             const c64 b1 = {v[4], v[5]}, b2 = {v[6], v[7]};
@@ -1625,56 +1738,58 @@ struct ExactChi2 {
             a_re = aa.re;
             a_im = aa.im;
         } else {
-            double v[4] = {0, 0, 0, 0};  // num(2), den(2)
-            for (long long i = s0 + threadIdx.x; i < s1; i += EXACT_WG) {
-                c64 p;
-                double w;
-                if (!load(V, i, p, w)) continue;
-                const c64 m = model(V, i, p, b, phi);
-                if (mcg) {
-                    mcg[i - s0].re = m.re;
-                    mcg[i - s0].im = m.im;
-                }
-                const c64 mwc = {m.re * w, -(m.im * w)};  // conj(model .* weight)
-                const c64 xx = cmul(mwc, d_of(V, doff + i));
-                const c64 yy = cmul(mwc, m);
-                v[0] += xx.re;
-                v[1] += xx.im;
-                v[2] += yy.re;
-                v[3] += yy.im;
-            }
-            block_sum<EXACT_WG, 4>(v, lp);
+            double v[4];  // num(2), den(2)
+            cr_sum<4>(
+                [&](long long i, double (&a)[4]) {
+                    c64 p;
+                    double w;
+                    if (!load(V, i, p, w)) return;
+                    const c64 m = model(V, i, p, b, phi);
+                    if (mcg) {
+                        mcg[i - s0].re = m.re;
+                        mcg[i - s0].im = m.im;
+                    }
+                    const c64 mwc = {m.re * w, -(m.im * w)};  // conj(model .* weight)
+                    const c64 xv = cmul(mwc, d_of(V, doff + i));
+                    const c64 yv = cmul(mwc, m);
+                    a[0] += xv.re;
+                    a[1] += xv.im;
+                    a[2] += yv.re;
+                    a[3] += yv.im;
+                },
+                v);
             const c64 aa = cdiv(c64{v[0], v[1]}, c64{v[2], v[3]});  // (src/Modulation.jl:144)
             c_re = c_im = 0.0;
             a_re = aa.re;
             a_im = aa.im;
         }
         // weighted_norm2(model .- data, weight) / N  (src/Modulation.jl:299-305, 325)
-        double s[1] = {0.0};
+        double s[1];
         const c64 aa = {a_re, a_im};
-        for (long long i = s0 + threadIdx.x; i < s1; i += EXACT_WG) {
-            c64 m;
-            double w;
-            if (mcg) {  // the same thread wrote element i in the first pass
-                int st;
-                if (!valid(V, i, st)) continue;
-                w = weight_of(st);
-                m = c64{mcg[i - s0].re, mcg[i - s0].im};
-            } else {
-                c64 p;
-                if (!load(V, i, p, w)) continue;
-                m = model(V, i, p, b, phi);
-            }
-            c64 mm = cmul(aa, m);
-            if (OFFS) {
-                mm.re = c_re + mm.re;
-                mm.im = c_im + mm.im;
-            }
-            const c64 dd = d_of(V, doff + i);
-            const double rr = mm.re - dd.re, ri = mm.im - dd.im;
-            s[0] += w * (rr * rr + ri * ri);
-        }
-        block_sum<EXACT_WG, 1>(s, lp);
+        cr_sum<1>(
+            [&](long long i, double (&a)[1]) {
+                c64 m;
+                double w;
+                if (mcg) {  // the same thread wrote element i in the first pass
+                    int st;
+                    if (!valid(V, i, st)) return;
+                    w = weight_of(st);
+                    m = c64{mcg[i - s0].re, mcg[i - s0].im};
+                } else {
+                    c64 p;
+                    if (!load(V, i, p, w)) return;
+                    m = model(V, i, p, b, phi);
+                }
+                c64 mm = cmul(aa, m);
+                if (OFFS) {
+                    mm.re = c_re + mm.re;
+                    mm.im = c_im + mm.im;
+                }
+                const c64 dd = d_of(V, doff + i);
+                const double rr = mm.re - dd.re, ri = mm.im - dd.im;
+                a[0] += w * (rr * rr + ri * ri);
+            },
+            s);
         return s[0] / nvalid;
     }
 };
@@ -1684,29 +1799,40 @@ struct ExactChi2 {
 template <class F>
 __device__ __forceinline__ void setup_exact(F &f, const Problem &pb, long long k,
                                             const c64 *__restrict__ phbuf, double *lds,
-                                            double nvalid_all) {
+                                            double nvalid_all, int G = 1, int g = 0,
+                                            Xchg x = Xchg{nullptr, nullptr}) {
     const Span sp = span_of(pb, k);
     f.pb = &pb;
     f.doff = sp.col * pb.ldd;
-    const long long g = pb.fcop[sp.col];
-    f.foff = g * pb.ldfc;
-    f.src = phbuf ? phbuf + g * pb.N : nullptr;
+    const long long fcol = pb.fcop[sp.col];
+    f.foff = fcol * pb.ldfc;
+    f.src = phbuf ? phbuf + fcol * pb.N : nullptr;
     f.lds = lds;
     f.mc = nullptr;
     f.s0 = sp.s0;
     f.s1 = sp.s1;
+    f.G = G;
+    f.g = g;
+    f.x = x;
+    f.nbar = 0;
+    f.sync_fail = false;
     if (pb.win > 0) {
-        double c[1] = {0.0};
-        for (long long i = sp.s0 + threadIdx.x; i < sp.s1; i += EXACT_WG) {
+        double c[1];
+        f.cr_sum([&](long long i, double (&a)[1]) {
             int st;
-            if (sample_valid(pb, i, st)) c[0] += 1.0;
-        }
-        block_sum<EXACT_WG, 1>(c, lds);
+            if (sample_valid(pb, i, st)) a[0] += 1.0;
+        }, c);
         f.nvalid = c[0];
     } else {
         f.nvalid = nvalid_all;
     }
 }
+
+// Multi-workgroup layout: workgroup b serves series xser(b) as part xpart(b) of G.  Blocks b and
+// b + 8 share an XCD (round-robin dispatch), so the G parts of one series are dealt to one XCD
+// (their exchange stays in its L2) — placement is a speed hint only, never correctness.
+__device__ __forceinline__ long long xser(long long b, int G) { return ((b >> 3) / G) * 8 + (b & 7); }
+__device__ __forceinline__ int xpart(long long b, int G) { return (int)((b >> 3) % G); }
 
 template <bool FAINT, bool OFFS, bool PHBUF>
 __global__ __launch_bounds__(EXACT_WG) void k_fit_exact(Problem pb, const Info *__restrict__ info,
@@ -1717,13 +1843,40 @@ __global__ __launch_bounds__(EXACT_WG) void k_fit_exact(Problem pb, const Info *
                                                         Param *__restrict__ out,
                                                         double *__restrict__ raw, int extra_status,
                                                         c64 *__restrict__ mcache = nullptr,
-                                                        long long mstride = 0) {
-    __shared__ double lds[(EXACT_WG / 64) * 8];
+                                                        long long mstride = 0, int G = 1,
+                                                        double *__restrict__ xtot = nullptr,
+                                                        unsigned *__restrict__ xcnt = nullptr) {
+    __shared__ double lds[EXACT_LDS];
     // NEWUOA state: one copy per wave in LDS (all lanes of a wave run the same iteration and
     // read/write the same addresses), instead of replicated in every thread's registers
     __shared__ Newuoa<2, 5, true> nwx[EXACT_WG / 64];
-    const long long total = list ? (long long)(*count) : pb.P;
     const double nvalid = (double)info->nvalid;
+    if (G > 1) {  // one series per G workgroups (whole exposures, no list)
+        const long long k = xser(blockIdx.x, G);
+        if (k >= pb.P) return;  // uniform per series: all its parts leave together
+        const int g = xpart(blockIdx.x, G);
+        ExactChi2<FAINT, OFFS, PHBUF> f;
+        setup_exact(f, pb, k, PHBUF ? phbuf : nullptr, lds, nvalid, G, g,
+                    Xchg{xtot + k * (2 * CR_BLOCKS * CR_NV), xcnt + k});
+        if (mcache) f.mc = mcache + k * mstride;
+        if (FAINT) {
+#pragma unroll
+            for (int q = 0; q < 5; ++q) {
+                f.m5[q] = fstat[k * 16 + q];
+                f.w5[q] = fstat[k * 16 + 5 + q];
+            }
+        }
+        f.a_re = f.a_im = f.c_re = f.c_im = 0.0;
+        f.nfev = 0;
+        double x[2];
+        int status = ST_EXACT | extra_status;
+        drive_fit(f, pb, x, status, nwx[threadIdx.x >> 6]);
+        const double chi2 = f(x);
+        if (g == 0 && threadIdx.x == 0)
+            store_param(out, raw, k, f.c_re, f.c_im, f.a_re, f.a_im, x[0], x[1], chi2, f.nfev, status);
+        return;
+    }
+    const long long total = list ? (long long)(*count) : pb.P;
     for (long long idx = blockIdx.x; idx < total; idx += gridDim.x) {
         const long long k = list ? (long long)list[idx] : idx;
         ExactChi2<FAINT, OFFS, PHBUF> f;
@@ -1760,7 +1913,7 @@ __global__ __launch_bounds__(EXACT_WG) void k_refine_exact(Problem pb, const Inf
                                                            const c64 *__restrict__ phbuf,
                                                            const double *__restrict__ raw,
                                                            Param *__restrict__ out) {
-    __shared__ double lds[(EXACT_WG / 64) * 8];
+    __shared__ double lds[EXACT_LDS];
     for (long long k = blockIdx.x; k < pb.P; k += gridDim.x) {
         if (out[k].status & ST_EXACT) continue;  // uniform per workgroup
         ExactChi2<false, true, PHBUF> f;
@@ -1786,7 +1939,7 @@ __global__ __launch_bounds__(EXACT_WG) void k_chi2_exact(Problem pb, const Info 
                                                          const double *__restrict__ fstat,
                                                          const double *__restrict__ bphi,
                                                          Param *__restrict__ out) {
-    __shared__ double lds[(EXACT_WG / 64) * 8];
+    __shared__ double lds[EXACT_LDS];
     const long long k = blockIdx.x;
     ExactChi2<FAINT, OFFS, PHBUF> f;
     setup_exact(f, pb, k, PHBUF ? phbuf : nullptr, lds, (double)info->nvalid);
@@ -1889,7 +2042,7 @@ __global__ __launch_bounds__(256) void k_output(Problem pb, const Param *__restr
     const Span sp = span_of(pb, k);
     const Param pk = par[k];
     const double b = raw[2 * k], phi = raw[2 * k + 1];
-    const double arga = atan2(pk.a_im, pk.a_re);
+    const double arga = jl_atan2(pk.a_im, pk.a_re);
     const c64 aa = {pk.a_re, pk.a_im};
     const bool offs = (pb.flags & F_OFFSETS) != 0;
     const long long doff = sp.col * pb.ldd;
@@ -1900,7 +2053,7 @@ __global__ __launch_bounds__(256) void k_output(Problem pb, const Param *__restr
         th = th + phi;
         c64 dd = d_at(pb, doff + i);
         if (pb.flags & F_RECENTER) {
-            double ph = b * sin(th);  // getphase (src/Modulation.jl:66-69)
+            double ph = b * jl_sin(th);  // getphase (src/Modulation.jl:66-69)
             ph = ph + arga;
             const double psi = ph - arga;
             if (offs) {
@@ -1909,13 +2062,42 @@ __global__ __launch_bounds__(256) void k_output(Problem pb, const Param *__restr
             }
             o[i] = cmul(dd, cisj(-psi));
         } else {
-            c64 mv = cmul(aa, cisj(b * sin(th)));
+            c64 mv = cmul(aa, cisj(b * jl_sin(th)));
             if (offs) {
                 mv.re = pk.c_re + mv.re;
                 mv.im = pk.c_im + mv.im;
             }
-            o[i] = cmul(dd, cisj(-atan2(mv.im, mv.re)));
+            o[i] = cmul(dd, cisj(-jl_atan2(mv.im, mv.re)));
         }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// gpd_libm_eval: the shared Julia-libm restatement evaluated on the device (bitwise tests).
+__global__ __launch_bounds__(256) void k_libm(int fn, long long n, const double *__restrict__ x,
+                                              const double *__restrict__ y, double *__restrict__ out) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    switch (fn) {
+    case 0: out[i] = jl_sin(x[i]); break;
+    case 1: out[i] = jl_cos(x[i]); break;
+    case 2: {
+        double s, c;
+        jl_sincos(x[i], &s, &c);
+        out[2 * i] = s;
+        out[2 * i + 1] = c;
+        break;
+    }
+    case 3: out[i] = jl_atan(x[i]); break;
+    case 4: out[i] = jl_atan2(x[i], y[i]); break;
+    case 5: out[i] = jl_hypot(x[i], y[i]); break;
+    default: {
+        double hi, lo;
+        const int q = jl_rem_pio2(x[i], &hi, &lo);
+        out[3 * i] = (double)q;
+        out[3 * i + 1] = hi;
+        out[3 * i + 2] = lo;
+    }
     }
 }
 

@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include "gpd_jlmath.h"  // OptimPackNextGen is pure Julia: Julia Base cos/sin
+
 namespace gpd {
 
 #define GPD_HD __host__ __device__ __forceinline__
@@ -67,18 +69,18 @@ GPD_HD void wrc(double (&a)[R][C], int r, int c, double v) {
 
 constexpr double kTwoPi = 6.283185307179586476925286766559;  // 8·atan(1)
 // cos/sin of the fixed trial angles i·dang, dang = kTwoPi/50, of the three angle searches
-// (TRSAPP, BIGLAG, BIGDEN: 49 angles each), exactly as the oracle's libm computes them
-// (oracle/tools/angle_table.py).  Read by uniform index (scalar loads) instead of 98 fp64
+// (TRSAPP, BIGLAG, BIGDEN: 49 angles each), exactly as Julia Base's cos/sin give them
+// (gpd_jlmath.h, the oracle's too; oracle/tools/angle_table.py).  Read by uniform index (scalar loads) instead of 98 fp64
 // sin/cos evaluations per search — the bulk of the device NEWUOA's vector instructions.
 constexpr double kAngCos[50] = {
-    0x1.0000000000000p+0, 0x1.fbf675480d903p-1, 0x1.efea21d101ee0p-1, 0x1.dc0ba9def5ae4p-1,
+    0x1.0000000000000p+0, 0x1.fbf675480d903p-1, 0x1.efea21d101ee0p-1, 0x1.dc0ba9def5ae5p-1,
     0x1.c0ab44e81c059p-1, 0x1.9e3779b97f4a8p-1, 0x1.753b603d2b816p-1, 0x1.465c6feb501bbp-1,
     0x1.1257e3c182b50p-1, 0x1.b3ff7c925819cp-2, 0x1.3c6ef372fe950p-2, 0x1.7fc1c65037a75p-3,
     0x1.0130a1be09374p-4, -0x1.0130a1be0937bp-4, -0x1.7fc1c65037a80p-3, -0x1.3c6ef372fe952p-2,
     -0x1.b3ff7c925819dp-2, -0x1.1257e3c182b53p-1, -0x1.465c6feb501bcp-1, -0x1.753b603d2b817p-1,
     -0x1.9e3779b97f4a7p-1, -0x1.c0ab44e81c059p-1, -0x1.dc0ba9def5ae5p-1, -0x1.efea21d101ee0p-1,
     -0x1.fbf675480d903p-1, -0x1.0000000000000p+0, -0x1.fbf675480d903p-1, -0x1.efea21d101ee0p-1,
-    -0x1.dc0ba9def5ae3p-1, -0x1.c0ab44e81c058p-1, -0x1.9e3779b97f4a6p-1, -0x1.753b603d2b816p-1,
+    -0x1.dc0ba9def5ae3p-1, -0x1.c0ab44e81c059p-1, -0x1.9e3779b97f4a6p-1, -0x1.753b603d2b816p-1,
     -0x1.465c6feb501bap-1, -0x1.1257e3c182b4ep-1, -0x1.b3ff7c9258193p-2, -0x1.3c6ef372fe952p-2,
     -0x1.7fc1c65037a79p-3, -0x1.0130a1be0936dp-4, 0x1.0130a1be09392p-4, 0x1.7fc1c65037a8bp-3,
     0x1.3c6ef372fe94cp-2, 0x1.b3ff7c925819bp-2, 0x1.1257e3c182b52p-1, 0x1.465c6feb501bep-1,
@@ -295,7 +297,7 @@ struct Newuoa {
                 ang = 0.5 * (tempa - tempb) / (tempa + tempb);
             }
             ang = dang * ((double)isave + ang);
-            const double cth = cos(ang), sth = sin(ang);
+            const double cth = jl_cos(ang), sth = jl_sin(ang);
             const double reduc = qbeg - (sg + cf * cth) * cth - (dg + dhs * cth) * sth;
             gg = 0.0;
 #pragma unroll
@@ -438,7 +440,7 @@ struct Newuoa {
                 stp = 0.5 * (tempa - tempb) / (tempa + tempb);
             }
             const double ang = dang * ((double)isave + stp);
-            const double cth = cos(ang), sth = sin(ang);
+            const double cth = jl_cos(ang), sth = jl_sin(ang);
             tau = cf1 + (cf2 + cf4 * cth) * cth + (cf3 + cf5 * cth) * sth;
 #pragma unroll
             for (int i = 0; i < N; ++i) {
@@ -671,8 +673,8 @@ struct Newuoa {
                 stp = 0.5 * (tempa - tempb) / (tempa + tempb);
             }
             const double ang = dang * ((double)isave + stp);
-            par[1] = cos(ang);
-            par[2] = sin(ang);
+            par[1] = jl_cos(ang);
+            par[2] = jl_sin(ang);
 #pragma unroll
             for (int j = 3; j <= 7; j += 2) {
                 par[j] = par[1] * par[j - 2] - par[2] * par[j - 1];

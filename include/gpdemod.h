@@ -263,6 +263,15 @@ int gpd_synth_fill_dev(int64_t n_samples, int64_t n_pixels, int64_t pixel_offset
                        double *t, gpd_c64 *d, int64_t ldd, gpd_c64 *fc, int64_t ldfc,
                        int32_t *fc_of_pixel, gpd_param *truth, int device, void *stream);
 
+/*
+ * Julia Base's Float64 elementary functions exactly as the device evaluates them (gpd_jlmath.h:
+ * the restatement the exact evaluator applies per sample, src/Modulation.jl:137,388,419-421,
+ * src/Faint.jl:95-97), for host-vs-device bit-for-bit checks.  fn: 0 sin, 1 cos, 2 sincos (out
+ * holds n (s, c) pairs), 3 atan, 4 atan(x[i], y[i]), 5 hypot(x[i], y[i]), 6 rem_pio2 (n triples
+ * (quadrant, hi, lo)).  Host arrays (y may be NULL for the one-argument functions), synchronous.
+ */
+int gpd_libm_eval(int fn, int64_t n, const double *x, const double *y, double *out, int device);
+
 /* Per-kernel timing of the last gpd_fit_batch_dev call on `device` (ms, HIP events on the
  * launch stream).  names/ms arrays of length cap; returns the number of entries. */
 int gpd_last_timings(int device, const char **names, double *ms, int cap);

@@ -21,6 +21,10 @@
 #include <string.h>
 #include <float.h>
 #include "oracle.h"
+/* Julia Base's sin / sincos / atan(y,x) / hypot, restated once and shared with the device so the
+ * exact evaluator and this oracle compute the same per-sample bits (src/Modulation.jl:137,388,
+ * 419-421; src/Faint.jl:95-97) */
+#include "../gppupildemodulation.jl_amd/csrc/gpd_jlmath.h"
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -86,41 +90,57 @@ static cplx cdiv(cplx z, cplx w) {
 /* exp(im*x) as Julia evaluates exp(Complex(±0, x)): (cos x, sin x); x == 0 → (1, x). */
 static inline cplx cisj(double x) {
     cplx r;
-    if (x == 0) { r.re = 1.0; r.im = x; } else { r.re = cos(x); r.im = sin(x); }
+    if (x == 0) {
+        r.re = 1.0;
+        r.im = x;
+    } else {
+        jl_sincos(x, &r.im, &r.re); /* exp(Complex(0, x)): s, c = sincos(x) */
+    }
     return r;
 }
 
 /* ---- deterministic reduction order -------------------------------------------------
- * Julia's @simd loops and BLAS zdotc fix no summation order, so any order is a faithful
- * evaluation of the reference sums.  The oracle uses the order of the product's exact
- * evaluator: 256 strided partial sums (sample i → partial i mod 256, added in increasing i),
- * each 64-partial group combined by the xor butterfly (off = 32..1), then the four group
- * totals added left to right.  This makes exact-path parity a bit-level comparison. */
-#define GSUM_W 256
+ * Julia's @simd loops, mapreduce's pairwise blocks and BLAS zdotc fix no summation order, so any
+ * order is a faithful evaluation of the reference sums.  The oracle and the product use ONE
+ * canonical order ("CR8"): sample i of a series (index counted from the series' first sample)
+ * adds into slot i mod 2048, slots accumulate in increasing i; the slots form 8 blocks of 256,
+ * each block is 4 groups of 64 combined by the xor butterfly (off = 32..1) with the 4 group
+ * totals added left to right, and the 8 block totals are added left to right.  The device runs
+ * a block per 256-thread workgroup pass (one workgroup sweeping the 8 blocks in turn, or up to 8
+ * workgroups per series exchanging block totals), so every split gives the same bits. */
+#define GSUM_W 2048
+#define GSUM_BLOCK 256
+#define GSUM_NV 16
 typedef struct {
     int nv;
-    double v[GSUM_W][16];
+    double v[GSUM_NV][GSUM_W]; /* [quantity][slot] */
 } gsum_t;
 
 static void gsum_zero(gsum_t *g, int nv) {
     g->nv = nv;
-    memset(g->v, 0, sizeof g->v);
+    memset(g->v, 0, sizeof(double) * GSUM_W * (size_t)nv);
 }
+
+#define GSLOT(g, i, q) ((g)->v[q][(i) % GSUM_W])
 
 static void gsum_total(const gsum_t *g, double *out) {
     double lane[64];
     for (int q = 0; q < g->nv; ++q) {
-        double s = 0.0;
-        for (int w = 0; w < GSUM_W / 64; ++w) {
-            for (int l = 0; l < 64; ++l) lane[l] = g->v[w * 64 + l][q];
-            for (int off = 32; off >= 1; off >>= 1) {
-                double nxt[64];
-                for (int l = 0; l < 64; ++l) nxt[l] = lane[l] + lane[l ^ off];
-                memcpy(lane, nxt, sizeof lane);
+        double total = 0.0;
+        for (int blk = 0; blk < GSUM_W / GSUM_BLOCK; ++blk) {
+            double s = 0.0;
+            for (int w = 0; w < GSUM_BLOCK / 64; ++w) {
+                for (int l = 0; l < 64; ++l) lane[l] = g->v[q][blk * GSUM_BLOCK + w * 64 + l];
+                for (int off = 32; off >= 1; off >>= 1) {
+                    double nxt[64];
+                    for (int l = 0; l < 64; ++l) nxt[l] = lane[l] + lane[l ^ off];
+                    memcpy(lane, nxt, sizeof lane);
+                }
+                s = (w == 0) ? lane[0] : s + lane[0];
             }
-            s = (w == 0) ? lane[0] : s + lane[0];
+            total = (blk == 0) ? s : total + s;
         }
-        out[q] = s;
+        out[q] = total;
     }
 }
 
@@ -160,7 +180,7 @@ static double chi2_eval(chi2_ctx *c, double b, double phi) {
     for (int64_t i = 0; i < n; ++i) {
         double th = c->omega * c->t[i];
         th = th + phi;
-        double beta = b * sin(th);
+        double beta = b * jl_sin(th);
         model[i] = cmul(c->p[i], cisj(beta));
     }
     if (c->offsets) {
@@ -171,17 +191,17 @@ static double chi2_eval(chi2_ctx *c, double b, double phi) {
         for (int64_t i = 0; i < n; ++i) {
             double wi = c->w ? c->w[i] : 1.0;
             cplx m = model[i], dd = c->d[i];
-            double *v = g->v[c->orig[i] % GSUM_W];
-            v[0] += wi;
-            v[1] += wi * m.re;
-            v[2] += wi * m.im;
-            v[3] += wi * (m.re * m.re + m.im * m.im);
-            v[4] += wi * dd.re;
-            v[5] += wi * dd.im;
+            const int64_t o = c->orig[i];
+            GSLOT(g, o, 0) += wi;
+            GSLOT(g, o, 1) += wi * m.re;
+            GSLOT(g, o, 2) += wi * m.im;
+            GSLOT(g, o, 3) += wi * (m.re * m.re + m.im * m.im);
+            GSLOT(g, o, 4) += wi * dd.re;
+            GSLOT(g, o, 5) += wi * dd.im;
             cplx wm = {wi * m.re, wi * (-m.im)}; /* weight[i]*conj(model[i]) */
             cplx pr = cmul(wm, dd);
-            v[6] += pr.re;
-            v[7] += pr.im;
+            GSLOT(g, o, 6) += pr.re;
+            GSLOT(g, o, 7) += pr.im;
         }
         gsum_total(g, tot);
         double a11 = tot[0], a22 = tot[3];
@@ -215,11 +235,11 @@ static double chi2_eval(chi2_ctx *c, double b, double phi) {
             cplx mwc = {mw.re, -mw.im};
             cplx x = cmul(mwc, c->d[i]);
             cplx y = cmul(mwc, model[i]);
-            double *v = g->v[c->orig[i] % GSUM_W];
-            v[0] += x.re;
-            v[1] += x.im;
-            v[2] += y.re;
-            v[3] += y.im;
+            const int64_t o = c->orig[i];
+            GSLOT(g, o, 0) += x.re;
+            GSLOT(g, o, 1) += x.im;
+            GSLOT(g, o, 2) += y.re;
+            GSLOT(g, o, 3) += y.im;
         }
         gsum_total(g, tot);
         cplx num = {tot[0], tot[1]}, den = {tot[2], tot[3]};
@@ -238,7 +258,7 @@ static double chi2_eval(chi2_ctx *c, double b, double phi) {
         for (int64_t i = 0; i < n; ++i) {
             double rr = model[i].re - c->d[i].re, ri = model[i].im - c->d[i].im;
             double a2 = rr * rr + ri * ri;
-            g->v[c->orig[i] % GSUM_W][0] += (c->w ? c->w[i] : 1.0) * a2;
+            GSLOT(g, c->orig[i], 0) += (c->w ? c->w[i] : 1.0) * a2;
         }
         gsum_total(g, &s);
     }
@@ -291,17 +311,16 @@ static void mean_var_power_idx(int64_t n, const int8_t *states, const cplx *d, c
     gsum_zero(g, 10);
     for (int64_t i = 0; i < n; ++i) {
         int q = states[i] + 1; /* TRANSIENT=-1 → 0 ... HIGH=3 → 4 */
-        double *v = g->v[orig[i] % GSUM_W];
-        v[q] += 1.0;
-        v[5 + q] += hypot(d[i].re, d[i].im); /* abs(::Complex) = hypot */
+        GSLOT(g, orig[i], q) += 1.0;
+        GSLOT(g, orig[i], 5 + q) += jl_hypot(d[i].re, d[i].im); /* abs(::Complex) = hypot */
     }
     gsum_total(g, tot);
     for (int q = 0; q < 5; ++q) m5[q] = tot[5 + q] / tot[q];
     gsum_zero(g, 5);
     for (int64_t i = 0; i < n; ++i) {
         int q = states[i] + 1;
-        double dv = hypot(d[i].re, d[i].im) - m5[q];
-        g->v[orig[i] % GSUM_W][q] += dv * dv;
+        double dv = jl_hypot(d[i].re, d[i].im) - m5[q];
+        GSLOT(g, orig[i], q) += dv * dv;
     }
     gsum_total(g, ss);
     for (int q = 0; q < 5; ++q) w5[q] = 1.0 / (ss[q] / (tot[q] - 1.0));
@@ -402,7 +421,7 @@ static void fit_pixel(int64_t n, const double *t, const cplx *dcol, const cplx *
         s->t[nv] = t[i];
         s->orig[nv] = i;
         s->d[nv] = dcol[i];
-        s->p[nv] = cisj(atan2(fccol[i].im, fccol[i].re));
+        s->p[nv] = cisj(jl_atan2(fccol[i].im, fccol[i].re));
         nv++;
     }
     if (faint) {
@@ -468,22 +487,22 @@ static void fit_pixel(int64_t n, const double *t, const cplx *dcol, const cplx *
     if (outcol) { /* output column over ALL samples (src/Modulation.jl:417-425) */
         double b = par->b, phi = par->phi;
         cplx aa = {par->a_re, par->a_im}, cc = {par->c_re, par->c_im};
-        double arga = atan2(aa.im, aa.re);
+        double arga = jl_atan2(aa.im, aa.re);
         for (int64_t i = 0; i < n; ++i) {
             double th = omega * t[i];
             th = th + phi;
             cplx dd = dcol[i];
             if (flags & ORACLE_RECENTER) {
-                double ph = b * sin(th); /* getphase: b .* sin.(ω .* t .+ ϕ) .+ angle(a) */
+                double ph = b * jl_sin(th); /* getphase: b .* sin.(ω .* t .+ ϕ) .+ angle(a) */
                 ph = ph + arga;
                 double psi = ph - arga;
                 cplx e = cisj(-psi);
                 if (offsets) { dd.re = dd.re - cc.re; dd.im = dd.im - cc.im; }
                 outcol[i] = cmul(dd, e);
             } else { /* data * exp(-im*angle(mod(t))) */
-                cplx mv = cmul(aa, cisj(b * sin(th)));
+                cplx mv = cmul(aa, cisj(b * jl_sin(th)));
                 if (offsets) { mv.re = cc.re + mv.re; mv.im = cc.im + mv.im; }
-                outcol[i] = cmul(dd, cisj(-atan2(mv.im, mv.re)));
+                outcol[i] = cmul(dd, cisj(-jl_atan2(mv.im, mv.re)));
             }
         }
     }
@@ -532,6 +551,32 @@ int oracle_fit_batch(int64_t n_samples, int64_t n_pixels, const double *t, const
         free(s.model);
         free(s.orig);
         free(s.gs);
+    }
+    return 0;
+}
+
+/* Elementwise evaluation of the shared Julia-libm restatement (tests/test_jlmath.py).
+ * fn: 0 sin, 1 cos, 2 sincos → (s, c) pairs in out[2i..2i+1], 3 atan, 4 atan(x[i], y[i]),
+ *     5 hypot(x[i], y[i]), 6 rem_pio2 → (n, hi, lo) triples in out[3i..3i+2] */
+int oracle_jl_eval(int fn, int64_t n, const double *x, const double *y, double *out) {
+    for (int64_t i = 0; i < n; ++i) {
+        switch (fn) {
+        case 0: out[i] = jl_sin(x[i]); break;
+        case 1: out[i] = jl_cos(x[i]); break;
+        case 2: jl_sincos(x[i], &out[2 * i], &out[2 * i + 1]); break;
+        case 3: out[i] = jl_atan(x[i]); break;
+        case 4: out[i] = jl_atan2(x[i], y[i]); break;
+        case 5: out[i] = jl_hypot(x[i], y[i]); break;
+        case 6: {
+            double hi, lo;
+            const int q = jl_rem_pio2(x[i], &hi, &lo);
+            out[3 * i] = (double)q;
+            out[3 * i + 1] = hi;
+            out[3 * i + 2] = lo;
+            break;
+        }
+        default: return -1;
+        }
     }
     return 0;
 }

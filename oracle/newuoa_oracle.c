@@ -18,6 +18,9 @@
 #include <math.h>
 #include <stddef.h>
 #include "oracle.h"
+/* cos/sin of the trial angles as OptimPackNextGen (pure Julia) evaluates them: Julia Base's
+ * msun-derived functions, restated once for the oracle and the device */
+#include "../gppupildemodulation.jl_amd/csrc/gpd_jlmath.h"
 
 #define ZERO 0.0
 #define HALF 0.5
@@ -150,8 +153,8 @@ L120:
     qnew = qbeg;
     for (i = 1; i <= iu; ++i) {
         angle = (double)i * temp;
-        cth = cos(angle);
-        sth = sin(angle);
+        cth = jl_cos(angle);
+        sth = jl_sin(angle);
         qnew = (sg + cf * cth) * cth + (dg + dhs * cth) * sth;
         if (qnew < qmin) {
             qmin = qnew;
@@ -171,8 +174,8 @@ L120:
         angle = HALF * (tempa - tempb) / (tempa + tempb);
     }
     angle = temp * ((double)isave + angle);
-    cth = cos(angle);
-    sth = sin(angle);
+    cth = jl_cos(angle);
+    sth = jl_sin(angle);
     reduc = qbeg - (sg + cf * cth) * cth - (dg + dhs * cth) * sth;
     gg = ZERO;
     for (i = 1; i <= n; ++i) {
@@ -316,8 +319,8 @@ L80:
     tau = taubeg;
     for (i = 1; i <= iu; ++i) {
         angle = (double)i * temp;
-        cth = cos(angle);
-        sth = sin(angle);
+        cth = jl_cos(angle);
+        sth = jl_sin(angle);
         tau = cf1 + (cf2 + cf4 * cth) * cth + (cf3 + cf5 * cth) * sth;
         if (fabs(tau) > fabs(taumax)) {
             taumax = tau;
@@ -337,8 +340,8 @@ L80:
         step = HALF * (tempa - tempb) / (tempa + tempb);
     }
     angle = temp * ((double)isave + step);
-    cth = cos(angle);
-    sth = sin(angle);
+    cth = jl_cos(angle);
+    sth = jl_sin(angle);
     tau = cf1 + (cf2 + cf4 * cth) * cth + (cf3 + cf5 * cth) * sth;
     for (i = 1; i <= n; ++i) {
         D[i] = cth * D[i] + sth * S[i];
@@ -534,8 +537,8 @@ L70:
     par[1] = ONE;
     for (i = 1; i <= iu; ++i) {
         angle = (double)i * temp;
-        par[2] = cos(angle);
-        par[3] = sin(angle);
+        par[2] = jl_cos(angle);
+        par[3] = jl_sin(angle);
         for (j = 4; j <= 8; j += 2) {
             par[j] = par[2] * par[j - 2] - par[3] * par[j - 1];
             par[j + 1] = par[2] * par[j - 1] + par[3] * par[j - 2];
@@ -561,8 +564,8 @@ L70:
     }
     angle = temp * ((double)isave + step);
 
-    par[2] = cos(angle);
-    par[3] = sin(angle);
+    par[2] = jl_cos(angle);
+    par[3] = jl_sin(angle);
     for (j = 4; j <= 8; j += 2) {
         par[j] = par[2] * par[j - 2] - par[3] * par[j - 1];
         par[j + 1] = par[2] * par[j - 1] + par[3] * par[j - 2];

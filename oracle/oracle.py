@@ -27,7 +27,8 @@ _lib = None
 
 
 def build(force: bool = False) -> str:
-    srcs = ("newuoa_oracle.c", "demod_oracle.c", "oracle.h", "Makefile")
+    srcs = ("newuoa_oracle.c", "demod_oracle.c", "oracle.h", "Makefile",
+            "../gppupildemodulation.jl_amd/csrc/gpd_jlmath.h")
     stale = not os.path.exists(_LIB) or any(
         os.path.getmtime(os.path.join(_HERE, f)) > os.path.getmtime(_LIB) for f in srcs)
     if force or stale:
@@ -63,6 +64,8 @@ def lib():
                                     ctypes.c_double, ctypes.c_int, OBJ, P, P]
         L.oracle_newuoa.restype = ctypes.c_int
         L._OBJ = OBJ
+        L.oracle_jl_eval.argtypes = [ctypes.c_int, ctypes.c_int64, P, P, P]
+        L.oracle_jl_eval.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -142,6 +145,35 @@ def mean_var_power(states, d):
     w = np.zeros(d.size)
     L.oracle_mean_var_power(d.size, _ptr(s), _ptr(d), _ptr(m), _ptr(w))
     return m, w
+
+
+JL_FN = {"sin": 0, "cos": 1, "sincos": 2, "atan": 3, "atan2": 4, "hypot": 5, "rem_pio2": 6}
+
+
+def jl_eval(fn, x, y=None):
+    """The shared Julia-Base libm restatement (gpd_jlmath.h) on the host, elementwise.
+    sincos → (n, 2) [s, c]; rem_pio2 → (n, 3) [quadrant, hi, lo]; atan2(x=y_coord, y=x_coord)
+    takes (x, y) = (imaginary, real) like Julia's atan(y, x)."""
+    code = JL_FN[fn]
+    x = np.ascontiguousarray(x, dtype=np.float64).ravel()
+    yy = None if y is None else np.ascontiguousarray(y, dtype=np.float64).ravel()
+    width = {2: 2, 6: 3}.get(code, 1)
+    out = np.empty(x.size * width)
+    if lib().oracle_jl_eval(code, x.size, _ptr(x), _ptr(yy), _ptr(out)) != 0:
+        raise ValueError(fn)
+    return out.reshape(-1, width) if width > 1 else out
+
+
+def fc_phasor(fc):
+    """exp.(im .* angle.(fc)) (src/Modulation.jl:388) with Julia Base's atan(y, x) and sincos
+    (the shared restatement): p = (cos θ, sin θ), θ = atan(im, re); θ == 0 → (1, θ)."""
+    fc = np.asarray(fc, dtype=np.complex128)
+    th = jl_eval("atan2", fc.imag.ravel(), fc.real.ravel())
+    sc = jl_eval("sincos", th)
+    p = sc[:, 1] + 1j * sc[:, 0]
+    zero = th == 0
+    p[zero] = 1.0 + 1j * th[zero]
+    return p.reshape(fc.shape)
 
 
 def phi_grid():

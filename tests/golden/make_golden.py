@@ -37,20 +37,26 @@ def states(N):
     return st
 
 
-def run_case(oracle, spec):
+def case_inputs(spec):
+    """(batch, states or None, xinit or None) of a fixture case — shared with the GPU test."""
     import synth
 
     B = synth.make_batch(spec["N"], spec["P"], seed=spec["seed"], t0=spec.get("t0", 0.0),
                          offsets=spec.get("offsets", False))
+    st = states(spec["N"]) if spec.get("faint") else None
+    if st is not None:
+        B["d"] = B["d"] * np.where(st == 3, 1.1, np.where(st == 1, 0.3, 0.6))[None, :]
+    xi = np.array(spec["xinit"]) if "xinit" in spec else None
+    return B, st, xi
+
+
+def run_case(oracle, spec):
+    B, st, xi = case_inputs(spec)
     flags = oracle.RECENTER if spec.get("recenter", True) else 0
     if spec.get("offsets"):
         flags |= oracle.FIT_OFFSETS
     if spec.get("onlyhigh"):
         flags |= oracle.ONLY_HIGH
-    st = states(spec["N"]) if spec.get("faint") else None
-    if st is not None:
-        B["d"] = B["d"] * np.where(st == 3, 1.1, np.where(st == 1, 0.3, 0.6))[None, :]
-    xi = np.array(spec["xinit"]) if "xinit" in spec else None
     par = oracle.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], state=st, xinit=xi,
                            flags=flags, nthreads=1)
     return {"b": par["b"].tolist(), "phi": par["phi"].tolist(), "chi2": par["chi2"].tolist(),

@@ -198,19 +198,18 @@ def test_device_bessel_matches_scipy(tmp_path):
         assert np.all(np.abs(out[big] - ref[big]) <= 1e-13 * np.abs(ref[big]) + 1e-300)
 
 
-def test_newuoa_angle_table_is_the_oracles_libm():
-    """kAngCos/kAngSin (gpd_newuoa.hpp) hold cos/sin(i·2π/50) exactly as the oracle's libm
-    computes them (oracle/tools/angle_table.py): the device NEWUOA's angle searches then use the
-    oracle's own numbers."""
-    import math
+def test_newuoa_angle_table_is_the_oracles_libm(oracle):
+    """kAngCos/kAngSin (gpd_newuoa.hpp) hold cos/sin(i·2π/50) exactly as Julia Base computes them
+    (gpd_jlmath.h, which the oracle's NEWUOA also calls; oracle/tools/angle_table.py): the device
+    NEWUOA's angle searches use the oracle's own numbers."""
     import re
     text = open(os.path.join(CSRC, "gpd_newuoa.hpp")).read()
-    dang = 6.283185307179586476925286766559 / 50.0
-    for name, fn in (("kAngCos", math.cos), ("kAngSin", math.sin)):
+    ang = np.array([float(i) * (6.283185307179586476925286766559 / 50.0) for i in range(50)])
+    for name, fn in (("kAngCos", "cos"), ("kAngSin", "sin")):
         body = re.search(name + r"\[50\] = \{([^}]*)\}", text).group(1)
         vals = [float.fromhex(v) for v in re.findall(r"-?0x[0-9a-f.]+p[-+]\d+", body)]
         assert len(vals) == 50
-        assert vals == [fn(float(i) * dang) for i in range(50)]
+        assert vals == [float(v) for v in oracle.jl_eval(fn, ang)]
 
 
 def _build_c_example(out):

@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 import synth
-from test_gpu_parity import assert_fit_parity, faint_states, ulps_for
+from test_gpu_parity import assert_exact_bitwise, assert_fit_parity, faint_states, ulps_for
 
 NPERTURB = 24  # short windows: more outcomes per series to sample
 
@@ -52,11 +52,21 @@ def test_windows_match_oracle(gpu, oracle, N, nwindow, method):
         spans = np.minimum(nwindow, N - nwindow * np.arange(got.shape[0]))
         assert np.all(exact[spans < 256])  # short last window: exact fallback
         assert np.mean(~exact[spans >= 256]) > 0.9  # harmonic fits
-    # few-hundred-sample windows: the oracle's own outcomes under ulp noise spread beyond
-    # NEWUOA's rhoend (1e-3), so the bound on any landing point is relaxed there
-    print(assert_fit_parity(got.reshape(-1), ref.reshape(-1), [p.reshape(-1) for p in pert],
-                            label=f"windows {method} N={N} w={nwindow}",
-                            max_dev=1e-3 if min(nwindow, N % nwindow or nwindow) >= 500 else 1e-2))
+    if method == "exact":
+        print(assert_exact_bitwise(got.reshape(-1), ref.reshape(-1),
+                                   label=f"windows exact N={N} w={nwindow}"))
+    else:
+        # windows shorter than 256 samples (and a short last window) are fitted exactly: bitwise
+        sp = np.minimum(nwindow, N - nwindow * np.arange(got.shape[0]))
+        print(assert_exact_bitwise(got[sp < 256].reshape(-1), ref[sp < 256].reshape(-1),
+                                   label="short windows"))
+        # few-hundred-sample windows: the oracle's own outcomes under ulp noise spread beyond
+        # NEWUOA's rhoend (1e-3), so the bound on any landing point is relaxed there
+        print(assert_fit_parity(got[sp >= 256].reshape(-1), ref[sp >= 256].reshape(-1),
+                                [p[sp >= 256].reshape(-1) for p in pert],
+                                label=f"windows {method} N={N} w={nwindow}",
+                                max_dev=1e-3 if min(nwindow, N % nwindow or nwindow) >= 500 else 1e-2)
+              if np.any(sp >= 256) else "no harmonic windows")
     # output rows of window w use window w's parameters (src/GPPupilDemodulation.jl:207)
     for w in range(ref.shape[0]):
         I = slice(w * nwindow, min(N, (w + 1) * nwindow))
@@ -80,6 +90,10 @@ def test_windows_faint(gpu, oracle, onlyhigh, method):
     flags = oracle.RECENTER | (oracle.ONLY_HIGH if onlyhigh else 0)
     ref, pert = oracle_windows(oracle, B, nwindow, B["fc_of_pixel"], state=st, flags=flags,
                                ulps=ulps_for(method))
+    if method == "exact":
+        print(assert_exact_bitwise(got.reshape(-1), ref.reshape(-1),
+                                   label=f"faint windows exact onlyhigh={onlyhigh}"))
+        return
     print(assert_fit_parity(got.reshape(-1), ref.reshape(-1), [p.reshape(-1) for p in pert],
                             label=f"faint windows {method} onlyhigh={onlyhigh}"))
 
@@ -89,15 +103,10 @@ def test_windows_offsets_and_multi_gpu_split(gpu, oracle):
     B = synth.make_batch(N, 32, seed=9, offsets=True)
     got = gpu.fit_windows(B["t"], B["d"], B["fc"], B["fc_of_pixel"], nwindow, fitoffsets=True,
                           n_gpus=8)  # clamps to the visible devices
-    # the offsets χ² (2×2 Cramer solve, src/Modulation.jl:189-192) matches the oracle to ≤ 2 ulp
-    # (test_chi2_evaluation_parity); short windows make its landscape flat, so the envelope
-    # perturbs by up to 4 ulp
-    ref, pert = oracle_windows(oracle, B, nwindow, B["fc_of_pixel"],
-                               flags=oracle.RECENTER | oracle.FIT_OFFSETS, ulps=4.0)
-    # 1000-sample windows with offsets: the oracle re-routes ~30 % of series under its own
-    # ulp noise, so the strict-match floor is lowered accordingly
-    print(assert_fit_parity(got.reshape(-1), ref.reshape(-1), [p.reshape(-1) for p in pert],
-                            label="offsets windows", min_match=0.5))
+    # windows with fitoffsets are fitted by the exact evaluator: the oracle's bits per window
+    ref, _ = oracle_windows(oracle, B, nwindow, B["fc_of_pixel"],
+                            flags=oracle.RECENTER | oracle.FIT_OFFSETS, ulps=4.0)
+    print(assert_exact_bitwise(got.reshape(-1), ref.reshape(-1), label="offsets windows"))
 
 
 def test_windows_harmonic_offsets_rejected(gpu):

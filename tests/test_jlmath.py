@@ -1,0 +1,206 @@
+"""The shared restatement of Julia Base's Float64 sin / cos / sincos / atan / atan(y, x) / hypot /
+rem_pio2 (gppupildemodulation.jl_amd/csrc/gpd_jlmath.h): the functions the reference applies per
+sample (src/Modulation.jl:137,388,419-421; src/Faint.jl:95-97) and OptimPackNextGen's NEWUOA per
+trial angle.  One source is compiled into the oracle (gcc) and the device (hipcc, gfx950).
+
+CPU: the constants are re-derived from exact integer arithmetic, the functions are checked
+against correctly rounded values (decimal, 110 digits) and glibc — msun's kernels are within one
+ulp and agree with the correctly rounded value for ~97 % of arguments.  Parity of the
+restatement with Julia itself stays UNPINNED (no Julia here).
+GPU: the device evaluates every function bit for bit as the oracle does, over argument ranges
+that take every reduction branch (two-constant and extended Cody–Waite, Payne–Hanek at
+MJD-scale arguments) and the special values."""
+import math
+import os
+import re
+import sys
+from decimal import Decimal, getcontext
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "gppupildemodulation.jl_amd", "csrc", "gpd_jlmath.h")
+sys.path.insert(0, os.path.join(ROOT, "oracle", "tools"))
+import inv2pi  # noqa: E402
+
+
+def ulps(a, b):
+    """Distance in units in the last place between two float64 arrays (same sign or zero)."""
+    ai = np.asarray(a, dtype=np.float64).view(np.int64)
+    bi = np.asarray(b, dtype=np.float64).view(np.int64)
+    lo = np.int64(-0x8000000000000000)
+    ai = np.where(ai < 0, lo - ai, ai)
+    bi = np.where(bi < 0, lo - bi, bi)
+    return np.abs(ai - bi)
+
+
+def same_bits(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    both_nan = np.isnan(a) & np.isnan(b)
+    return np.all(both_nan | (a.view(np.int64) == b.view(np.int64)))
+
+
+def test_inv2pi_words_and_hypot_thresholds_are_exact():
+    text = open(HDR).read()
+    body = text[text.index("jlm_inv2pi(int i)"):text.index("default: return 0;")]
+    words = [int(w, 16) for w in re.findall(r"return 0x([0-9a-f]{16})ull", body)]
+    assert words == inv2pi.inv2pi_words()
+    th = inv2pi.hypot_thresholds()
+    assert th["sqrt(eps/2)"] in text and th["sqrt(floatmax/2)"] in text
+
+
+def argument_sets(rng, n):
+    """Every branch of rem_pio2_kernel: |x| < π/4 (no reduction), ≲ 9π/4 (two constants, n=±1..±4),
+    near multiples of π/2 (the extended scheme), < 2^20·π/2 (extended), MJD-scale ω·t ≈ 3.3e10 and
+    huge arguments (Payne–Hanek)."""
+    mult = np.array([k * math.pi / 2 for k in range(-8, 9) if k])
+    near = (np.tile(mult, n // 16 + 1) * (1 + rng.uniform(-1e-9, 1e-9, 16 * (n // 16 + 1))))[:n]
+    return {
+        "small": rng.uniform(-0.785, 0.785, n),
+        "quadrants": rng.uniform(-7.1, 7.1, n),
+        "near_k_pi_2": near,
+        "medium": rng.uniform(-1.6e6, 1.6e6, n),
+        "mjd": rng.uniform(3.2e10, 3.4e10, n),
+        "huge": np.sign(rng.uniform(-1, 1, n)) * 10.0 ** rng.uniform(7, 300, n),
+        "tiny": np.sign(rng.uniform(-1, 1, n)) * 10.0 ** rng.uniform(-320, -7, n),
+    }
+
+
+@pytest.mark.parametrize("fn", ["sin", "cos"])
+def test_sin_cos_against_glibc(oracle, fn):
+    rng = np.random.default_rng(3)
+    ref = np.vectorize(getattr(math, fn))
+    for name, x in argument_sets(rng, 40000).items():
+        got = oracle.jl_eval(fn, x)
+        u = ulps(got, ref(x))
+        assert u.max() <= 1, (fn, name, u.max())
+        assert (u == 0).mean() >= 0.95, (fn, name, (u == 0).mean())
+
+
+def _dec_pi(bits=380):
+    return Decimal(inv2pi.pi_fixed(bits)) / (Decimal(2) ** bits)
+
+
+def _dec_sin_cos(x, pi):
+    X = Decimal(x)
+    k = (X / (pi / 2)).to_integral_value()
+    r = X - k * (pi / 2)
+    r2 = r * r
+    eps = Decimal(10) ** -105
+    s = t = r
+    n = 1
+    while abs(t) > eps:
+        t = -t * r2 / ((2 * n) * (2 * n + 1))
+        s += t
+        n += 1
+    c = t = Decimal(1)
+    n = 1
+    while abs(t) > eps:
+        t = -t * r2 / ((2 * n - 1) * (2 * n))
+        c += t
+        n += 1
+    q = int(k) % 4
+    return [(s, c), (c, -s), (-s, -c), (-c, s)][q]
+
+
+def test_sin_cos_against_correctly_rounded(oracle):
+    """msun's sin/cos: within one ulp of the correctly rounded value everywhere, equal to it for
+    the large majority of arguments (the reduction is exact up to MJD scale)."""
+    getcontext().prec = 110
+    pi = _dec_pi()
+    rng = np.random.default_rng(5)
+    for lo, hi in ((-0.785, 0.785), (-10.0, 10.0), (-2e3, 2e3), (1e5, 1.6e6), (3.2e10, 3.4e10)):
+        x = rng.uniform(lo, hi, 600)
+        sc = [_dec_sin_cos(v, pi) for v in x]
+        cr_s = np.array([float(s) for s, _ in sc])
+        cr_c = np.array([float(c) for _, c in sc])
+        for got, cr in ((oracle.jl_eval("sin", x), cr_s), (oracle.jl_eval("cos", x), cr_c)):
+            u = ulps(got, cr)
+            assert u.max() <= 1 and (u == 0).mean() >= 0.93, (lo, hi, u.max(), (u == 0).mean())
+
+
+def test_sincos_is_sin_and_cos(oracle):
+    """Julia's sincos returns the very values of sin and cos (exp(Complex(0, β)) and sin(θ) of
+    the model agree)."""
+    rng = np.random.default_rng(7)
+    for x in argument_sets(rng, 20000).values():
+        sc = oracle.jl_eval("sincos", x)
+        assert same_bits(sc[:, 0], oracle.jl_eval("sin", x))
+        assert same_bits(sc[:, 1], oracle.jl_eval("cos", x))
+
+
+def test_rem_pio2_is_an_exact_reduction(oracle):
+    """x = n·π/2 + (hi + lo) far beyond double precision of the remainder (msun's design: the
+    Cody–Waite rounds stop once ~2^-70 of |hi| is reached, Payne–Hanek keeps ~2^-100; checked in
+    420-digit decimal arithmetic)."""
+    getcontext().prec = 420  # |x| up to 1e300
+    pi = _dec_pi(1500)
+    rng = np.random.default_rng(9)
+    for name, x in argument_sets(rng, 300).items():
+        x = x[np.abs(x) >= 0.7854]  # the callers reduce only |x| ≥ π/4
+        if x.size == 0:
+            continue
+        r = oracle.jl_eval("rem_pio2", x)
+        for xi, (q, hi, lo) in zip(x, r):
+            assert abs(hi) <= 0.7854 + 1e-9
+            exact = Decimal(xi) - Decimal(int(q)) * (pi / 2)
+            # Payne–Hanek returns the quadrant modulo 4: compare the remainder modulo 2π
+            exact = exact - ((exact - Decimal(hi)) / (2 * pi)).to_integral_value() * 2 * pi
+            err = abs(exact - (Decimal(hi) + Decimal(lo)))
+            assert err <= Decimal(2) ** -68 * abs(Decimal(hi)), (name, xi, q, hi, lo, err)
+
+
+def test_atan_atan2_hypot_against_glibc(oracle):
+    rng = np.random.default_rng(11)
+    n = 100000
+    x = rng.standard_normal(n) * np.exp(rng.uniform(-30, 30, n))
+    y = rng.standard_normal(n) * np.exp(rng.uniform(-30, 30, n))
+    u = ulps(oracle.jl_eval("atan", x), np.vectorize(math.atan)(x))
+    assert u.max() <= 1 and (u == 0).mean() >= 0.98
+    u = ulps(oracle.jl_eval("atan2", y, x), np.vectorize(math.atan2)(y, x))
+    assert u.max() <= 1 and (u == 0).mean() >= 0.8
+    # Julia's hypot with hardware fma is correctly rounded, as is glibc's
+    assert same_bits(oracle.jl_eval("hypot", x, y), np.vectorize(math.hypot)(x, y))
+
+
+def test_special_values(oracle):
+    inf, nan = math.inf, math.nan
+    s = oracle.jl_eval("sin", [0.0, -0.0, inf, -inf, nan, 1e-300])
+    assert s[0] == 0 and math.copysign(1, s[1]) == -1 and np.isnan(s[2:5]).all() and s[5] == 1e-300
+    c = oracle.jl_eval("cos", [0.0, inf, nan])
+    assert c[0] == 1.0 and np.isnan(c[1:]).all()
+    # angle(Complex(x, y)) = atan(y, x): the quadrant conventions of src/Modulation.jl:388
+    y = np.array([0.0, -0.0, 0.0, -0.0, 1.0, -1.0, inf, inf, -inf, 1.0, 2.0, nan])
+    x = np.array([1.0, 1.0, -1.0, -1.0, 0.0, 0.0, inf, -inf, 5.0, -inf, 1.0, 1.0])
+    ref = np.array([math.atan2(a, b) for a, b in zip(y, x)])
+    got = oracle.jl_eval("atan2", y, x)
+    assert same_bits(got[:-1], ref[:-1]) and np.isnan(got[-1])
+    h = oracle.jl_eval("hypot", [inf, nan, 3.0, 0.0, 1e-310], [nan, inf, 4.0, 0.0, 1e-310])
+    assert h[0] == inf and h[1] == inf and h[2] == 5.0 and h[3] == 0.0
+    assert h[4] == math.hypot(1e-310, 1e-310)
+
+
+@pytest.mark.gpu
+def test_device_libm_equals_oracle_bitwise(gpu, oracle):
+    """The exact evaluator's per-sample functions on the device = the oracle's, bit for bit."""
+    rng = np.random.default_rng(13)
+    sets = argument_sets(rng, 50000)
+    specials = np.array([0.0, -0.0, math.inf, -math.inf, math.nan, 5e-324, -5e-324, 1e-310,
+                         math.pi / 2, math.pi, 3 * math.pi / 2, 2 * math.pi, 1e300, -1e300,
+                         2.0 ** 1023, 86400.0 * 60000.0 * 6.283185])
+    sets["specials"] = specials
+    for name, x in sets.items():
+        for fn in ("sin", "cos", "sincos", "atan", "rem_pio2"):
+            if fn == "rem_pio2":
+                x = x[np.isfinite(x) & (np.abs(x) >= 0.7854)]
+            d, h = gpu.libm_eval(fn, x), oracle.jl_eval(fn, x)
+            assert same_bits(d, h), (fn, name, np.nonzero(~(d.view(np.int64) == h.view(np.int64)))[0][:5])
+    n = 200000
+    xs = rng.standard_normal(n) * np.exp(rng.uniform(-40, 40, n))
+    ys = rng.standard_normal(n) * np.exp(rng.uniform(-40, 40, n))
+    xs[:16] = specials
+    ys[:16] = specials[::-1]
+    for fn in ("atan2", "hypot"):
+        assert same_bits(gpu.libm_eval(fn, xs, ys), oracle.jl_eval(fn, xs, ys)), fn

@@ -1,20 +1,33 @@
-"""C2 exposure (32 diodes x 1e5) through gpd_fit_batch with and without fitoffsets (the
-exact evaluator is the fitoffsets default): wall time per call and kernel times."""
-import sys, time, json
+"""C2 exposure (32 diodes × 1e5) through gpd_fit_batch: harmonic (default without offsets) and
+the exact evaluator (the fitoffsets default, the reference's `--center fit`), the latter with
+each series split over G = 1, 2, 4, 8 workgroups (GPD_EXACT_G; default 8 for 32 series).
+Prints one JSON line per case: host wall time per call (PCIe included) and kernel times."""
+import json
 import os
+import sys
+import time
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for _p in (ROOT, os.path.join(ROOT, 'tests')):
+for _p in (ROOT, os.path.join(ROOT, "tests")):
     sys.path.insert(0, _p)
-import torch  # noqa
-import numpy as np
-import gpdemod_loader, synth
+import torch  # noqa: F401,E402  (HIP runtime order, as in the tests)
+import gpdemod_loader  # noqa: E402
+import synth  # noqa: E402
+
 gpd = gpdemod_loader.load()
 B = synth.make_batch(100000, 32, seed=42, offsets=True)
 args = (B["t"], B["d"], B["fc"], B["fc_of_pixel"])
-for off in (False, True):
-    gpd.fit_batch(*args, fitoffsets=off)
+cases = [(False, "auto", None)] + [(off, "exact", g) for off in (False, True)
+                                     for g in ("1", "2", "4", "8")]
+for off, method, g in cases:
+    if g is None:
+        os.environ.pop("GPD_EXACT_G", None)
+    else:
+        os.environ["GPD_EXACT_G"] = g
+    gpd.fit_batch(*args, fitoffsets=off, method=method)
     t0 = time.perf_counter()
     for _ in range(3):
-        gpd.fit_batch(*args, fitoffsets=off)
-    print(json.dumps({"fitoffsets": off, "ms": (time.perf_counter() - t0) / 3 * 1e3,
-                      "kernels": gpd.timings(0)}))
+        gpd.fit_batch(*args, fitoffsets=off, method=method)
+    print(json.dumps({"fitoffsets": off, "method": method, "G": g,
+                      "ms": round((time.perf_counter() - t0) / 3 * 1e3, 3),
+                      "kernels_ms": {k: round(v, 3) for k, v in gpd.timings(0).items()}}))
