@@ -11,7 +11,9 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgpdemod.so")
+# GPD_LIB=diag: the diagnostics build (moment-kernel timing variants, build.py --diag)
+LIB_PATH = os.path.join(HERE, "libgpdemod_diag.so" if os.environ.get("GPD_LIB") == "diag"
+                        else "libgpdemod.so")
 
 GPD_ABI_VERSION = 1
 GPD_FIT_OFFSETS = 0x1

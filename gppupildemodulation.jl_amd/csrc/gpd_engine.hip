@@ -91,8 +91,10 @@ struct Layout {
     size_t info, tab, part, mom, aux, fstat, raw, list, phbuf, partG, momG, auxG, fcid, d0, mcache,
         xtot, xcnt, total;
     long long mstride;  // model-cache elements per exact-path workgroup (0: no cache)
-    int nch;
-    long long chunk;
+    int nch;            // sample chunks of the moment grid (grid.y)
+    long long chunk;    // samples per chunk (a whole number of units)
+    int units;          // sample units = partial-moment sets
+    long long unit_len; // samples per unit
 };
 
 Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic, bool phbuf,
@@ -104,37 +106,39 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
         off += align_up(bytes);
         return o;
     };
-    // moment-pass grid: (series groups) × (sample chunks).  The producer/consumer kernel runs
-    // one workgroup per CU, so the chunk count is chosen to fill the last wave of workgroups:
-    // among 6..32 chunks the one whose grid wastes the smallest fraction of its last wave
-    // (C3 on 256 CUs: 782 × 17 = 13294 = 51.9 waves) — more chunks also mean more partial
-    // moments (nch·99·P doubles), so ties go to the smaller count.  Few series (npg·6 below
-    // the CU count): ~6k workgroups of short chunks instead.
+    // moment-pass grid: (series groups) × (sample chunks).  The samples are cut into U ≤ 32
+    // fixed units (whole 32-sample tiles, a function of N only) and every unit gets its own set
+    // of partial moments, reduced in unit order — so a series' moments do not depend on P, i.e.
+    // on the batch or the shard it is in (a sharded run gives the 1-GPU records bit for bit).
+    // A workgroup of the producer/consumer kernel (one per CU) streams `upw` consecutive units;
+    // upw is chosen to fill the last wave of workgroups: the smallest number of unit-times
+    // ceil(npg·ceil(U/upw) / n_cu)·upw, ties to the larger upw (fewer, longer workgroups).
+    // C3 (782 series groups, 256 CUs): upw 2 → 12512 workgroups = 48.9 waves; 12 500 series
+    // per GPU (C4 on 8 GPUs, 98 groups): upw 1 → 3136 = 12.25 waves.
     const long long per = mfma ? MM_PIX : 64;
     const long long npg = (P + per - 1) / per;
-    long long nch = 1;
-    if (harmonic) {
-        if (mfma && n_cu > 0 && npg * 6 >= n_cu) {
-            double best = 2.0;
-            for (long long c = 6; c <= 32; ++c) {
-                const double w = (double)(npg * c) / n_cu;
-                const double waste = (std::ceil(w) - w) / std::ceil(w);
-                if (waste < best - 0.005) {
-                    best = waste;
-                    nch = c;
-                }
+    long long U = std::min<long long>(32, std::max<long long>(1, (N + 255) / 256));
+    long long ulen = (N + U - 1) / U;
+    ulen = (ulen + MM_TS - 1) / MM_TS * MM_TS;
+    U = (N + ulen - 1) / ulen;
+    long long upw = 1;
+    if (harmonic && mfma && n_cu > 0) {
+        long long best = LLONG_MAX;
+        for (long long w = 1; w <= U; ++w) {
+            const long long wg = npg * ((U + w - 1) / w);
+            const long long cost = (wg + n_cu - 1) / n_cu * w;
+            if (cost <= best) {
+                best = cost;
+                upw = w;
             }
-        } else {
-            nch = std::max<long long>(1, (mfma ? 6144 : 8192) / std::max<long long>(npg, 1));
         }
     }
-    if (const char *e = getenv("GPD_NCH")) nch = std::max(1LL, atoll(e));  // A/B sweeps only
-    nch = std::min<long long>(nch, std::max<long long>(1, (N + 255) / 256));
-    long long chunk = (N + nch - 1) / nch;
-    chunk = (chunk + MM_TS - 1) / MM_TS * MM_TS;
-    nch = (N + chunk - 1) / chunk;
-    L.nch = (int)nch;
-    L.chunk = chunk;
+    if (const char *e = getenv("GPD_UPW")) upw = std::min(U, std::max(1LL, atoll(e)));  // A/B only
+    L.units = (int)U;
+    L.unit_len = ulen;
+    L.chunk = mfma ? upw * ulen : ulen;
+    L.nch = (int)((U + (L.chunk / ulen) - 1) / (L.chunk / ulen));
+    const long long nch = U;  // partial-moment sets
     L.info = take(sizeof(Info));
     // cos/sin table, padded to whole MM_TS-sample tiles (k_table_mix fills the padding)
     L.tab = take(harmonic ? (size_t)((N + MM_TS - 1) / MM_TS * MM_TS) * 2 * KH * sizeof(double) : 0);
@@ -246,12 +250,10 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     hipStream_t stream = (hipStream_t)stream_;
     const bool faint = state != nullptr;
     const bool offs = (flags & GPD_FIT_OFFSETS) != 0;
-    // fp64 MFMA moment pass by default (producer/consumer kernel for non-faint series);
-    // GPD_MOMENTS=valu | mfma1 selects the VALU / single-role MFMA kernel (A/B runs)
+    // fp64 MFMA moment pass (producer/consumer kernel, non-temporal series loads); the VALU
+    // kernel when a series row or the cos/sin table exceeds the buffer descriptors' 32-bit
+    // offsets (N ≳ 1e6 samples) — GPD_MOMENTS=valu forces it (tests of that fallback)
     const char *mk = getenv("GPD_MOMENTS");
-    // the series stream is read exactly once: non-temporal loads (no MALL allocation; C3 moments
-    // 44.6 → 44.1 ms); GPD_NT=0 restores the default policy (A/B runs)
-    static const bool nt_loads = !(getenv("GPD_NT") && std::string(getenv("GPD_NT")) == "0");
     // buffer descriptors of the MFMA kernels address 128 series rows / the cos-sin table
     // with 32-bit offsets
     const double esz = is_c32 ? 8.0 : 16.0;  // bytes per stored complex element
@@ -392,7 +394,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         // the producer/consumer kernel (non-faint whole-exposure series, also the UNIT pass
         // of harmonic fitoffsets) reads the k_table_mix layout when mixing; every other
         // moment kernel the plain rows
-        const bool ws_kernel = use_mfma && window == 0 && !(mk && std::string(mk) == "mfma1");
+        const bool ws_kernel = use_mfma && window == 0;
         tmix = mix && ws_kernel;
         if (tmix)
             k_table_mix<<<(unsigned)((N + MM_TS - 1) / MM_TS * MM_TS / 256 + 1), 256, 0, stream>>>(
@@ -408,46 +410,37 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             mark("moments_win");
         } else if (use_mfma) {
             dim3 g((unsigned)((P + MM_PIX - 1) / MM_PIX), (unsigned)L.nch);
-            const bool mfma1 = mk && std::string(mk) == "mfma1";  // single-role kernel (A/B runs)
-            if (faint && mfma1 && is_c32)
-                k_moments_mfma<true, c32><<<g, 256, 0, stream>>>(pb, tab, fstat, L.chunk, part);
-            else if (faint && mfma1)
-                k_moments_mfma<true><<<g, 256, 0, stream>>>(pb, tab, fstat, L.chunk, part);
-            else if (mfma1)
-                k_moments_mfma<false><<<g, 256, 0, stream>>>(pb, tab, fstat, L.chunk, part);
-            else if (faint && is_c32 && tmix)  // faint series: the producer/consumer kernel, weighted
-                k_moments_ws<0, false, c32, 2, true, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part, fstat);
+            if (faint && is_c32 && tmix)  // faint series: the producer/consumer kernel, weighted
+                k_moments_ws<0, false, c32, 2, true, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, fstat);
             else if (faint && tmix)
-                k_moments_ws<0, false, c64, 2, true, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part, fstat);
+                k_moments_ws<0, false, c64, 2, true, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, fstat);
             else if (faint && is_c32)
-                k_moments_ws<0, false, c32, 2, false, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part, fstat);
+                k_moments_ws<0, false, c32, 2, false, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, fstat);
             else if (faint)
-                k_moments_ws<0, false, c64, 2, false, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part, fstat);
+                k_moments_ws<0, false, c64, 2, false, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, fstat);
             else if (!tmix && is_c32)  // all-f64 MFMA variants (GPD_MIX=0)
-                k_moments_ws<0, false, c32, 2, false><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
+                k_moments_ws<0, false, c32, 2, false><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
             else if (!tmix)
-                k_moments_ws<0, false, c64, 2, false><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
-            else if (is_c32 && nt_loads)  // Float32 storage: the producer/consumer kernel on 8-B elements
-                k_moments_ws<0, false, c32, 2><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
-            else if (is_c32)
-                k_moments_ws<0, false, c32><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
-            else if (!(mk && *mk) && nt_loads)  // the production kernel
-                k_moments_ws<0, false, c64, 2><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
-            else if (mk && std::string(mk) == "ws_nomfma")  // timing experiments only
-                k_moments_ws<1><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
+                k_moments_ws<0, false, c64, 2, false><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
+            else if (is_c32)  // Float32 storage: the producer/consumer kernel on 8-B elements
+                k_moments_ws<0, false, c32, 2><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
+#ifdef GPD_DIAG
+            // timing variants (results invalid), diagnostics build only (build.py --diag)
+            else if (mk && std::string(mk) == "ws_nomfma")
+                k_moments_ws<1><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
             else if (mk && std::string(mk) == "ws_noload")
-                k_moments_ws<2><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
+                k_moments_ws<2><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
             else if (mk && std::string(mk) == "ws_nof0")
-                k_moments_ws<7><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
+                k_moments_ws<7><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
             else if (mk && std::string(mk) == "ws_noq")
-                k_moments_ws<8><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
+                k_moments_ws<8><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
             else if (mk && std::string(mk) == "ws_mfmaonly")
-                k_moments_ws<5><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
+                k_moments_ws<5><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
             else if (mk && std::string(mk) == "ws_prof") {  // cycle split per role (stderr)
                 unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
                 HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_wsprof), z, sizeof z, 0,
                                                hipMemcpyHostToDevice, stream));
-                k_moments_ws<6><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
+                k_moments_ws<6><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
                 HIP_TRY(hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_wsprof), sizeof z, 0,
                                                  hipMemcpyDeviceToHost, stream));
                 HIP_TRY(hipStreamSynchronize(stream));
@@ -457,21 +450,20 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                         "consumer mfma %.3g barrier %.3g\n",
                         z[0] / pw, z[1] / pw, z[2] / pw, z[3] / cw, z[4] / cw);
             }
-            else if (nt_loads)
-                k_moments_ws<0, false, c64, 2><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
-            else
-                k_moments_ws<0><<<g, 512, 0, stream>>>(pb, tab, L.chunk, part);
+#endif
+            else  // the production kernel
+                k_moments_ws<0, false, c64, 2><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
         } else {
-            dim3 g((unsigned)((P + 63) / 64), (unsigned)L.nch);
+            dim3 g((unsigned)((P + 63) / 64), (unsigned)L.units);
             if (faint)
-                k_moments<true><<<g, 64, 0, stream>>>(pb, tab, fstat, L.chunk, part);
+                k_moments<true><<<g, 64, 0, stream>>>(pb, tab, fstat, L.unit_len, part);
             else
-                k_moments<false><<<g, 64, 0, stream>>>(pb, tab, fstat, L.chunk, part);
+                k_moments<false><<<g, 64, 0, stream>>>(pb, tab, fstat, L.unit_len, part);
         }
         if (window == 0) {
             mark("moments");
             dim3 gr((unsigned)((P + 255) / 256), (unsigned)NMOM);
-            k_reduce_moments<<<gr, 256, 0, stream>>>(part, L.nch, P, info, fstat, faint ? 1 : 0,
+            k_reduce_moments<<<gr, 256, 0, stream>>>(part, L.units, P, info, fstat, faint ? 1 : 0,
                                                      mom, aux);
             mark("reduce");
         }
@@ -492,15 +484,15 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             double *partG = (double *)(ws + L.partG), *auxG = (double *)(ws + L.auxG);
             dim3 gG((unsigned)((n_fc + MM_PIX - 1) / MM_PIX), (unsigned)L.nch);
             if (is_c32 && tmix)
-                k_moments_ws<0, true, c32><<<gG, 512, 0, stream>>>(pg, tab, L.chunk, partG);
+                k_moments_ws<0, true, c32><<<gG, 512, 0, stream>>>(pg, tab, L.chunk, L.unit_len, partG);
             else if (tmix)
-                k_moments_ws<0, true><<<gG, 512, 0, stream>>>(pg, tab, L.chunk, partG);
+                k_moments_ws<0, true><<<gG, 512, 0, stream>>>(pg, tab, L.chunk, L.unit_len, partG);
             else if (is_c32)
-                k_moments_ws<0, true, c32, 0, false><<<gG, 512, 0, stream>>>(pg, tab, L.chunk, partG);
+                k_moments_ws<0, true, c32, 0, false><<<gG, 512, 0, stream>>>(pg, tab, L.chunk, L.unit_len, partG);
             else
-                k_moments_ws<0, true, c64, 0, false><<<gG, 512, 0, stream>>>(pg, tab, L.chunk, partG);
+                k_moments_ws<0, true, c64, 0, false><<<gG, 512, 0, stream>>>(pg, tab, L.chunk, L.unit_len, partG);
             dim3 grG((unsigned)((n_fc + 255) / 256), (unsigned)NMOM);
-            k_reduce_moments<<<grG, 256, 0, stream>>>(partG, L.nch, n_fc, info, nullptr, 0, momG, auxG);
+            k_reduce_moments<<<grG, 256, 0, stream>>>(partG, L.units, n_fc, info, nullptr, 0, momG, auxG);
             k_series_sum<<<(unsigned)P, 256, 0, stream>>>(pb, d0);
             mark("offsets_moments");
         }
@@ -709,7 +701,11 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
         set_err(errbuf, errlen, "gpd_batch: no HIP device visible");
         return GPD_E_NODEV;
     }
-    int G = n_gpus <= 0 ? 1 : std::min<int>(n_gpus, ndev);
+    // GPD_FAKE_GPUS=1 (tests): keep n_gpus shards even beyond the visible devices, shard g on
+    // device g % ndev — the multi-device split (series / window ranges, FC column subsets,
+    // record offsets) then runs on a one-GPU box exactly as on an 8-GPU node
+    const bool fake = getenv("GPD_FAKE_GPUS") && atoi(getenv("GPD_FAKE_GPUS")) > 0;
+    int G = n_gpus <= 0 ? 1 : (fake ? std::min<int>(n_gpus, 64) : std::min<int>(n_gpus, ndev));
     const int64_t nwin = window > 0 ? (n_samples + window - 1) / window : 0;
     G = (int)std::min<int64_t>(G, window > 0 ? nwin : n_pixels);
     const int64_t Nall = n_samples;
@@ -737,8 +733,9 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
         }
         const int64_t P = p1 - p0;
         const int64_t nrec = window > 0 ? P * ((N + window - 1) / window) : P;
-        if (hipSetDevice(g) != hipSuccess) {
-            set_err(errbuf_l, errlen_l, "hipSetDevice(%d) failed", g);
+        const int dev = g % ndev;
+        if (hipSetDevice(dev) != hipSuccess) {
+            set_err(errbuf_l, errlen_l, "hipSetDevice(%d) failed", dev);
             return fail(GPD_E_HIP);
         }
         auto chk = [&](hipError_t e, const char *what) {
@@ -759,8 +756,8 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
         const int64_t nfc = (int64_t)cmax - cmin + 1;
         std::vector<int32_t> fcop_l(fc_of_pixel + p0, fc_of_pixel + p1);
         for (auto &c : fcop_l) c -= cmin;
-        DevCtx *cx = ctx_for(g);
-        std::lock_guard<std::mutex> hlk(cx->hmu);
+        DevCtx *cx = ctx_for(dev);
+        std::lock_guard<std::mutex> hlk(cx->hmu);  // shards sharing a device run in turn
         size_t off = 0;
         auto take = [&](size_t bytes) {
             const size_t o = off;
@@ -813,7 +810,7 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
             return fail(GPD_E_HIP);
         }
         int r = pipeline_dev(N, P, dt, dd, N, dfc, nfc, N, dfcop, dst, omega, xinit, flags, maxfun,
-                             (gpd_param *)dpar, (gpd_c64 *)dout, N, dbphi, g, s, errbuf_l,
+                             (gpd_param *)dpar, (gpd_c64 *)dout, N, dbphi, dev, s, errbuf_l,
                              errlen_l, window, is_c32);
         if (r != GPD_OK) {
             cleanup();

@@ -50,7 +50,12 @@ struct Info {
     int pad;
     double qbase;      // mode 1: a multiple of that ulp inside the binade of fl(ωt)
     double xmin, xmax; // range of |fl(ω t)| over valid samples
+    double phimax;     // mode 1: |ϕ| up to which fl(x+ϕ) stays in the binade of every x
 };
+// ϕ margin of the quantised mode: NEWUOA starts at |ϕ| ≤ π with rhobeg 1 and after a π-flip
+// re-fit may step past ±π by its trust radius, so the binade test covers |ϕ| ≤ 2π + 2; an
+// evaluation beyond it sends the series to the exact evaluator (HarmChi2::eval).
+constexpr double PHI_MARGIN = 2.0 * 3.141592653589793 + 2.0;
 
 struct Problem {
     long long N, P;
@@ -248,7 +253,8 @@ __global__ __launch_bounds__(1024) void k_prepare(Problem pb, Info *info) {
         // in one binade [2^e, 2^(e+1)), fl(x+ϕ) = x + round(ϕ to a multiple of ulp 2^(e-52)):
         // the harmonic path reproduces it by quantising ϕ.  Small |x| (< 2^16): the per-sample
         // rounding noise is below 2e-11 rad and uncorrelated, harmonic without quantisation.
-        const double lo = xmn - PI_F64, hi = xmx + PI_F64;
+        const double lo = xmn - PHI_MARGIN, hi = xmx + PHI_MARGIN;
+        in.phimax = PHI_MARGIN;
         int elo, ehi;
         frexp(lo > 0 ? lo : 0.0, &elo);
         frexp(hi, &ehi);
@@ -489,11 +495,11 @@ __global__ __launch_bounds__(64) void k_moments(Problem pb, const double *__rest
                 dv = d_at(pb, pp * pb.ldd + ss);
                 const c64 z = fc_at(pb, (long long)gld(pb.fcop + pp) * pb.ldfc + ss);
                 const double r2 = z.re * z.re + z.im * z.im;
-                if (r2 > 0.0) {
+                if (r2 == 0.0) {
+                    pv = {1.0, 0.0};  // angle(0) = 0 (a NaN sample stays NaN)
+                } else {
                     const double inv = 1.0 / sqrt(r2);
                     pv = {z.re * inv, z.im * inv};
-                } else {
-                    pv = {1.0, 0.0};  // angle(0) = 0
                 }
             }
             dtile[ls][prow] = dv;
@@ -542,30 +548,24 @@ __global__ __launch_bounds__(64) void k_moments(Problem pb, const double *__rest
 }
 
 // ---------------------------------------------------------------------------------------
-// k_moments_mfma: the same moments as a dense fp64 contraction on the matrix cores.
-//   Out[row][col] = Σ_s A[row][s] · B[s][col],  row = (series, re/im of q), col = (harmonic n,
-//   cos/sin), s = sample.  v_mfma_f64_16x16x4_f64: A = 16 rows (8 series) × 4 samples, B = 4
-//   samples × 16 cols (8 harmonics); each wave owns 32 series (4 M-tiles) × 24 harmonics (3
-//   N-tiles) = 12 accumulators (48 f64 per lane).
-// Workgroup = 4 waves = 128 series; tile = MM_TS samples.  Software pipeline per tile:
-//   (1) from registers loaded one tile ahead: normalise the 4 FC samples of the thread's groups,
-//       form q = w p̄ d for its 16 (series, sample) elements → LDS [sample][series] (padded row +
-//       xor swizzle: conflict-free transposed writes and fragment reads); cos/sin rows → LDS;
-//   (2) issue the global loads of the next tile (coalesced 512-B row segments);
-//   (3) barrier; MFMA phase (MM_TS/4 K-steps × 12 MFMAs) while those loads fly; F0 = Σq and
-//       Σ|q|² accumulate on the VALU from the A fragments; (4) barrier.
+// MFMA moment pass (k_moments_ws below): the moments as a dense fp64 contraction on the matrix
+//   cores.  Out[row][col] = Σ_s A[row][s] · B[s][col],  row = (series, re/im of q), col =
+//   (harmonic n, cos/sin), s = sample.  v_mfma_f64_16x16x4_f64: A = 16 rows (8 series) × 4
+//   samples, B = 4 samples × 16 cols (8 harmonics).
 // Fragment maps (gfx950, cdna_hip_programming.md §3): A lane l ↔ A[l&15][l>>4];
 // B lane l ↔ B[l>>4][l&15]; D lane l, reg r ↔ D[(l>>4)+4r][l&15].
 typedef double v4d __attribute__((ext_vector_type(4)));
 
 // z/|z| for the harmonic moments (angle(0) = 0 → 1): v_rsq_f64 + one Newton step, ~1 ulp
 // — the harmonic path's tolerance is set by its truncation test, not by correct rounding.
+// Only z = 0 maps to 1: a NaN sample keeps a NaN phasor, as exp(im·angle(NaN)) does in the
+// reference (src/Modulation.jl:388), so its series end with a NaN χ² (status NAN).
 __device__ __forceinline__ c64 unit_phasor(c64 z) {
     const double r2 = fma(z.re, z.re, z.im * z.im);
     double y = __builtin_amdgcn_rsq(r2);
     y = y * fma(-0.5 * r2, y * y, 1.5);
     c64 ph = {z.re * y, z.im * y};
-    if (!(r2 > 0.0)) ph = {1.0, 0.0};
+    if (r2 == 0.0) ph = {1.0, 0.0};
     return ph;
 }
 
@@ -596,197 +596,17 @@ __device__ __forceinline__ TS buf_ld(__amdgpu_buffer_rsrc_t rs, int voff) {
         return __builtin_bit_cast(TS, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, 0, POL));
 }
 
-template <bool FAINT, class TS = c64>
-__global__ __launch_bounds__(256, 2) void k_moments_mfma(Problem pb, const double *__restrict__ tab,
-                                                         const double *__restrict__ fstat,
-                                                         long long chunk_len,
-                                                         double *__restrict__ part) {
-    __shared__ c64 qs[MM_TS * MM_ROW];
-    __shared__ __attribute__((aligned(16))) double ts[MM_TS * 2 * KH];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const long long p0 = (long long)blockIdx.x * MM_PIX;
-    const long long s_begin = (long long)blockIdx.y * chunk_len;
-    long long s_end = s_begin + chunk_len;
-    if (s_end > pb.N) s_end = pb.N;
-
-    // ---- staging role: sample ss of the tile; FC groups gq + 8 r (r = 0..3), their 4 series
-    __shared__ int fcl[MM_PIX];             // FC column of each series of the workgroup
-    __shared__ double wml[FAINT ? MM_PIX * 5 : 1];  // faint: w·m per series and state
-    const int ss = tid & 31, gq = tid >> 5;
-    if (tid < MM_PIX) {
-        const long long p = p0 + tid;
-        fcl[tid] = p < pb.P ? pb.fcop[p] : 0;
-        if (FAINT) {
-#pragma unroll
-            for (int q = 0; q < 5; ++q)
-                wml[tid * 5 + q] = p < pb.P ? fstat[p * 16 + 5 + q] * fstat[p * 16 + q] : 0.0;
-        }
-    }
-    __syncthreads();
-    int gcol[4];        // group's FC column (series 4g)
-    unsigned ownmask = 0;  // bit 4r+j: series has its own FC column (general fc_of_pixel)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int g = gq + 8 * r;
-        gcol[r] = fcl[4 * g];
-#pragma unroll
-        for (int j = 1; j < 4; ++j)
-            if (fcl[4 * g + j] != gcol[r]) ownmask |= 1u << (4 * r + j);
-    }
-    const long long ldd = pb.ldd, ldfc = pb.ldfc;
-    // series rows of this workgroup through one buffer descriptor (wave-uniform base and size,
-    // T8/T20): per-thread voffset + per-load scalar soffset, out-of-range rows read as 0.
-    const long long nrows = (pb.P - p0) < MM_PIX ? (pb.P - p0) : MM_PIX;
-    constexpr int ES = (int)sizeof(TS);
-    const unsigned dbytes = __builtin_amdgcn_readfirstlane((unsigned)(nrows * ldd * ES));
-    const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
-        uniform_ptr(d_base<TS>(pb) + p0 * ldd), (short)0, (int)dbytes, 0x00020000);
-    const int dvoff = (int)((4 * gq * ldd + ss) * ES);
-    const int ldd16 = __builtin_amdgcn_readfirstlane((int)(ldd * ES));
-    const TS *fcp[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) fcp[r] = fc_base<TS>(pb) + (long long)gcol[r] * ldfc + ss;
-    // ---- MFMA role
-    const int fi = lane & 15, fk = lane >> 4, comp = fi & 1, ppair = fi >> 1;
-    v4d acc[4][3];
-    double f0[4] = {0, 0, 0, 0}, q2[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 3; ++n) acc[m][n] = (v4d){0.0, 0.0, 0.0, 0.0};
-
-    // ---- prefetch registers (one tile ahead)
-    TS rd[4][4], rf[4];
-    double2 rt[3];
-    auto issue = [&](long long s0) {
-        const bool in = s0 + ss < s_end;
-        const int s016 = (int)(s0 * ES);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            rf[r] = in ? fcp[r][s0] : TS{0, 0};
-#pragma unroll
-            for (int j = 0; j < 4; ++j)  // every offset part in voffset: the range check ignores soffset
-                rd[r][j] = buf_ld<TS>(drs, dvoff + (32 * r + j) * ldd16 + s016);
-        }
-        // cos/sin rows: MM_TS × 48 doubles = 768 double2, 3 per thread
-        const double2 *trow = (const double2 *)tab + s0 * KH;
-#pragma unroll
-        for (int u = 0; u < 3; ++u) {
-            const int e = tid + 256 * u;  // double2 index in the tile
-            rt[u] = s0 + e / KH < s_end ? trow[e] : double2{0.0, 0.0};
-        }
-    };
-    if (s_begin < s_end) issue(s_begin);
-    for (long long s0 = s_begin; s0 < s_end; s0 += MM_TS) {
-        // (1) stage tile s0 from registers
-        const long long s = s0 + ss;
-        int st = 0;
-        const bool sok = (s < s_end) && sample_valid(pb, s, st);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const c64 z = widen(rf[r]);
-            const double r2 = z.re * z.re + z.im * z.im;
-            c64 ph = {1.0, 0.0};  // angle(0) = 0
-            if (r2 > 0.0) {
-                const double inv = 1.0 / sqrt(r2);
-                ph = {z.re * inv, z.im * inv};
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int pl = 4 * (gq + 8 * r) + j;  // series within the workgroup
-                c64 pj = ph;
-                if (ownmask & (1u << (4 * r + j))) {  // general fc_of_pixel: own FC column
-                    const c64 zz = fc_at(pb, (long long)fcl[pl] * ldfc + s);
-                    const double rr = zz.re * zz.re + zz.im * zz.im;
-                    pj = {1.0, 0.0};
-                    if (rr > 0.0) {
-                        const double iv = 1.0 / sqrt(rr);
-                        pj = {zz.re * iv, zz.im * iv};
-                    }
-                }
-                const c64 dv = widen(rd[r][j]);
-                c64 q;
-                q.re = fma(pj.re, dv.re, pj.im * dv.im);
-                q.im = fma(pj.re, dv.im, -(pj.im * dv.re));
-                if (FAINT) {
-                    const double f = wml[pl * 5 + st + 1];
-                    q.re *= f;
-                    q.im *= f;
-                }
-                const bool keep = sok && (p0 + pl < pb.P);  // rows beyond P read as 0 anyway
-                q.re = keep ? q.re : 0.0;
-                q.im = keep ? q.im : 0.0;
-                qs[mm_phys(4 * (gq + 8 * r) + j, ss)] = q;
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 3; ++u) ((double2 *)ts)[tid + 256 * u] = rt[u];
-        // (2) next tile's loads fly during the MFMA phase
-        if (s0 + MM_TS < s_end) issue(s0 + MM_TS);
-        __syncthreads();
-        // (3) MFMA phase (unroll 2: bounds the LDS fragments the scheduler keeps in flight)
-#pragma unroll 2
-        for (int ks = 0; ks < MM_TS / 4; ++ks) {
-            const int k = ks * 4 + fk;
-            double a[4], b[3];
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const c64 q = qs[mm_phys(wave * 32 + m * 8 + ppair, k)];
-                a[m] = comp ? q.im : q.re;
-                f0[m] += a[m];
-                q2[m] = fma(a[m], a[m], q2[m]);
-            }
-#pragma unroll
-            for (int n = 0; n < 3; ++n) b[n] = ts[k * 2 * KH + n * 16 + fi];
-#pragma unroll
-            for (int m = 0; m < 4; ++m)
-#pragma unroll
-                for (int n = 0; n < 3; ++n)
-                    acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b[n], acc[m][n], 0, 0, 0);
-        }
-        __syncthreads();
-    }
-    // ---- epilogue: harmonic moments from the accumulators
-    double *base = part + (long long)blockIdx.y * NMOM * pb.P;
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 3; ++n)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = fk + 4 * r, col = fi;
-                const long long pix = p0 + wave * 32 + m * 8 + (row >> 1);
-                const int cq = row & 1, trig = col & 1;
-                const int h = n * 8 + (col >> 1);  // harmonic index 0..K-1 (n = h + 1)
-                const int code = cq == 0 ? (trig == 0 ? 0 : 3) : (trig == 1 ? 1 : 2);
-                if (pix < pb.P) base[(long long)(3 + 4 * h + code) * pb.P + pix] = acc[m][n][r];
-            }
-    // ---- F0 (re/im lanes) and Σ|q|² (= Σ w²|p|²|d|²; Σ|d|² when w = |p| = 1)
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        f0[m] += __shfl_xor(f0[m], 16, 64);
-        f0[m] += __shfl_xor(f0[m], 32, 64);
-        q2[m] += __shfl_xor(q2[m], 16, 64);
-        q2[m] += __shfl_xor(q2[m], 32, 64);
-        const double q2o = __shfl_xor(q2[m], 1, 64);
-        const long long pix = p0 + wave * 32 + m * 8 + ppair;
-        if (fk == 0 && pix < pb.P) {
-            base[(long long)comp * pb.P + pix] = f0[m];
-            if (comp == 0) base[2 * pb.P + pix] = q2[m] + q2o;
-        }
-    }
-}
-
 // k_moments_ws: the MFMA contraction with producer/consumer wave roles (every whole-exposure
 // series; faint ones weighted per state).
 //   Workgroup = 8 waves, one workgroup per CU (LDS 157 KB): waves 0-3 (consumers) only run the
-//   MFMA phase — the f64 fragments of k_moments_mfma for harmonics 1..16 (8 accumulators per
+//   MFMA phase — f64 fragments (maps above) for harmonics 1..16 (8 accumulators per
 //   wave) and, with MIX, split-bf16 MFMAs for harmonics 17..24 (4 f32 accumulators); waves 4-7
 //   (producers) stream d / FC / cos-sin rows two tiles ahead in registers, form q = p̄ d and
 //   write the next tile into the other half of a double-buffered LDS tile.  One barrier per
 //   tile: consumers on buffer i&1 while producers fill buffer (i+1)&1, so each SIMD hosts one
 //   consumer that keeps its matrix core busy and one producer whose loads and VALU work overlap
-//   it (the single-role kernel serialises staging and MFMA behind two barriers per tile).
+//   it (a single-role kernel serialises staging and MFMA behind two barriers per tile: 61.5 vs
+//   52.6 ms on C3).
 // DBG == 6 (diagnostics only): per-role cycle split, summed over waves
 //   [0] producer stage, [1] producer issue, [2] producer barrier, [3] consumer MFMA phase,
 //   [4] consumer barrier
@@ -835,10 +655,16 @@ __device__ __forceinline__ void split_bf16x2(float f0, float f1, unsigned &h, un
 // compute_mean_var_power (fstat, src/Faint.jl:89-100; src/Modulation.jl:392-396); samples
 // outside the valid mask (TRANSIENT, or not HIGH/NORMAL with onlyhigh: src/Modulation.jl:373-382)
 // contribute 0.  The state byte of each sample is loaded with the tile.
+// Sample units: the samples are cut into fixed units of unit_len samples (a function of N only,
+// plan() in gpd_engine.hip) and the consumers write one set of partial moments per unit,
+// part[unit][moment][series], restarting their accumulators at each unit boundary; a workgroup
+// streams chunk_len = (units per workgroup) × unit_len samples.  The units per workgroup follow
+// the grid fill (a function of P), but every moment is the same sum in the same order for any
+// of them — a series' moments, and so its fit, do not depend on the batch or shard it is in.
 template <int DBG = 0, bool UNIT = false, class TS = c64, int POL = 0, bool MIX = true,
           bool FAINT = false>
 __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double *__restrict__ tab,
-                                                       long long chunk_len,
+                                                       long long chunk_len, long long unit_len,
                                                        double *__restrict__ part,
                                                        const double *__restrict__ fstat = nullptr) {
     __shared__ c64 qs[2][MM_TS * MM_ROW];
@@ -1070,6 +896,50 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
         for (int n = 0; n < NC; ++n) acc[m][n] = (v4d){0.0, 0.0, 0.0, 0.0};
         acc32[m] = (v4f){0.0f, 0.0f, 0.0f, 0.0f};
     }
+    // partial moments of one sample unit: write part[u], restart the accumulators
+    const int tpu = (int)(unit_len / MM_TS);  // tiles per unit (units are whole tiles)
+    auto put = [&](double *base, int m, int n, int row, int col, double v) {
+        // moment index of output element (row, col) of column tile n: series row >> 1, re/im
+        // of q row & 1, harmonic 8n + (col >> 1) + 1, cos/sin col & 1 → (A, B, C, D) code
+        const long long pix = p0 + wave * 32 + m * 8 + (row >> 1);
+        const int cq = row & 1, trig = col & 1;
+        const int h = n * 8 + (col >> 1);
+        const int code = cq == 0 ? (trig == 0 ? 0 : 3) : (trig == 1 ? 1 : 2);
+        if (pix < pb.P) base[(long long)(3 + 4 * h + code) * pb.P + pix] = v;
+    };
+    auto flush = [&](long long u) {
+        double *base = part + u * NMOM * pb.P;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+#pragma unroll
+            for (int n = 0; n < NC; ++n)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) put(base, m, n, fk + 4 * r, fi, acc[m][n][r]);  // f64 D map
+            if constexpr (MIX) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) put(base, m, 2, 4 * fk + r, fi, (double)acc32[m][r]);  // bf16 D map
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            double f = f0[m], q = q2[m];
+            f += __shfl_xor(f, 16, 64);
+            f += __shfl_xor(f, 32, 64);
+            q += __shfl_xor(q, 16, 64);
+            q += __shfl_xor(q, 32, 64);
+            const double qo = __shfl_xor(q, 1, 64);
+            const long long pix = p0 + wave * 32 + m * 8 + ppair;
+            if (fk == 0 && pix < pb.P) {
+                base[(long long)comp * pb.P + pix] = f;
+                if (comp == 0) base[2 * pb.P + pix] = q + qo;
+            }
+            f0[m] = q2[m] = 0.0;
+#pragma unroll
+            for (int n = 0; n < NC; ++n) acc[m][n] = (v4d){0.0, 0.0, 0.0, 0.0};
+            acc32[m] = (v4f){0.0f, 0.0f, 0.0f, 0.0f};
+        }
+    };
+    const long long u_first = s_begin / unit_len;
     __syncthreads();  // tile 0 staged
     unsigned long long cmf = 0, cbar = 0;  // DBG == 6 only
     // fragments of K-step ks+1 are read from LDS while the MFMAs of K-step ks run
@@ -1152,40 +1022,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
         }
         __syncthreads();
         if constexpr (DBG == 6) cbar += __builtin_amdgcn_s_memtime() - c1;
-    }
-    double *base = part + (long long)blockIdx.y * NMOM * pb.P;
-    // moment index of output element (row, col) of column tile n: series row >> 1, re/im of q
-    // row & 1, harmonic 8n + (col >> 1) + 1, cos/sin col & 1 → (A, B, C, D) code
-    auto put = [&](int m, int n, int row, int col, double v) {
-        const long long pix = p0 + wave * 32 + m * 8 + (row >> 1);
-        const int cq = row & 1, trig = col & 1;
-        const int h = n * 8 + (col >> 1);
-        const int code = cq == 0 ? (trig == 0 ? 0 : 3) : (trig == 1 ? 1 : 2);
-        if (pix < pb.P) base[(long long)(3 + 4 * h + code) * pb.P + pix] = v;
-    };
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-#pragma unroll
-        for (int n = 0; n < NC; ++n)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) put(m, n, fk + 4 * r, fi, acc[m][n][r]);  // f64 D map
-        if constexpr (MIX) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) put(m, 2, 4 * fk + r, fi, (double)acc32[m][r]);  // bf16 D map
-        }
-    }
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        f0[m] += __shfl_xor(f0[m], 16, 64);
-        f0[m] += __shfl_xor(f0[m], 32, 64);
-        q2[m] += __shfl_xor(q2[m], 16, 64);
-        q2[m] += __shfl_xor(q2[m], 32, 64);
-        const double q2o = __shfl_xor(q2[m], 1, 64);
-        const long long pix = p0 + wave * 32 + m * 8 + ppair;
-        if (fk == 0 && pix < pb.P) {
-            base[(long long)comp * pb.P + pix] = f0[m];
-            if (comp == 0) base[2 * pb.P + pix] = q2[m] + q2o;
-        }
+        if ((i + 1) % tpu == 0 || i + 1 == ntiles) flush(u_first + i / tpu);  // uniform
     }
     if constexpr (DBG == 6) {
         if (lane == 0) {
@@ -1311,7 +1148,7 @@ __global__ __launch_bounds__(256) void k_moments_win(Problem pb, const double *_
 struct HarmChi2 {
     const double *__restrict__ mom;
     long long P, k;
-    double nvalid, W2, DEN, tailref, qbase;
+    double nvalid, W2, DEN, tailref, qbase, phimax;
     double a_re, a_im;
     int nfev;
     bool fallback;
@@ -1388,7 +1225,13 @@ struct HarmChi2 {
             fallback = true;  // truncated expansion not exact here → exact evaluator
             return 0.0;
         }
-        if (qbase != 0.0) phi = (qbase + phi) - qbase;  // θ = fl(x + ϕ) = x + ϕ_q (one binade)
+        if (qbase != 0.0) {
+            if (!(fabs(phi) <= phimax)) {  // fl(x + ϕ) may leave the binade: exact evaluator
+                fallback = true;
+                return 0.0;
+            }
+            phi = (qbase + phi) - qbase;  // θ = fl(x + ϕ) = x + ϕ_q (one binade)
+        }
         double sph, cph;
         jl_sincos(phi, &sph, &cph);
         double Sr, Si;  // S = Σ w m̄ d
@@ -1468,6 +1311,7 @@ __global__ __launch_bounds__(64) void k_fit_harmonic(Problem pb, const Info *__r
     // tail bound: |Σ_{|n|>K} J_n e^{-jnϕ} F_n| ≤ 2|J_{K+1}| sqrt(N Σ|q|²) ≤ 1e-16 sqrt(W2·DEN)
     f.tailref = 0.5e-16 * sqrt(f.W2 * f.DEN) / sqrt(f.nvalid * Q2);
     f.qbase = in.mode == 1 ? in.qbase : 0.0;
+    f.phimax = in.phimax;
     f.a_re = f.a_im = 0.0;
     f.nfev = 0;
     f.fallback = false;
@@ -1987,6 +1831,7 @@ __global__ __launch_bounds__(64) void k_chi2_harmonic(Problem pb, const Info *__
     f.DEN = aux[4 * k + 1];
     f.tailref = 0.5e-16 * sqrt(f.W2 * f.DEN) / sqrt(f.nvalid * aux[4 * k + 2]);
     f.qbase = in.mode == 1 ? in.qbase : 0.0;
+    f.phimax = in.phimax;
     f.a_re = f.a_im = 0.0;
     f.nfev = 0;
     f.fallback = in.mode == 2;

@@ -20,6 +20,11 @@ def shard_range(n_total: int, world: int, rank: int, align: int = GROUP) -> tupl
     return min(g0 * align, n_total), min(g1 * align, n_total)
 
 
+def shard_counts(n_total: int, world: int, align: int = GROUP) -> list[int]:
+    """Series per rank under shard_range."""
+    return [e - b for b, e in (shard_range(n_total, world, r, align) for r in range(world))]
+
+
 def weak_offset(per_rank: int, rank: int) -> int:
     """Global index of rank's first series when every rank owns `per_rank` series (weak scaling)."""
     if per_rank % GROUP:
@@ -27,17 +32,31 @@ def weak_offset(per_rank: int, rank: int) -> int:
     return rank * per_rank
 
 
-def gather_records(local, world: int, rank: int, dst: int = 0, group=None):
-    """Gather equal-sized record tensors (uint8, n×64) to `dst`; returns the concatenation on
-    dst, None elsewhere.  Works for CUDA tensors under nccl (RCCL) and CPU tensors under gloo."""
+def gather_records(local, world: int, rank: int, dst: int = 0, group=None, counts=None):
+    """Gather record tensors (uint8, n×64) to `dst`; returns the concatenation in rank order on
+    dst, None elsewhere.  `counts` (records per rank, e.g. from shard_range) allows unequal
+    shards: every rank sends max(counts) rows (one collective, the padding trimmed on dst).
+    Works for CUDA tensors under nccl (RCCL) and CPU tensors under gloo."""
     import torch
     import torch.distributed as dist
 
     if world == 1:
         return local
-    bufs = [torch.empty_like(local) for _ in range(world)] if rank == dst else None
-    dist.gather(local, gather_list=bufs, dst=dst, group=group)
-    return torch.cat(bufs) if rank == dst else None
+    n = local.shape[0]
+    if counts is None:
+        counts = [n] * world
+    if counts[rank] != n:
+        raise ValueError(f"rank {rank}: {n} records, counts says {counts[rank]}")
+    m = max(counts)
+    send = local
+    if n < m:
+        send = torch.zeros((m,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        send[:n] = local
+    bufs = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
+    dist.gather(send.contiguous(), gather_list=bufs, dst=dst, group=group)
+    if rank != dst:
+        return None
+    return torch.cat([b[:c] for b, c in zip(bufs, counts)])
 
 
 def records_to_numpy(t, dtype) -> np.ndarray:

@@ -34,23 +34,45 @@ def test_bench_json_contract():
     assert out["fits"]["nan"] == 0
 
 
-def test_bench_two_ranks_rehearsal():
-    """The multi-rank path of bench.py (torch.distributed.run, barrier, max-over-ranks time,
-    gather of the records to rank 0, one JSON line from rank 0) with two ranks sharing cuda:0
-    under gloo (GPD_DIST_BACKEND) — the scaling runs use RCCL with one rank per GPU."""
+def _run_bench(nproc, extra, tmp, tag):
     import socket
-    with socket.socket() as so:  # a free rendezvous port on this box
-        so.bind(("127.0.0.1", 0))
-        port = so.getsockname()[1]
+    dump = os.path.join(tmp, f"rec_{tag}.npy")
+    args = [os.path.join(ROOT, "bench.py"), "--pixels", "520", "--samples", "4096", "--steps", "2",
+            "--warmup", "1", "--no-cpu", "--no-f64", "--dump-records", dump, *extra]
+    if nproc == 1:
+        cmd = [sys.executable, *args]
+    else:
+        with socket.socket() as so:  # a free rendezvous port on this box
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+               str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(port), *args,
+               "--gpus", str(nproc)]
     env = dict(os.environ, GPD_DIST_BACKEND="gloo")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
-                        "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2",
-                        "--pixels", "256", "--samples", "4096", "--steps", "2", "--warmup", "1",
-                        "--no-cpu"], capture_output=True, text=True, timeout=110, cwd=ROOT, env=env)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
-    out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["config"]["total_series"] == 512
-    assert out["scaling"] == "weak" and out["value"] > 0
+    import numpy as np
+    return json.loads(lines[0]), np.load(dump)
+
+
+@pytest.mark.parametrize("nproc", [2, 3])
+def test_bench_multi_rank_strong_scaling_bitwise(tmp_path, nproc):
+    """The multi-rank path of bench.py (torch.distributed.run, barrier, max-over-ranks time,
+    gather of the records to rank 0, one JSON line from rank 0) with `nproc` ranks sharing
+    cuda:0 under gloo (GPD_DIST_BACKEND) — the scaling runs use RCCL with one rank per GPU.
+    Strong scaling (BASELINE C4): the one batch of 520 series is split into whole-FC-group
+    shards (3 ranks: 43/43/44 groups, unequal), and the records gathered on rank 0 are the
+    1-rank run's bit for bit."""
+    one, r1 = _run_bench(1, [], str(tmp_path), "1")
+    out, rn = _run_bench(nproc, [], str(tmp_path), str(nproc))
+    assert out["n_gpus"] == nproc and out["config"]["total_series"] == 520
+    assert out["scaling"] == "strong" and out["value"] > 0
+    assert one["config"]["total_series"] == 520 and len(r1) == 520 and len(rn) == 520
+    assert r1.tobytes() == rn.tobytes(), "sharded records differ from the 1-rank run"
+
+
+def test_bench_weak_scaling_label(tmp_path):
+    out, rn = _run_bench(2, ["--scaling", "weak"], str(tmp_path), "w")
+    assert out["scaling"] == "weak" and out["config"]["total_series"] == 1040 and len(rn) == 1040

@@ -1,0 +1,80 @@
+"""Sharding is invisible in the results (BASELINE C4).
+
+Series are independent (src/Modulation.jl:387-389), so a batch split over devices must give the
+1-device records bit for bit.  The harmonic moments are sums over fixed sample units (a function
+of N only), so neither the shard a series lands in nor the moment grid's fill (units per
+workgroup, GPD_UPW) changes them.  GPD_FAKE_GPUS=1 keeps n_gpus shards on a one-GPU box (shard g
+on device g % ndev): the library's multi-device split — series or window ranges, per-shard FC
+column subsets, record and output offsets — runs here exactly as on an 8-GPU node."""
+import numpy as np
+import pytest
+
+import synth
+from test_gpu_parity import faint_states
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(a, b):
+    ra = a.view(np.uint8).reshape(len(a), -1)
+    rb = b.view(np.uint8).reshape(len(b), -1)
+    diff = int((ra != rb).any(axis=1).sum())
+    assert diff == 0, f"{diff}/{len(a)} records differ"
+
+
+@pytest.mark.parametrize("method", ["auto", "exact"])
+@pytest.mark.parametrize("faint", [False, True])
+def test_fit_batch_shards_bit_identical(gpu, monkeypatch, method, faint):
+    monkeypatch.setenv("GPD_FAKE_GPUS", "1")
+    N, P = 5003, 70  # ragged: P not a multiple of 4 or of the shard count
+    B = synth.make_batch(N, P, seed=61)
+    st = faint_states(N, seed=3) if faint else None
+    args = (B["t"], B["d"], B["fc"], B["fc_of_pixel"])
+    ref, ref_out = gpu.fit_batch(*args, state=st, method=method, want_output=True)
+    for g in (2, 3, 8):
+        got, out = gpu.fit_batch(*args, state=st, method=method, want_output=True, n_gpus=g)
+        _same(got, ref)
+        np.testing.assert_array_equal(out, ref_out)
+
+
+def test_fit_batch_shards_offsets_harmonic(gpu, monkeypatch):
+    """Harmonic fitoffsets: the shards' FC-column subsets carry their own G_n moments."""
+    monkeypatch.setenv("GPD_FAKE_GPUS", "1")
+    B = synth.make_batch(4000, 48, seed=62, offsets=True)
+    args = (B["t"], B["d"], B["fc"], B["fc_of_pixel"])
+    ref = gpu.fit_batch(*args, fitoffsets=True, method="harmonic")
+    for g in (2, 5):
+        _same(gpu.fit_batch(*args, fitoffsets=True, method="harmonic", n_gpus=g), ref)
+
+
+@pytest.mark.parametrize("window", [1500, 200])
+def test_fit_windows_shards_bit_identical(gpu, monkeypatch, window):
+    """Windows are split over devices (not diodes): a ragged last window, window-major record
+    offsets and the demodulated output slices must land where the 1-device call puts them."""
+    monkeypatch.setenv("GPD_FAKE_GPUS", "1")
+    N = 12_345
+    B = synth.make_batch(N, 32, seed=63)
+    fop = np.arange(32) // 4
+    ref, ref_out = gpu.fit_windows(B["t"], B["d"], B["fc"], fop, window, want_output=True)
+    for g in (2, 3):
+        got, out = gpu.fit_windows(B["t"], B["d"], B["fc"], fop, window, want_output=True,
+                                   n_gpus=g)
+        _same(got, ref)
+        np.testing.assert_array_equal(out, ref_out)
+
+
+def test_records_independent_of_batch_and_grid(gpu, monkeypatch):
+    """A series' harmonic record does not depend on the other series of its batch (a sub-batch
+    starting mid-workgroup) nor on the moment grid (units per workgroup 1, 2, 3, 7)."""
+    N, P = 20_000, 96
+    B = synth.make_batch(N, P, seed=64)
+    args = (B["t"], B["d"], B["fc"], B["fc_of_pixel"])
+    ref = gpu.fit_batch(*args, method="harmonic")
+    sub = slice(36, 84)
+    fo = B["fc_of_pixel"][sub]
+    got = gpu.fit_batch(B["t"], B["d"][sub], B["fc"][fo.min():fo.max() + 1], fo - fo.min(),
+                        method="harmonic")
+    _same(got, ref[sub])
+    for upw in ("1", "2", "3", "7"):
+        monkeypatch.setenv("GPD_UPW", upw)
+        _same(gpu.fit_batch(*args, method="harmonic"), ref)
