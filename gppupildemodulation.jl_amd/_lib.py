@@ -11,8 +11,9 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# GPD_LIB=diag: the diagnostics build (moment-kernel timing variants, build.py --diag)
-LIB_PATH = os.path.join(HERE, "libgpdemod_diag.so" if os.environ.get("GPD_LIB") == "diag"
+# GPD_LIB=<name>: load libgpdemod_<name>.so instead — "diag" is the diagnostics build
+# (moment-kernel timing variants, build.py --diag); other names are A/B builds of another revision
+LIB_PATH = os.path.join(HERE, f"libgpdemod_{os.environ['GPD_LIB']}.so" if os.environ.get("GPD_LIB")
                         else "libgpdemod.so")
 
 GPD_ABI_VERSION = 1
