@@ -17,7 +17,8 @@ from ._lib import (GPD_FIT_OFFSETS, GPD_METHOD_EXACT, GPD_METHOD_HARMONIC, GPD_O
                    GPD_ST_REFIT, PARAM_DTYPE, GpdError, libm_eval, load, timings)
 from .demod import (DAY_TO_SEC, M_2PI, MJD_1970_1_1, Diode, FaintStates, MetState,
                     ModulationNoOffsets, ModulationWithOffsets, Side, buildfaintparameters,
-                    buildstates, chi2_batch, demodulate_windows, metrology_times, processmetrology,
+                    buildstates, chi2_batch, compute_mean_var_power, demodulate_windows,
+                    mean_var_power_batch, metrology_times, processmetrology,
                     demodulateall, fc_column_of, fit_batch, fit_windows, idx, process_volt,
                     read_stefan_file, window_length, window_tables)
 
@@ -29,4 +30,5 @@ __all__ = [
     "demodulate_windows", "demodulateall", "fc_column_of", "fit_batch", "fit_windows", "idx",
     "window_length", "window_tables", "process_volt", "read_stefan_file", "DAY_TO_SEC",
     "MJD_1970_1_1", "buildfaintparameters", "metrology_times", "processmetrology",
+    "compute_mean_var_power", "mean_var_power_batch",
 ]

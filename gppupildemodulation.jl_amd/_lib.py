@@ -46,7 +46,8 @@ EXPORTS = ("gpd_version", "gpd_strerror", "gpd_device_count", "gpd_fit_batch",
            "gpd_fit_batch_dev", "gpd_chi2_batch", "gpd_chi2_batch_dev", "gpd_buildstates",
            "gpd_synth_fill_dev", "gpd_last_timings", "gpd_fit_windows", "gpd_fit_windows_dev",
            "gpd_process_volt", "gpd_fit_batch_c32", "gpd_fit_batch_c32_dev", "gpd_fit_windows_c32",
-           "gpd_fit_windows_c32_dev", "gpd_buildstates_dev", "gpd_release", "gpd_libm_eval")
+           "gpd_fit_windows_c32_dev", "gpd_buildstates_dev", "gpd_release", "gpd_libm_eval",
+           "gpd_mean_var_power")
 
 
 class GpdError(RuntimeError):
@@ -109,6 +110,9 @@ def load():
     L.gpd_synth_fill_dev.restype = ctypes.c_int
     L.gpd_synth_fill_dev.argtypes = [I64, I64, I64, ctypes.c_uint64, D, D, D, ctypes.c_int, D, V, V,
                                      I64, V, I64, V, V, ctypes.c_int, V]
+    L.gpd_mean_var_power.restype = ctypes.c_int
+    L.gpd_mean_var_power.argtypes = [I64, I64, V, I64, V, U32, V, ctypes.c_int, ctypes.c_char_p,
+                                     ctypes.c_size_t]
     L.gpd_libm_eval.restype = ctypes.c_int
     L.gpd_libm_eval.argtypes = [ctypes.c_int, I64, V, V, V, ctypes.c_int]
     L.gpd_last_timings.restype = ctypes.c_int
@@ -135,7 +139,7 @@ def check(rc: int, errbuf=None):
         raise GpdError(rc, f"{L.gpd_strerror(rc).decode()}: {msg}")
 
 
-LIBM_FN = {"sin": 0, "cos": 1, "sincos": 2, "atan": 3, "atan2": 4, "hypot": 5, "rem_pio2": 6}
+LIBM_FN = {"sin": 0, "cos": 1, "sincos": 2, "atan": 3, "atan2": 4, "hypot": 5, "rem_pio2": 6, "hypot_nb": 7}
 
 
 def libm_eval(fn: str, x, y=None, device: int = 0):

@@ -13,6 +13,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "gpd_jlmath.h"  // Julia Base's sin/cos/sincos/atan/hypot, shared with the oracle
 
 namespace gpd {

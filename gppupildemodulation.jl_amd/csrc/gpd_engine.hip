@@ -89,12 +89,13 @@ size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
 struct Layout {
     size_t info, tab, part, mom, aux, fstat, raw, list, phbuf, partG, momG, auxG, fcid, d0, mcache,
-        xtot, xcnt, total;
+        xtot, xcnt, fsx, fsc, total;
     long long mstride;  // model-cache elements per exact-path workgroup (0: no cache)
     int nch;            // sample chunks of the moment grid (grid.y)
     long long chunk;    // samples per chunk (a whole number of units)
     int units;          // sample units = partial-moment sets
     long long unit_len; // samples per unit
+    bool fs8;           // faint statistics by k_faint_stats8
 };
 
 Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic, bool phbuf,
@@ -167,8 +168,29 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     // arrival counters (zeroed per launch)
     L.xtot = take(exact_g > 1 ? (size_t)P * 2 * CR_BLOCKS * CR_NV * sizeof(double) : 0);
     L.xcnt = take(exact_g > 1 ? (size_t)(P + 3) / 4 * 16 : 0);
+    // one-pass faint statistics (k_faint_stats8): per-series block totals (2 × 8 × 16 doubles)
+    // and arrival counters
+    L.fs8 = faint && !windowed && N <= (long long)FS_MAXM * 2048 && P * FS_G < (1LL << 31);
+    L.fsx = take(L.fs8 ? (size_t)P * 2 * FS_G * FS_NV * sizeof(double) : 0);
+    L.fsc = take(L.fs8 ? (size_t)P * sizeof(unsigned) : 0);
     L.total = off;
     return L;
+}
+
+// k_faint_stats8 is persistent (one workgroup per CU, 8 per series in lockstep): launched
+// cooperatively so that every workgroup is resident; grid = a multiple of 8 ≤ resident capacity
+// and ≤ 8·P.
+hipError_t launch_faint_stats8(Problem pb, double *fstat, double *fx, unsigned *fc, bool is_c32,
+                               int n_cu, hipStream_t stream) {
+    const void *fn = is_c32 ? (const void *)k_faint_stats8<c32> : (const void *)k_faint_stats8<c64>;
+    int per_cu = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0);
+    if (e != hipSuccess) return e;
+    long long grid = (long long)std::max(1, per_cu) * std::max(1, n_cu);
+    grid = std::min<long long>(grid / FS_G * FS_G, pb.P * FS_G);
+    if (grid < FS_G) grid = FS_G;
+    void *args[] = {&pb, &fstat, &fx, &fc};
+    return hipLaunchCooperativeKernel(fn, dim3((unsigned)grid), dim3(256), args, 0, stream);
 }
 
 const char *kErrStr[] = {"ok", "invalid argument", "HIP runtime error", "no HIP device",
@@ -385,7 +407,18 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     HIP_TRY(hipMemsetAsync(count, 0, sizeof(int), stream));
     mark("prepare");
     if (faint) {
-        k_faint_stats<<<(unsigned)P, 256, 0, stream>>>(pb, fstat);
+        // one HBM pass (8 workgroups per series, |d| kept in LDS) for whole-exposure series of
+        // ≤ 131072 samples; windows and longer series: the two-pass kernel (same bits);
+        // GPD_FAINT_STATS=2 forces the two-pass kernel (tests of that identity)
+        const bool fs8 = L.fs8 && !(getenv("GPD_FAINT_STATS") &&
+                                              std::string(getenv("GPD_FAINT_STATS")) == "2");
+        if (fs8) {
+            HIP_TRY(hipMemsetAsync(ws + L.fsc, 0, (size_t)P * sizeof(unsigned), stream));
+            HIP_TRY(launch_faint_stats8(pb, fstat, (double *)(ws + L.fsx),
+                                        (unsigned *)(ws + L.fsc), is_c32, cx->n_cu, stream));
+        } else {
+            k_faint_stats<<<(unsigned)P, 256, 0, stream>>>(pb, fstat);
+        }
         mark("faint_stats");
     }
     const unsigned exact_grid = (unsigned)std::min<long long>(P, 1024);
@@ -1009,7 +1042,8 @@ int gpd_process_volt(int64_t n_samples, const double *t, const float *volt, int6
 int gpd_libm_eval(int fn, int64_t n, const double *x, const double *y, double *out, int device) {
     char *errbuf = nullptr;
     size_t errlen = 0;
-    if (fn < 0 || fn > 6 || n < 0 || (n > 0 && (!x || !out)) || ((fn == 4 || fn == 5) && n > 0 && !y))
+    if (fn < 0 || fn > 7 || n < 0 || (n > 0 && (!x || !out)) ||
+        ((fn == 4 || fn == 5 || fn == 7) && n > 0 && !y))
         return GPD_E_ARG;
     const int ndev = gpd_device_count();
     if (ndev <= 0) return GPD_E_NODEV;
@@ -1040,6 +1074,79 @@ int gpd_libm_eval(int fn, int64_t n, const double *x, const double *y, double *o
     if (e == hipSuccess) e = hipMemcpy(out, dout, n * width * sizeof(double), hipMemcpyDeviceToHost);
     release();
     return e == hipSuccess ? GPD_OK : GPD_E_HIP;
+}
+
+int gpd_mean_var_power(int64_t n_samples, int64_t n_series, const gpd_c64 *d, int64_t ldd,
+                       const int8_t *state, uint32_t flags, double *out, int device, char *errbuf,
+                       size_t errlen) {
+    // compute_mean_var_power (src/Faint.jl:89-100) of whole series with demodulateall's valid
+    // mask — the statistics the fit uses (k_faint_stats8, or the two-pass kernel for long series)
+    if (n_samples < 1 || n_series < 1 || !d || !state || !out || ldd < n_samples) {
+        set_err(errbuf, errlen, "gpd_mean_var_power: invalid shapes/pointers");
+        return GPD_E_ARG;
+    }
+    const int ndev = gpd_device_count();
+    if (ndev <= 0) {
+        set_err(errbuf, errlen, "gpd_mean_var_power: no HIP device visible");
+        return GPD_E_NODEV;
+    }
+    if (device < 0 || device >= ndev) return GPD_E_ARG;
+    HIP_TRY(hipSetDevice(device));
+    const long long N = n_samples, P = n_series;
+    const bool fs8 = N <= (long long)FS_MAXM * 2048 && P * FS_G < (1LL << 31) &&
+                     !(getenv("GPD_FAINT_STATS") && std::string(getenv("GPD_FAINT_STATS")) == "2");
+    c64 *dd = nullptr;
+    int8_t *dst = nullptr;
+    double *fst = nullptr, *fx = nullptr;
+    unsigned *fc = nullptr;
+    auto release = [&]() {
+        (void)hipFree(dd);
+        (void)hipFree(dst);
+        (void)hipFree(fst);
+        (void)hipFree(fx);
+        (void)hipFree(fc);
+    };
+    if (hipMalloc(&dd, (size_t)P * N * sizeof(c64)) != hipSuccess ||
+        hipMalloc(&dst, (size_t)N) != hipSuccess ||
+        hipMalloc(&fst, (size_t)P * 16 * sizeof(double)) != hipSuccess ||
+        (fs8 && (hipMalloc(&fx, (size_t)P * 2 * FS_G * FS_NV * sizeof(double)) != hipSuccess ||
+                 hipMalloc(&fc, (size_t)P * sizeof(unsigned)) != hipSuccess))) {
+        release();
+        (void)hipGetLastError();
+        set_err(errbuf, errlen, "gpd_mean_var_power: out of device memory");
+        return GPD_E_OOM;
+    }
+    Problem pb{};
+    pb.N = N;
+    pb.P = P;
+    pb.d = dd;
+    pb.ldd = N;
+    pb.state = dst;
+    pb.flags = flags & GPD_ONLY_HIGH;
+    pb.ncol = P;
+    hipError_t e = hipMemcpy2D(dd, N * sizeof(c64), d, ldd * sizeof(gpd_c64), N * sizeof(c64), P,
+                               hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dst, state, (size_t)N, hipMemcpyHostToDevice);
+    if (e == hipSuccess && fs8) e = hipMemset(fc, 0, (size_t)P * sizeof(unsigned));
+    if (e == hipSuccess) {
+        int ncu = 0;
+        e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
+        if (e == hipSuccess && fs8)
+            e = launch_faint_stats8(pb, fst, fx, fc, false, ncu, nullptr);
+        else if (e == hipSuccess)
+            k_faint_stats<<<(unsigned)P, 256>>>(pb, fst);
+        e = hipGetLastError();
+    }
+    std::vector<double> h((size_t)P * 16);
+    if (e == hipSuccess) e = hipMemcpy(h.data(), fst, h.size() * sizeof(double), hipMemcpyDeviceToHost);
+    release();
+    if (e != hipSuccess) {
+        set_err(errbuf, errlen, "gpd_mean_var_power: %s", hipGetErrorString(e));
+        return GPD_E_HIP;
+    }
+    for (long long k = 0; k < P; ++k)
+        for (int q = 0; q < 10; ++q) out[k * 10 + q] = h[k * 16 + q];
+    return GPD_OK;
 }
 
 int gpd_synth_fill_dev(int64_t n_samples, int64_t n_pixels, int64_t pixel_offset, uint64_t seed,

@@ -465,4 +465,30 @@ JLM_FN double jl_hypot(double x, double y) {
     return h * scale;
 }
 
+/* jl_hypot without branches: every path of jl_hypot is evaluated and the result selected, so
+ * that many independent evaluations interleave (the faint statistics evaluate 16 per thread at
+ * a time).  The same operations on the same operands as the taken path of jl_hypot — the same
+ * bits for every input (tests/test_jlmath.py: special values, scaling ranges, random pairs). */
+JLM_FN double jl_hypot_nb(double x, double y) {
+    const double fx = __builtin_fabs(x), fy = __builtin_fabs(y);
+    const int inf = __builtin_isinf(fx) | __builtin_isinf(fy);
+    const int sw = fy > fx;
+    const double ax = sw ? fy : fx, ay = sw ? fx : fy;
+    const int early = ay <= ax * 0x1.6a09e667f3bcdp-27;
+    const int big = ax > 0x1.6a09e667f3bccp+511;
+    const int small = !big && (ay < 0x1p-511);
+    /* x / 2^-563 == x * 2^563 exactly (a power-of-two reciprocal): the scaled operands of both
+     * scaling branches are products */
+    const double f = big ? 0x1p-563 : (small ? 0x1p+563 : 1.0);
+    const double scale = big ? 0x1p+563 : (small ? 0x1p-563 : 1.0);
+    const double bx = ax * f, by = ay * f;
+    double h = __builtin_sqrt(jlm_fma(bx, bx, by * by));
+    const double hsquared = h * h, axsquared = bx * bx;
+    h = h - ((jlm_fma(-by, by, hsquared - axsquared) + jlm_fma(h, h, -hsquared)) -
+             jlm_fma(bx, bx, -axsquared)) /
+                (2 * h);
+    const double r = h * scale;
+    return inf ? __builtin_inf() : (early ? ax : r);
+}
+
 #endif /* GPD_JLMATH_H */

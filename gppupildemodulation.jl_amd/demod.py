@@ -136,6 +136,35 @@ def buildstates(faintstates: FaintStates, timestamp, lag: int = 0, preswitchdela
     return out
 
 
+def mean_var_power_batch(states, d, *, onlyhigh=False, device=0):
+    """Per-state faint power m and weight w of every series (rows of d) as the fit computes them
+    on the GPU (gpd_mean_var_power): two (P, 5) arrays indexed by MetState code + 1."""
+    L = load()
+    d = np.ascontiguousarray(np.atleast_2d(d), dtype=np.complex128)
+    st = np.ascontiguousarray(states, dtype=np.int8)
+    P, N = d.shape
+    if st.shape != (N,):
+        raise ValueError("states and data must have the same length")
+    out = np.empty((P, 10))
+    err = ctypes.create_string_buffer(512)
+    check(L.gpd_mean_var_power(N, P, ptr(d), N, ptr(st), GPD_ONLY_HIGH if onlyhigh else 0,
+                               ptr(out), int(device), err, len(err)), err)
+    return out[:, :5], out[:, 5:]
+
+
+def compute_mean_var_power(states, data):
+    """compute_mean_var_power(states, data) → (m, w) per sample (src/Faint.jl:89-100), for one
+    series, on the GPU.  Every sample counts (the reference function has no mask; demodulateall
+    passes it the valid samples only, src/Modulation.jl:391-395)."""
+    st = np.asarray(states, dtype=np.int8)
+    if np.any(st == MetState.TRANSIENT):
+        # TRANSIENT samples are not part of any statistic the fit uses (dropped by the valid
+        # mask before the call, src/Modulation.jl:380-382)
+        raise ValueError("compute_mean_var_power: TRANSIENT samples must be masked by the caller")
+    m5, w5 = mean_var_power_batch(st, np.asarray(data)[None, :])
+    return m5[0][st + 1], w5[0][st + 1]
+
+
 def _method_flags(method: str) -> int:
     if method == "auto":
         return 0

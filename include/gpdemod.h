@@ -252,6 +252,19 @@ int gpd_buildstates_dev(int64_t n_samples, const double *t, int64_t n1, const do
                         double postwitchdelay, int8_t *states, int device, void *stream);
 
 /*
+ * compute_mean_var_power (src/Faint.jl:89-100) as demodulateall applies it to whole series
+ * (src/Modulation.jl:373-396): per series k (column k of d, host buffers) and MetState, over the
+ * valid samples (TRANSIENT dropped; GPD_ONLY_HIGH in flags keeps HIGH ∪ NORMAL),
+ *   m = mean(abs, d[state .== s]),   w = 1 / var(abs.(d[state .== s]); mean = m)
+ * — the faint power and weight the fit uses, computed by the same kernel, bit for bit.
+ * out[10k + c] = m and out[10k + 5 + c] = w of MetState code c − 1 (c = 0 TRANSIENT … 4 HIGH;
+ * NaN for a state without samples, w NaN for a 1-sample state, as Julia's 0/0).  Synchronous.
+ */
+int gpd_mean_var_power(int64_t n_samples, int64_t n_series, const gpd_c64 *d, int64_t ldd,
+                       const int8_t *state, uint32_t flags, double *out, int device, char *errbuf,
+                       size_t errlen);
+
+/*
  * Synthetic GRAVITY-like metrology batch generated ON DEVICE (benchmarks):
  * d[k][i] = p_i(c_k + a_k exp(j b_k sin(ω t_i + ϕ_k))) + σ CN(0,1), FC column g = 1.3 exp(jΦ_g),
  * Φ a random walk (σ 1e-3 rad/step), 4 series per FC column, counter-based RNG keyed by
@@ -268,7 +281,7 @@ int gpd_synth_fill_dev(int64_t n_samples, int64_t n_pixels, int64_t pixel_offset
  * the restatement the exact evaluator applies per sample, src/Modulation.jl:137,388,419-421,
  * src/Faint.jl:95-97), for host-vs-device bit-for-bit checks.  fn: 0 sin, 1 cos, 2 sincos (out
  * holds n (s, c) pairs), 3 atan, 4 atan(x[i], y[i]), 5 hypot(x[i], y[i]), 6 rem_pio2 (n triples
- * (quadrant, hi, lo)).  Host arrays (y may be NULL for the one-argument functions), synchronous.
+ * (quadrant, hi, lo)), 7 hypot(x[i], y[i]) in its branch-free form (the faint statistics').  Host arrays (y may be NULL for the one-argument functions), synchronous.
  */
 int gpd_libm_eval(int fn, int64_t n, const double *x, const double *y, double *out, int device);
 

@@ -306,7 +306,7 @@ double oracle_chi2(int64_t n, const double *t, const double *d, const double *w,
  * mean(abs, x) = Σ|x|/n and var(|x|; mean=m) = Σ(|x|-m)²/(n-1); sums in the reduction order
  * above (lane = original sample index mod 256).  A 1-sample state gives 0/0 = NaN weights. */
 static void mean_var_power_idx(int64_t n, const int8_t *states, const cplx *d, const int64_t *orig,
-                               double *m, double *w, gsum_t *g) {
+                               double *m, double *w, gsum_t *g, double *m5o, double *w5o) {
     double tot[10], m5[5], w5[5], ss[5];
     gsum_zero(g, 10);
     for (int64_t i = 0; i < n; ++i) {
@@ -328,6 +328,10 @@ static void mean_var_power_idx(int64_t n, const int8_t *states, const cplx *d, c
         m[i] = m5[states[i] + 1];
         w[i] = w5[states[i] + 1];
     }
+    if (m5o)
+        for (int q = 0; q < 5; ++q) m5o[q] = m5[q];
+    if (w5o)
+        for (int q = 0; q < 5; ++q) w5o[q] = w5[q];
 }
 
 void oracle_mean_var_power(int64_t n, const int8_t *states, const double *d_, double *m,
@@ -335,8 +339,37 @@ void oracle_mean_var_power(int64_t n, const int8_t *states, const double *d_, do
     int64_t *orig = (int64_t *)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
     gsum_t *g = (gsum_t *)malloc(sizeof(gsum_t));
     for (int64_t i = 0; i < n; ++i) orig[i] = i;
-    mean_var_power_idx(n, states, (const cplx *)d_, orig, m, w, g);
+    mean_var_power_idx(n, states, (const cplx *)d_, orig, m, w, g, NULL, NULL);
     free(orig);
+    free(g);
+}
+
+void oracle_mean_var_power_series(int64_t n, const int8_t *states, const double *d_, uint32_t flags,
+                                  double *m5, double *w5) {
+    const cplx *d = (const cplx *)d_;
+    int64_t *orig = (int64_t *)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+    int8_t *sv = (int8_t *)malloc((size_t)(n > 0 ? n : 1));
+    cplx *dv = (cplx *)malloc(sizeof(cplx) * (size_t)(n > 0 ? n : 1));
+    double *m = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    double *w = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    gsum_t *g = (gsum_t *)malloc(sizeof(gsum_t));
+    int64_t nv = 0;
+    for (int64_t i = 0; i < n; ++i) { /* valid mask, src/Modulation.jl:373-382 */
+        int ok = 1;
+        if (flags & ORACLE_ONLY_HIGH) ok = (states[i] == ST_HIGH) || (states[i] == ST_NORMAL);
+        if (states[i] == ST_TRANSIENT) ok = 0;
+        if (!ok) continue;
+        orig[nv] = i;
+        sv[nv] = states[i];
+        dv[nv] = d[i];
+        nv++;
+    }
+    mean_var_power_idx(nv, sv, dv, orig, m, w, g, m5, w5);
+    free(orig);
+    free(sv);
+    free(dv);
+    free(m);
+    free(w);
     free(g);
 }
 
@@ -434,7 +467,7 @@ static void fit_pixel(int64_t n, const double *t, const cplx *dcol, const cplx *
             if (state[i] == ST_TRANSIENT) ok = 0;
             if (ok) sv[k++] = state[i];
         }
-        mean_var_power_idx(nv, sv, s->d, s->orig, m, s->w, s->gs);
+        mean_var_power_idx(nv, sv, s->d, s->orig, m, s->w, s->gs, NULL, NULL);
         for (int64_t i = 0; i < nv; ++i) { /* p = power .* FCphasor[valid] */
             s->p[i].re = m[i] * s->p[i].re;
             s->p[i].im = m[i] * s->p[i].im;
@@ -567,6 +600,7 @@ int oracle_jl_eval(int fn, int64_t n, const double *x, const double *y, double *
         case 3: out[i] = jl_atan(x[i]); break;
         case 4: out[i] = jl_atan2(x[i], y[i]); break;
         case 5: out[i] = jl_hypot(x[i], y[i]); break;
+        case 7: out[i] = jl_hypot_nb(x[i], y[i]); break;
         case 6: {
             double hi, lo;
             const int q = jl_rem_pio2(x[i], &hi, &lo);

@@ -59,6 +59,12 @@ int oracle_buildstates(int64_t n, const double *t, int64_t n1, const double *tim
 void oracle_mean_var_power(int64_t n, const int8_t *states, const double *d, double *m,
                            double *w);
 
+/* compute_mean_var_power as demodulateall applies it (src/Modulation.jl:373-396): the valid
+ * mask of a whole series (TRANSIENT dropped; ORACLE_ONLY_HIGH keeps HIGH ∪ NORMAL), sums in the
+ * reduction order of the ORIGINAL sample indices (as in the fit).  m5/w5: per MetState code + 1. */
+void oracle_mean_var_power_series(int64_t n, const int8_t *states, const double *d, uint32_t flags,
+                                  double *m5, double *w5);
+
 /* src/Modulation.jl:360 ϕrange = range(-π, π, 8), as Float64 values. */
 void oracle_phi_grid(double *out8);
 

@@ -56,6 +56,8 @@ def lib():
         L.oracle_buildstates.restype = ctypes.c_int
         L.oracle_mean_var_power.argtypes = [ctypes.c_int64, P, P, P, P]
         L.oracle_mean_var_power.restype = None
+        L.oracle_mean_var_power_series.argtypes = [ctypes.c_int64, P, P, ctypes.c_uint32, P, P]
+        L.oracle_mean_var_power_series.restype = None
         L.oracle_phi_grid.argtypes = [P]
         L.oracle_phi_grid.restype = None
         OBJ = ctypes.CFUNCTYPE(ctypes.c_double, ctypes.c_void_p, ctypes.c_int,
@@ -147,7 +149,20 @@ def mean_var_power(states, d):
     return m, w
 
 
-JL_FN = {"sin": 0, "cos": 1, "sincos": 2, "atan": 3, "atan2": 4, "hypot": 5, "rem_pio2": 6}
+def mean_var_power_series(states, d, onlyhigh=False):
+    """Per-state (m, w) of one whole series as demodulateall computes them (valid mask applied,
+    sums over the original sample indices): arrays of 5, index = MetState code + 1."""
+    L = lib()
+    s = np.ascontiguousarray(states, dtype=np.int8)
+    d = np.ascontiguousarray(d, dtype=np.complex128)
+    m5 = np.zeros(5)
+    w5 = np.zeros(5)
+    L.oracle_mean_var_power_series(d.size, _ptr(s), _ptr(d), ONLY_HIGH if onlyhigh else 0,
+                                   _ptr(m5), _ptr(w5))
+    return m5, w5
+
+
+JL_FN = {"sin": 0, "cos": 1, "sincos": 2, "atan": 3, "atan2": 4, "hypot": 5, "rem_pio2": 6, "hypot_nb": 7}
 
 
 def jl_eval(fn, x, y=None):

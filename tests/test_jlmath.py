@@ -182,6 +182,30 @@ def test_special_values(oracle):
     assert h[4] == math.hypot(1e-310, 1e-310)
 
 
+def _hypot_args(rng, n):
+    """Pairs across every path of hypot: ordinary, swapped, ratio below sqrt(eps/2), both
+    scaling ranges (> sqrt(floatmax/2), < sqrt(floatmin)), subnormals, ±0, ±Inf, NaN."""
+    x = rng.standard_normal(n) * np.exp(rng.uniform(-745, 709, n))
+    y = rng.standard_normal(n) * np.exp(rng.uniform(-745, 709, n))
+    x[: n // 4] = rng.standard_normal(n // 4) * 2.0 ** 511 * rng.uniform(0.5, 3, n // 4)
+    y[: n // 4] = rng.standard_normal(n // 4) * 2.0 ** 511 * rng.uniform(0.1, 3, n // 4)
+    x[n // 4: n // 2] = rng.standard_normal(n // 4) * 2.0 ** -520
+    y[n // 4: n // 2] = rng.standard_normal(n // 4) * 2.0 ** -505
+    y[n // 2: n // 2 + 1000] = x[n // 2: n // 2 + 1000] * 1e-9
+    sp = [0.0, -0.0, math.inf, -math.inf, math.nan, 5e-324, -5e-324, 1e-310, 1.0, 2.0 ** 1023,
+          float.fromhex("0x1.6a09e667f3bccp+511"), float.fromhex("0x1.6a09e667f3bcdp+511"),
+          2.0 ** -511, 2.0 ** -512]
+    a, b = np.meshgrid(sp, sp)
+    return np.concatenate([x, a.ravel()]), np.concatenate([y, b.ravel()])
+
+
+def test_branch_free_hypot_equals_hypot(oracle):
+    """jl_hypot_nb (every path evaluated, result selected — the faint statistics' hypot) gives
+    jl_hypot's bits on every input."""
+    x, y = _hypot_args(np.random.default_rng(17), 400000)
+    assert same_bits(oracle.jl_eval("hypot_nb", x, y), oracle.jl_eval("hypot", x, y))
+
+
 @pytest.mark.gpu
 def test_device_libm_equals_oracle_bitwise(gpu, oracle):
     """The exact evaluator's per-sample functions on the device = the oracle's, bit for bit."""
@@ -202,5 +226,7 @@ def test_device_libm_equals_oracle_bitwise(gpu, oracle):
     ys = rng.standard_normal(n) * np.exp(rng.uniform(-40, 40, n))
     xs[:16] = specials
     ys[:16] = specials[::-1]
-    for fn in ("atan2", "hypot"):
+    for fn in ("atan2", "hypot", "hypot_nb"):
         assert same_bits(gpu.libm_eval(fn, xs, ys), oracle.jl_eval(fn, xs, ys)), fn
+    hx, hy = _hypot_args(rng, 200000)
+    assert same_bits(gpu.libm_eval("hypot_nb", hx, hy), oracle.jl_eval("hypot", hx, hy))

@@ -157,6 +157,17 @@ def main():
                        for m in ("harmonic", "exact")},
         "harmonic_vs_exact_f64": summarise(res["f64_harmonic"], res["f64_exact"]),
         "f64_exact_vs_truth_median_abs_b": float(np.median(np.abs(res["f64_exact"]["b"] - tr["b"]))),
+        # whole faint harmonic step against the HBM roofline: algorithmic bytes = the series
+        # (16 B, c32: 8) + its FC column shared by 4 (4 B, c32: 2) per sample, + t and the state
+        # byte per sample (shared) — every byte read once
+        "roofline_harmonic": {
+            key: {"algorithmic_bytes": P * N * (esz + esz / 4) + 9 * N,
+                  "step_ms": runs[f"{key}_harmonic"]["wall_ms"],
+                  "achieved_GBs": round((P * N * (esz + esz / 4) + 9 * N)
+                                        / (runs[f"{key}_harmonic"]["wall_ms"] * 1e-3) / 1e9, 1),
+                  "frac_of_8TBs": round((P * N * (esz + esz / 4) + 9 * N)
+                                        / (runs[f"{key}_harmonic"]["wall_ms"] * 1e-3) / 8e12, 4)}
+            for key, esz in (("f64", 16), ("c32", 8))},
         "tolerances": TOLS,
     }
     os.makedirs(os.path.dirname(args.out), exist_ok=True)

@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""C5 faint harmonic step only (4096 × 1e5, tools/c5_sweep.py's workload), for timing and
+rocprofv3 counter passes of the faint kernels.  Prints per-kernel HIP-event times."""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--series", type=int, default=4096)
+    ap.add_argument("--samples", type=int, default=100_000)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--c32", action="store_true")
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+
+    import gpdemod_loader
+    from c5_sweep import POWER, c5_states
+
+    gpd = gpdemod_loader.load()
+    L = gpd.load()
+    dev = torch.device("cuda", 0)
+    sptr = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    P, N = args.series, args.samples
+    G = P // 4
+    t = torch.empty(N, dtype=torch.float64, device=dev)
+    d = torch.empty((P, N, 2), dtype=torch.float64, device=dev)
+    fc = torch.empty((G, N, 2), dtype=torch.float64, device=dev)
+    fcop = torch.empty(P, dtype=torch.int32, device=dev)
+    gpd._lib.check(L.gpd_synth_fill_dev(N, P, 0, 11, 0.0, 0.002, 0.0, 0, gpd.M_2PI, t.data_ptr(),
+                                        d.data_ptr(), N, fc.data_ptr(), N, fcop.data_ptr(), None,
+                                        0, sptr))
+    st = c5_states(gpd, t.cpu().numpy())
+    power = torch.tensor([POWER[int(s)] for s in st], dtype=torch.float64, device=dev)
+    d.mul_(power[None, :, None])
+    d.add_(torch.randn(d.shape, dtype=torch.float64, device=dev), alpha=0.02 / np.sqrt(2.0))
+    if args.c32:
+        d, fc = d.float(), fc.float()
+    std = torch.from_numpy(st).to(dev)
+    params = torch.empty((P, 64), dtype=torch.uint8, device=dev)
+    err = ctypes.create_string_buffer(512)
+    fn = L.gpd_fit_batch_c32_dev if args.c32 else L.gpd_fit_batch_dev
+    out = []
+    for _ in range(args.reps):
+        gpd._lib.check(fn(N, P, t.data_ptr(), d.data_ptr(), N, fc.data_ptr(), G, N,
+                          fcop.data_ptr(), std.data_ptr(), gpd.M_2PI, None,
+                          gpd.GPD_RECENTER | gpd.GPD_METHOD_HARMONIC, 60, params.data_ptr(),
+                          None, N, 0, sptr, err, len(err)), err)
+        torch.cuda.synchronize(dev)
+        out.append({k: round(v, 3) for k, v in gpd.timings(0).items()})
+    print(json.dumps({"series": P, "samples": N, "c32": args.c32, "kernels_ms": out[-1],
+                      "faint_stats_ms": [o.get("faint_stats") for o in out]}))
+
+
+if __name__ == "__main__":
+    main()
