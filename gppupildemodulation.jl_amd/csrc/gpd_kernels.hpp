@@ -447,55 +447,81 @@ __global__ __launch_bounds__(256) void k_faint_stats(Problem pb, double *__restr
 }
 
 // ---------------------------------------------------------------------------------------
-// k_faint_stats8: the same statistics, bit for bit, in one HBM pass.  k_faint_stats re-reads the
-// series for the variance and evaluates Julia's hypot twice per sample (VALU-bound: 3.2 ms for
-// 4096 × 1e5).  Here a series is split over FS_G = 8 workgroups along the canonical order's 8
-// blocks: workgroup part g owns the samples i ≡ 256g + t (mod 2048), t = thread — M = ⌈N/2048⌉
-// samples per thread.  Pass 1 loads each sample once (non-temporal, two register batches of FS_U
-// loads in flight), evaluates |d| = hypot once, keeps |d| and the sample's state slot in LDS, and
-// accumulates count / Σ|d| / Σ|d|² per state in slot order (exactly the k_faint_stats chain);
-// the 8 block totals are exchanged through global memory behind a per-series barrier (every
-// part then adds them in block order → the same m); pass 2 runs Σ(|d| − m)² from LDS, and the
-// last part to publish its totals adds them in block order and writes the record.
-// Persistent: one workgroup per CU (the LDS holds one), launched cooperatively (all resident),
-// workgroup w is part w mod 8 of series w/8, w/8 + W/8, … — short workgroups at one per CU left
-// the CUs idle between dispatches (5.5 ms for C5 with one launch per (series, part)).  While a
-// part waits at the barrier the first batch of its next series is already in flight.
-// Whole-exposure series with N ≤ FS_MAXM·2048 (131072 samples); windows and longer series take
-// k_faint_stats.
+// Faint statistics in one pass over the series and one hypot per sample (k_faint_stats re-reads
+// every series for the variance and evaluates Julia's hypot twice per sample: VALU-bound).  The
+// same chains as k_faint_stats, so the same bits: a series is split into its FS_G = 8 canonical
+// blocks (part g owns the samples i ≡ 256g + t (mod 2048), t = thread, M = ⌈N/2048⌉ per thread).
+//   k_faint_p1  per (series, part): loads each sample once (non-temporal, two register batches
+//               of FS_U loads in flight), |d| = hypot (branch-free form, 8 evaluations
+//               interleaved), count / Σ|d| / Σ|d|² per state along the slot chain → the part's
+//               block totals; |d| is written to a scratch buffer;
+//   k_faint_p2  per (series, part): m = the 8 block totals added in block order, then
+//               Σ (|d| − m)² along the same chain from the scratch;
+//   k_faint_fin per series: adds the block totals in order, writes m, w, W2, DEN, Q2.
+// Series are processed in cohorts of ≤ 4 GB of scratch (8 B per sample; streamed, non-temporal).
+// No LDS beyond block_sum's,
+// no cross-workgroup waits: full occupancy hides the latencies (a persistent one-workgroup-per-CU
+// version holding |d| in LDS ran at one wave per SIMD and spent 4.7 ms on C5, latency-bound).
+// Whole-exposure series; windows take k_faint_stats (per-window spans).
 constexpr int FS_G = 8;  // = CR_BLOCKS, the canonical order's blocks
-constexpr int FS_MAXM = 64;
-constexpr int FS_U = 16;
+constexpr int FS_U = 8;
 constexpr int FS_NV = 16;  // payload doubles per block total (15 used)
 
+// Add (1, a, b) to the sums of state q (no state: q < 0) — the chains of k_faint_stats.  A
+// wave's 64 lanes hold 64 consecutive samples (128 ms at 2 ms), almost always of one state:
+// then one wave-uniform branch updates that state's three sums; otherwise every state's sums
+// take the sample or keep their value (branch-free).
+__device__ __forceinline__ void fs_accum3(int q, double a, double b, int (&cnt)[5],
+                                          double (&sa)[5], double (&sb)[5]) {
+    const int q0 = __builtin_amdgcn_readfirstlane(q);
+    if (__builtin_amdgcn_ballot_w64(q != q0) == 0) {
+        switch (q0) {
+#define GPD_FS_CASE(S)   \
+    case S:              \
+        cnt[S] += 1;     \
+        sa[S] += a;      \
+        sb[S] += b;      \
+        break;
+            GPD_FS_CASE(0) GPD_FS_CASE(1) GPD_FS_CASE(2) GPD_FS_CASE(3) GPD_FS_CASE(4)
+#undef GPD_FS_CASE
+        default: break;
+        }
+        return;
+    }
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+        const bool h = q == s;
+        cnt[s] += h;
+        const double xa = sa[s] + a, xb = sb[s] + b;
+        sa[s] = h ? xa : sa[s];
+        sb[s] = h ? xb : sb[s];
+    }
+}
+
 template <class TS>
-__global__ __launch_bounds__(256) void k_faint_stats8(Problem pb, double *__restrict__ out,
-                                                      double *__restrict__ xtot,
-                                                      unsigned *__restrict__ xcnt) {
-    __shared__ double ad[FS_MAXM * 256];        // |d| of the thread's samples, [m][t]
-    __shared__ signed char sq[FS_MAXM * 256];   // state slot (code + 1), −1: not a valid sample
+__global__ __launch_bounds__(256) void k_faint_p1(Problem pb, long long k0, int Mmax,
+                                                  double *__restrict__ scr,
+                                                  double *__restrict__ xt) {
     __shared__ double lds[4 * 16];
-    __shared__ double xb[FS_G * 16];
-    __shared__ int flag;
-    typedef __attribute__((address_space(1))) unsigned long long gu64_;
-    typedef __attribute__((address_space(1))) unsigned gu32_;
     typedef double nv2d __attribute__((ext_vector_type(2)));
     typedef float nv2f __attribute__((ext_vector_type(2)));
     // samples stay in their storage type until processed (a widening at the load would wait
     // for it there)
     typedef typename std::conditional<sizeof(TS) == 16, nv2d, nv2f>::type VT;
     typedef const __attribute__((address_space(1))) VT gVT;
+    typedef __attribute__((address_space(1))) double gd;
+    const long long j = blockIdx.x / FS_G, k = k0 + j;
     const int g = (int)(blockIdx.x % FS_G), t = threadIdx.x;
-    const long long stride = gridDim.x / FS_G, N = pb.N;
-    const long long i0 = 256LL * g + t;                         // first sample of this slot
-    const int M = i0 < N ? (int)((N - 1 - i0) / 2048 + 1) : 0;  // samples of this slot
+    const long long N = pb.N, i0 = 256LL * g + t;
+    const int M = i0 < N ? (int)((N - 1 - i0) / 2048 + 1) : 0;
     const bool only_high = (pb.flags & F_ONLY_HIGH) != 0;
+    gVT *dp = (gVT *)d_base<TS>(pb) + k * pb.ldd + i0;
+    gd *sp = (gd *)scr + (long long)blockIdx.x * Mmax * 256 + t;
     struct Batch {
         VT z[FS_U];
         int st[FS_U];
     };
-    auto issue = [&](Batch &B, long long k, int m0) {
-        gVT *dp = (gVT *)d_base<TS>(pb) + k * pb.ldd + i0;
+    auto issue = [&](Batch &B, int m0) {
 #pragma unroll
         for (int u = 0; u < FS_U; ++u) {
             const int m = m0 + u < M ? m0 + u : M - 1;  // clamped (branch-free loads)
@@ -503,179 +529,172 @@ __global__ __launch_bounds__(256) void k_faint_stats8(Problem pb, double *__rest
             B.st[u] = gld(pb.state + i0 + 2048LL * m);
         }
     };
-    Batch A, B;
-    long long k = blockIdx.x / FS_G;
-    if (k < pb.P && M > 0) issue(A, k, 0);
-    for (; k < pb.P; k += stride) {
-        int cnt[5] = {0, 0, 0, 0, 0};
-        double sa[5] = {0, 0, 0, 0, 0}, s2[5] = {0, 0, 0, 0, 0};
-        auto process = [&](const Batch &Bt, int m0) {
-            // the batch's 16 hypots in one branch-free block (independent: they interleave —
-            // at one wave per SIMD nothing else hides the fp64 latency), then the in-order
-            // accumulation chain
-            double a[FS_U], d2[FS_U];
+    int cnt[5] = {0, 0, 0, 0, 0};
+    double sa[5] = {0, 0, 0, 0, 0}, s2[5] = {0, 0, 0, 0, 0};
+    auto process = [&](const Batch &Bt, int m0) {
+        double a[FS_U], d2[FS_U];
 #pragma unroll
-            for (int u = 0; u < FS_U; ++u) {
-                const double zr = (double)Bt.z[u].x, zi = (double)Bt.z[u].y;
-                a[u] = jl_hypot_nb(zr, zi);
-                d2[u] = zr * zr + zi * zi;
-            }
+        for (int u = 0; u < FS_U; ++u) {
+            const double zr = (double)Bt.z[u].x, zi = (double)Bt.z[u].y;
+            a[u] = jl_hypot_nb(zr, zi);
+            d2[u] = zr * zr + zi * zi;
+        }
 #pragma unroll
-            for (int u = 0; u < FS_U; ++u) {
-                const int m = m0 + u;
-                if (m >= M) break;
-                const int c = Bt.st[u];
-                const bool ok = c != -1 && (!only_high || c == 3 || c == 2);
-                const int q = ok ? c + 1 : -1;
-                sq[m * 256 + t] = (signed char)q;
-                ad[m * 256 + t] = a[u];
-                if (!ok) continue;
-#pragma unroll
-                for (int s = 0; s < 5; ++s)
-                    if (q == s) {
-                        ++cnt[s];
-                        sa[s] += a[u];
-                        s2[s] += d2[u];
-                    }
-            }
-        };
-        // pass 1 (batch A of this series is in flight already)
+        for (int u = 0; u < FS_U; ++u) {
+            const int m = m0 + u;
+            if (m >= M) break;
+            const int c = Bt.st[u];
+            const bool ok = c != -1 && (!only_high || c == 3 || c == 2);
+            const int q = ok ? c + 1 : -1;
+            __builtin_nontemporal_store(a[u], &sp[(long long)m * 256]);
+            fs_accum3(q, a[u], d2[u], cnt, sa, s2);
+        }
+    };
+    if (M > 0) {
+        Batch A, B;
+        issue(A, 0);
         int m0 = 0;
         for (; m0 + FS_U < M; m0 += 2 * FS_U) {
-            issue(B, k, m0 + FS_U);
+            issue(B, m0 + FS_U);
             process(A, m0);
-            if (m0 + 2 * FS_U < M) issue(A, k, m0 + 2 * FS_U);
+            if (m0 + 2 * FS_U < M) issue(A, m0 + 2 * FS_U);
             process(B, m0 + FS_U);
         }
         if (m0 < M) process(A, m0);
-
-        // block total (block_sum's fixed tree) → exchange slot 0 of the series, barrier
-        double v[15];
-#pragma unroll
-        for (int s = 0; s < 5; ++s) {
-            v[s] = (double)cnt[s];  // counts are exact in Float64: the bits of adding 1.0
-            v[5 + s] = sa[s];
-            v[10 + s] = s2[s];
-        }
-        block_sum<256, 15>(v, lds);
-        double *tot = xtot + k * (2 * FS_G * FS_NV);
-        if (t < 15) {
-            double x = v[0];
-#pragma unroll
-            for (int j = 1; j < 15; ++j) x = (t == j) ? v[j] : x;
-            __hip_atomic_store((gu64_ *)(tot + g * FS_NV + t),
-                               __builtin_bit_cast(unsigned long long, x), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (t == 0) {
-            __hip_atomic_fetch_add((gu32_ *)(xcnt + k), 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            unsigned spins = 0;
-            int f = 0;
-            while (__hip_atomic_load((gu32_ *)(xcnt + k), __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT) < (unsigned)FS_G) {
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > (1u << 24)) {  // a sibling is not resident (cooperative launch
-                    f = 1;                   // excludes it): give up, the series reports NaN
-                    break;
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            flag = f;
-        }
-        __syncthreads();
-        const bool sync_fail = flag != 0;
-        // the 8 × 15 block totals: one coherent load per value (threads 0..119) into LDS, then
-        // every thread adds them in block order (the same bits in every part)
-        if (t < FS_G * 15) {
-            const int b = t / 15, j = t - 15 * b;
-            xb[b * 16 + j] = __builtin_bit_cast(
-                double, __hip_atomic_load((gu64_ *)(tot + b * FS_NV + j), __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT));
-        }
-        __syncthreads();
-        double tv[15];
-#pragma unroll
-        for (int b = 0; b < FS_G; ++b)
-#pragma unroll
-            for (int j = 0; j < 15; ++j) tv[j] = (b == 0) ? xb[b * 16 + j] : tv[j] + xb[b * 16 + j];
-        if (sync_fail) {
-#pragma unroll
-            for (int j = 0; j < 15; ++j) tv[j] = __builtin_nan("");
-        }
-        double mu[5];
-#pragma unroll
-        for (int s = 0; s < 5; ++s) mu[s] = tv[5 + s] / tv[s];
-        // pass 2 from LDS: Σ (|d| − m)² per state, same slot chain
-        double sv[5] = {0, 0, 0, 0, 0};
-        for (int m = 0; m < M; ++m) {
-            const int q = sq[m * 256 + t];
-            if (q < 0) continue;
-            const double a = ad[m * 256 + t];
-#pragma unroll
-            for (int s = 0; s < 5; ++s)
-                if (q == s) {
-                    const double dv = a - mu[s];
-                    sv[s] += dv * dv;
-                }
-        }
-        block_sum<256, 5>(sv, lds);
-        if (t < 5) {
-            double x = sv[0];
-#pragma unroll
-            for (int j = 1; j < 5; ++j) x = (t == j) ? sv[j] : x;
-            __hip_atomic_store((gu64_ *)(tot + (FS_G + g) * FS_NV + t),
-                               __builtin_bit_cast(unsigned long long, x), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        // the last part of the series to arrive writes the record
-        if (t == 0) {
-            const unsigned old = __hip_atomic_fetch_add((gu32_ *)(xcnt + k), 1u, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT);
-            flag = old == 2 * FS_G - 1;
-            if (flag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        }
-        // the next series' first batch flies while the record is written (issued after this
-        // series' last payload store: a wait for those stores would drain these loads too)
-        const long long kn = k + stride;
-        if (kn < pb.P && M > 0) issue(A, kn, 0);
-        __syncthreads();
-        if (flag) {
-            if (t < FS_G * 5) {
-                const int b = t / 5, j = t - 5 * b;
-                xb[b * 16 + j] = __builtin_bit_cast(
-                    double, __hip_atomic_load((gu64_ *)(tot + (FS_G + b) * FS_NV + j),
-                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            }
-            __syncthreads();
-            if (t == 0) {
-                double ssum[5];
-                for (int b = 0; b < FS_G; ++b)
-                    for (int j = 0; j < 5; ++j)
-                        ssum[j] = (b == 0) ? xb[b * 16 + j] : ssum[j] + xb[b * 16 + j];
-                double *o = out + k * 16;
-                double W2 = 0.0, DEN = 0.0, Q2 = 0.0;
-                for (int q = 0; q < 5; ++q) {
-                    const double w = 1.0 / (ssum[q] / (tv[q] - 1.0));
-                    o[q] = mu[q];
-                    o[5 + q] = w;
-                    if (tv[q] > 0) {
-                        W2 += w * tv[10 + q];
-                        DEN += w * mu[q] * mu[q] * tv[q];
-                        Q2 += (w * mu[q]) * (w * mu[q]) * tv[10 + q];
-                    }
-                }
-                o[10] = W2;
-                o[11] = DEN;
-                o[12] = Q2;
-            }
-        }
-        __syncthreads();  // LDS (sq, ad, xb) is rewritten by the next series
     }
+    double v[15];
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+        v[s] = (double)cnt[s];  // counts are exact in Float64: the bits of adding 1.0
+        v[5 + s] = sa[s];
+        v[10 + s] = s2[s];
+    }
+    block_sum<256, 15>(v, lds);
+    if (t < 15) {
+        double x = v[0];
+#pragma unroll
+        for (int q = 1; q < 15; ++q) x = (t == q) ? v[q] : x;
+        xt[(long long)blockIdx.x * FS_NV + t] = x;
+    }
+}
+
+// the 8 block totals of series j (cohort-local) added in block order
+__device__ __forceinline__ void fs_totals(const double *__restrict__ xt, long long j, double (&tv)[15]) {
+#pragma unroll
+    for (int b = 0; b < FS_G; ++b)
+#pragma unroll
+        for (int q = 0; q < 15; ++q) {
+            const double x = xt[(j * FS_G + b) * FS_NV + q];
+            tv[q] = (b == 0) ? x : tv[q] + x;
+        }
+}
+
+__global__ __launch_bounds__(256) void k_faint_p2(Problem pb, int Mmax,
+                                                  const double *__restrict__ scr,
+                                                  const double *__restrict__ xt,
+                                                  double *__restrict__ x2) {
+    __shared__ double lds[4 * 8];
+    __shared__ double mus[5];
+    typedef const __attribute__((address_space(1))) double gd;
+    const long long j = blockIdx.x / FS_G;
+    const int g = (int)(blockIdx.x % FS_G), t = threadIdx.x;
+    const long long N = pb.N, i0 = 256LL * g + t;
+    const int M = i0 < N ? (int)((N - 1 - i0) / 2048 + 1) : 0;
+    const bool only_high = (pb.flags & F_ONLY_HIGH) != 0;
+    if (t == 0) {
+        double tv[15];
+        fs_totals(xt, j, tv);
+        for (int s = 0; s < 5; ++s) mus[s] = tv[5 + s] / tv[s];
+    }
+    __syncthreads();
+    double mu[5];
+#pragma unroll
+    for (int s = 0; s < 5; ++s) mu[s] = mus[s];
+    gd *sp = (gd *)scr + (long long)blockIdx.x * Mmax * 256 + t;
+    double sv[5] = {0, 0, 0, 0, 0};
+    for (int mb = 0; mb < M; mb += 8) {
+        int qq[8];
+        double aa[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int m = mb + u < M ? mb + u : M - 1;
+            const int c = gld(pb.state + i0 + 2048LL * m);
+            const bool ok = c != -1 && (!only_high || c == 3 || c == 2);
+            qq[u] = (ok && mb + u < M) ? c + 1 : -1;
+            aa[u] = __builtin_nontemporal_load(&sp[(long long)m * 256]);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int q = qq[u];
+            const int q0 = __builtin_amdgcn_readfirstlane(q);
+            if (__builtin_amdgcn_ballot_w64(q != q0) == 0) {  // one state across the wave
+                switch (q0) {
+#define GPD_FS_CASE(S)                        \
+    case S: {                                 \
+        const double dv = aa[u] - mu[S];      \
+        sv[S] += dv * dv;                     \
+    } break;
+                    GPD_FS_CASE(0) GPD_FS_CASE(1) GPD_FS_CASE(2) GPD_FS_CASE(3) GPD_FS_CASE(4)
+#undef GPD_FS_CASE
+                default: break;
+                }
+                continue;
+            }
+            double mq = mu[0];
+#pragma unroll
+            for (int s = 1; s < 5; ++s) mq = q == s ? mu[s] : mq;
+            const double dv = aa[u] - mq;
+            const double d2v = dv * dv;
+#pragma unroll
+            for (int s = 0; s < 5; ++s) {
+                const double x = sv[s] + d2v;
+                sv[s] = q == s ? x : sv[s];
+            }
+        }
+    }
+    block_sum<256, 5>(sv, lds);
+    if (t < 5) {
+        double x = sv[0];
+#pragma unroll
+        for (int q = 1; q < 5; ++q) x = (t == q) ? sv[q] : x;
+        x2[(long long)blockIdx.x * 8 + t] = x;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_faint_fin(long long k0, const double *__restrict__ xt,
+                                                  const double *__restrict__ x2,
+                                                  double *__restrict__ out) {
+    // one wave per series: the lanes fetch the 8 × (15 + 5) block totals, lane 0 adds them in
+    // block order and writes the record
+    __shared__ double v[FS_G * 20];
+    const long long j = blockIdx.x;
+    for (int e = threadIdx.x; e < FS_G * 20; e += 64) {
+        const int b = e / 20, q = e - 20 * b;
+        v[e] = q < 15 ? xt[(j * FS_G + b) * FS_NV + q] : x2[(j * FS_G + b) * 8 + (q - 15)];
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    double tv[15], ss[5];
+    for (int b = 0; b < FS_G; ++b) {
+        for (int q = 0; q < 15; ++q) tv[q] = (b == 0) ? v[b * 20 + q] : tv[q] + v[b * 20 + q];
+        for (int q = 0; q < 5; ++q) ss[q] = (b == 0) ? v[b * 20 + 15 + q] : ss[q] + v[b * 20 + 15 + q];
+    }
+    double *o = out + (k0 + j) * 16;
+    double W2 = 0.0, DEN = 0.0, Q2 = 0.0;
+    for (int q = 0; q < 5; ++q) {
+        const double m = tv[5 + q] / tv[q];
+        const double w = 1.0 / (ss[q] / (tv[q] - 1.0));
+        o[q] = m;
+        o[5 + q] = w;
+        if (tv[q] > 0) {
+            W2 += w * tv[10 + q];
+            DEN += w * m * m * tv[q];
+            Q2 += (w * m) * (w * m) * tv[10 + q];
+        }
+    }
+    o[10] = W2;
+    o[11] = DEN;
+    o[12] = Q2;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1581,7 +1600,7 @@ __global__ __launch_bounds__(64) void k_fit_harmonic(Problem pb, const Info *__r
 // every workgroup of the series adds all 8 after a per-series barrier — the same bits for every
 // G, so small batches (one exposure: 32 series) can spread over the chip.
 constexpr int CR_BLOCKS = 8;
-static_assert(FS_G == CR_BLOCKS, "k_faint_stats8 splits a series along the CR8 blocks");
+static_assert(FS_G == CR_BLOCKS, "the one-pass faint statistics split a series along the CR8 blocks");
 constexpr int CR_SLOTS = CR_BLOCKS * EXACT_WG;  // 2048
 constexpr int CR_NV = 8;                        // values per block total (offsets: 8)
 constexpr int CR_FLAG = (EXACT_WG / 64) * 8;    // LDS word after block_sum's partials

@@ -1,8 +1,8 @@
 """Faint power and weight on the GPU (§8 row a10): compute_mean_var_power (src/Faint.jl:89-100)
-as demodulateall applies it (valid mask, src/Modulation.jl:373-396) — the one-pass kernel
-(k_faint_stats8: |d| kept in LDS, 8 workgroups per series) and the two-pass kernel
-(GPD_FAINT_STATS=2; windows and series longer than 131072 samples) against the oracle, bit for
-bit, NaN for empty / 1-sample states included."""
+as demodulateall applies it (valid mask, src/Modulation.jl:373-396) — the one-pass kernels
+(k_faint_p1/p2/fin: one hypot per sample, |d| through a MALL-sized scratch, cohorts of series)
+and the two-pass kernel (GPD_FAINT_STATS=2; the windows' kernel) against the oracle, bit for bit,
+NaN for empty / 1-sample states included."""
 import numpy as np
 import pytest
 
@@ -52,11 +52,11 @@ def test_compute_mean_var_power_is_the_reference_function(gpu, oracle):
     assert _bits(m, rm) and _bits(w, rw)
 
 
-@pytest.mark.parametrize("N", [2047, 131_072, 131_073])
-def test_one_pass_equals_two_pass(gpu, monkeypatch, N):
-    """The two kernels give the same bits on every length, including the one-pass kernel's
-    largest (131072 = 64·2048 samples) and the first length past it (two-pass for both)."""
-    d, st = _series(N, 8, seed=3)
+@pytest.mark.parametrize("N,P", [(2047, 8), (131_073, 8), (100_000, 300)])
+def test_one_pass_equals_two_pass(gpu, monkeypatch, N, P):
+    """The two kernels give the same bits on every length (a part with no sample, ragged last
+    slots) and across several cohorts (300 series × 1e5 samples = 2 cohorts of ≤ 239)."""
+    d, st = _series(N, P, seed=3)
     a = gpu.mean_var_power_batch(st, d)
     monkeypatch.setenv("GPD_FAINT_STATS", "2")
     b = gpu.mean_var_power_batch(st, d)
