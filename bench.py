@@ -286,17 +286,20 @@ def main():
 
 
 def traffic_from_profiles(P, N, storage="c64"):
-    """HBM bytes per moment-kernel launch from the committed rocprofv3 PMC summary (FETCH_SIZE
-    doubled per MI355X_MICROARCH.md §HBM + WRITE_SIZE), when it was taken on this shape."""
-    path = os.path.join(ROOT, "profiles", "pmc_moments.json" if storage == "c64"
-                        else f"pmc_moments_{storage}.json")
-    try:
-        with open(path) as f:
-            j = json.load(f)
-        if j.get("pixels") == P and j.get("samples") == N:
+    """HBM bytes per moment-kernel launch from a committed rocprofv3 PMC summary
+    (profiles/pmc_moments*.json: FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM + WRITE_SIZE),
+    when one was taken on this shape and storage."""
+    import glob
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_moments*.json"))):
+        try:
+            with open(path) as f:
+                j = json.load(f)
+        except (OSError, ValueError):
+            continue
+        st = j.get("storage", "c32" if "c32" in os.path.basename(path) else "c64")
+        if j.get("pixels") == P and j.get("samples") == N and st == storage:
             return j.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
     return None
 
 

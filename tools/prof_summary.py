@@ -49,8 +49,10 @@ def main(tag, src=None):
     json.dump(summary, open(os.path.join(dst, "summary.json"), "w"), indent=1)
     storage = cfg.get("storage", "c64")
     name = "pmc_moments.json" if storage == "c64" else f"pmc_moments_{storage}.json"
+    if (cfg["series_per_gpu"], cfg["samples"]) != (100_000, 100_000):
+        name = name.replace(".json", f"_{cfg['series_per_gpu']}x{cfg['samples']}.json")
     json.dump({k: summary[k] for k in ("tag", "pixels", "samples", "hbm_bytes_per_launch",
-                                       "FETCH_SIZE_kB", "WRITE_SIZE_kB")},
+                                       "FETCH_SIZE_kB", "WRITE_SIZE_kB")} | {"storage": storage},
               open(os.path.join(ROOT, "profiles", name), "w"), indent=1)
     print(json.dumps({k: v for k, v in summary.items() if k != "bench"}, indent=1))
 
