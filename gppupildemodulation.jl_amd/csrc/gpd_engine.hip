@@ -592,6 +592,14 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         }
         if (exact_g > 1)
             HIP_TRY(hipMemsetAsync(ws + L.xcnt, 0, (size_t)(P + 3) / 4 * 16, stream));
+        // GPD_FIT_PROF (diagnostics): per-phase cycles of the multi-workgroup exact fit
+        static const bool xprof = getenv("GPD_FIT_PROF") != nullptr;
+        unsigned long long zx[4] = {0, 0, 0, 0};
+        if (xprof && exact_g > 1 && !bphi) {
+            pb.flags |= F_PROF;
+            HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_fitprof), zx, sizeof zx, 0,
+                                           hipMemcpyHostToDevice, stream));
+        }
         const unsigned fit_grid =
             exact_g > 1 ? (unsigned)((P + 7) / 8 * 8 * exact_g) : exact_grid;
 #define GPD_LAUNCH_EXACT(FA, OF, PH)                                                                 \
@@ -614,6 +622,16 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         }
 #undef GPD_LAUNCH_EXACT
         mark(bphi ? "chi2_exact" : "fit_exact");
+        if (pb.flags & F_PROF) {
+            pb.flags &= ~F_PROF;
+            HIP_TRY(hipMemcpyFromSymbolAsync(zx, HIP_SYMBOL(g_fitprof), sizeof zx, 0,
+                                             hipMemcpyDeviceToHost, stream));
+            HIP_TRY(hipStreamSynchronize(stream));
+            const double nwg = (double)P * exact_g;
+            fprintf(stderr, "exact fit_prof cycles per workgroup: pass1 %.4g residual %.4g "
+                    "exchange %.4g whole %.4g\n", zx[0] / nwg, zx[1] / nwg, zx[2] / nwg,
+                    zx[3] / nwg);
+        }
     }
     if (out_demod && !bphi) {
         const long long span = window > 0 ? std::min<long long>(window, N) : N;

@@ -1603,6 +1603,7 @@ constexpr int CR_BLOCKS = 8;
 static_assert(FS_G == CR_BLOCKS, "the one-pass faint statistics split a series along the CR8 blocks");
 constexpr int CR_SLOTS = CR_BLOCKS * EXACT_WG;  // 2048
 constexpr int CR_NV = 8;                        // values per block total (offsets: 8)
+constexpr int CR_U = 4;                         // cr_sum2: samples per prefetched batch
 constexpr int CR_FLAG = (EXACT_WG / 64) * 8;    // LDS word after block_sum's partials
 constexpr int EXACT_LDS = CR_FLAG + 1;          // doubles of LDS per exact-path workgroup
 
@@ -1639,6 +1640,10 @@ struct ExactChi2 {
     Xchg x;
     unsigned nbar;  // barriers passed
     bool sync_fail; // a barrier spin gave up (never observed; the series reports NaN)
+    // GPD_FIT_PROF (diagnostics): cycles of the first pass, the residual pass, the G > 1
+    // exchange (barrier) and the whole fit, per workgroup
+    bool prof;
+    unsigned long long pc[3];
 
     // Global-address-space views of the problem's arrays, taken once per evaluation: this
     // functor runs out of line, where plain pointers are generic and every flat load's wait
@@ -1714,6 +1719,56 @@ struct ExactChi2 {
         }
         return true;
     }
+    // A sample's inputs, loaded ahead of their use (cr_sum2): the state, ωt's t, the phasor
+    // (PHBUF) or the raw FC sample, the series sample — or, for the residual pass, the cached
+    // model in place of t and the phasor.
+    struct Raw {
+        c64 f, d;
+        double t;
+        int st;
+    };
+    __device__ __forceinline__ void load_raw(const View &v, long long i, Raw &r) const {
+        r.st = v.state ? (int)v.state[i] : 0;
+        r.t = v.t[i];
+        r.f = PHBUF ? ld(v.src + i) : (v.fc32 ? ld(v.fc32 + foff + i) : ld(v.fc + foff + i));
+        r.d = d_of(v, doff + i);
+    }
+    __device__ __forceinline__ void load_res(const View &v, long long i, Raw &r) const {
+        r.st = v.state ? (int)v.state[i] : 0;
+        const gmc64 *mcg = (const gmc64 *)mc;
+        r.f = c64{mcg[i - s0].re, mcg[i - s0].im};
+        r.d = d_of(v, doff + i);
+    }
+    // sample_valid on a loaded state (TRANSIENT dropped, onlyhigh keeps HIGH ∪ NORMAL)
+    __device__ __forceinline__ bool valid_st(const View &v, int st) const {
+        if (v.state == nullptr) return true;
+        if (st == -1) return false;
+        if (v.only_high) return st == 3 || st == 2;
+        return true;
+    }
+    // load() on a loaded sample: power·phasor and weight
+    __device__ __forceinline__ void pw_of(const Raw &r, c64 &p, double &w) const {
+        const c64 ph = PHBUF ? r.f : fc_phasor(r.f);
+        if (FAINT) {
+            double m = m5[0], ww = w5[0];
+#pragma unroll
+            for (int q = 1; q < 5; ++q) {
+                m = (r.st + 1 == q) ? m5[q] : m;
+                ww = (r.st + 1 == q) ? w5[q] : ww;
+            }
+            p = {m * ph.re, m * ph.im};  // power .* FCphasor (src/Modulation.jl:396)
+            w = ww;
+        } else {
+            p = ph;
+            w = 1.0;
+        }
+    }
+    __device__ __forceinline__ c64 model_t(double t, const c64 &p, double b, double phi) const {
+        double th = pb->omega * t;
+        th = th + phi;
+        const double beta = b * jl_sin(th);
+        return cmul(p, cisj(beta));  // power * exp(ȷ b sin(ωt+ϕ)) (src/Modulation.jl:137)
+    }
     __device__ __forceinline__ c64 model(const View &v, long long i, const c64 &p, double b,
                                          double phi) const {
         double th = v.omega * v.t[i];
@@ -1751,13 +1806,22 @@ struct ExactChi2 {
     // every workgroup of the series returns the same NV totals.
     template <int NV, class A>
     __device__ __forceinline__ void cr_sum(A &&accum, double (&tot)[NV]) {
+        cr_sum_blocks<NV>(
+            [&](long long i0, double (&acc)[NV]) {
+                for (long long i = i0; i < s1; i += CR_SLOTS) accum(i, acc);
+            },
+            tot);
+    }
+    // chain(i0, acc): add the chain of samples i0, i0 + 2048, … < s1 into acc, in order
+    template <int NV, class C>
+    __device__ __forceinline__ void cr_sum_blocks(C &&chain, double (&tot)[NV]) {
         ldouble *lp = (ldouble *)lds;
         const int nb = CR_BLOCKS / G, b0 = g * nb;
         for (int blk = b0; blk < b0 + nb; ++blk) {
             double acc[NV];
 #pragma unroll
             for (int k = 0; k < NV; ++k) acc[k] = 0.0;
-            for (long long i = s0 + blk * EXACT_WG + threadIdx.x; i < s1; i += CR_SLOTS) accum(i, acc);
+            chain(s0 + blk * EXACT_WG + threadIdx.x, acc);
             block_sum<EXACT_WG, NV>(acc, lp);
             if (G == 1) {
 #pragma unroll
@@ -1773,7 +1837,9 @@ struct ExactChi2 {
             }
         }
         if (G == 1) return;
+        const unsigned long long tb = prof ? __builtin_amdgcn_s_memtime() : 0;
         xbarrier();
+        if (prof) pc[2] += __builtin_amdgcn_s_memtime() - tb;
         const double *base = x.tot + (nbar & 1) * (CR_BLOCKS * CR_NV);
 #pragma unroll
         for (int blk = 0; blk < CR_BLOCKS; ++blk) {
@@ -1791,24 +1857,64 @@ struct ExactChi2 {
         }
     }
 
+    // cr_sum with the loads of each chain issued CR_U samples ahead: load(i, Raw&) fetches a
+    // sample's inputs, accum(i, const Raw&, acc) computes and adds in chain order — the same
+    // sums as cr_sum (one wave per SIMD: nothing else hides the memory latency of a chain).
+    template <int NV, int U = CR_U, class L, class A>
+    __device__ __forceinline__ void cr_sum2(L &&load, A &&accum, double (&tot)[NV]) {
+        cr_sum_blocks<NV>(
+            [&](long long i0, double (&acc)[NV]) {
+                const int M = i0 < s1 ? (int)((s1 - 1 - i0) / CR_SLOTS + 1) : 0;
+                if (M == 0) return;
+                Raw A_[U], B_[U];
+                auto issue = [&](Raw (&X)[U], int m0) {
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int m = m0 + u < M ? m0 + u : M - 1;
+                        load(i0 + (long long)m * CR_SLOTS, X[u]);
+                    }
+                };
+                auto run = [&](const Raw (&X)[U], int m0) {
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        if (m0 + u >= M) break;
+                        accum(i0 + (long long)(m0 + u) * CR_SLOTS, X[u], acc);
+                    }
+                };
+                issue(A_, 0);
+                int m0 = 0;
+                for (; m0 + U < M; m0 += 2 * U) {
+                    issue(B_, m0 + U);
+                    run(A_, m0);
+                    if (m0 + 2 * U < M) issue(A_, m0 + 2 * U);
+                    run(B_, m0 + U);
+                }
+                if (m0 < M) run(A_, m0);
+            },
+            tot);
+    }
+
     __device__ double operator()(const double (&xx)[2]) {
         ++nfev;
         const double b = xx[0], phi = xx[1];
         const View V = view();
         gmc64 *mcg = (gmc64 *)mc;
+        const unsigned long long tp0 = prof ? __builtin_amdgcn_s_memtime() : 0;
         if (OFFS) {
             double v[8];  // a11, a12(2), a22, b1(2), b2(2)
-            cr_sum<8>(
-                [&](long long i, double (&a)[8]) {
+            cr_sum2<8>(
+                [&](long long i, Raw &r) { load_raw(V, i, r); },
+                [&](long long i, const Raw &r, double (&a)[8]) {
+                    if (!valid_st(V, r.st)) return;
                     c64 p;
                     double w;
-                    if (!load(V, i, p, w)) return;
-                    const c64 m = model(V, i, p, b, phi);
+                    pw_of(r, p, w);
+                    const c64 m = model_t(r.t, p, b, phi);
                     if (mcg) {
                         mcg[i - s0].re = m.re;
                         mcg[i - s0].im = m.im;
                     }
-                    const c64 dd = d_of(V, doff + i);
+                    const c64 dd = r.d;
                     a[0] += w;
                     a[1] += w * m.re;
                     a[2] += w * m.im;
@@ -1835,18 +1941,20 @@ struct ExactChi2 {
             a_im = aa.im;
         } else {
             double v[4];  // num(2), den(2)
-            cr_sum<4>(
-                [&](long long i, double (&a)[4]) {
+            cr_sum2<4>(
+                [&](long long i, Raw &r) { load_raw(V, i, r); },
+                [&](long long i, const Raw &r, double (&a)[4]) {
+                    if (!valid_st(V, r.st)) return;
                     c64 p;
                     double w;
-                    if (!load(V, i, p, w)) return;
-                    const c64 m = model(V, i, p, b, phi);
+                    pw_of(r, p, w);
+                    const c64 m = model_t(r.t, p, b, phi);
                     if (mcg) {
                         mcg[i - s0].re = m.re;
                         mcg[i - s0].im = m.im;
                     }
                     const c64 mwc = {m.re * w, -(m.im * w)};  // conj(model .* weight)
-                    const c64 xv = cmul(mwc, d_of(V, doff + i));
+                    const c64 xv = cmul(mwc, r.d);
                     const c64 yv = cmul(mwc, m);
                     a[0] += xv.re;
                     a[1] += xv.im;
@@ -1859,33 +1967,38 @@ struct ExactChi2 {
             a_re = aa.re;
             a_im = aa.im;
         }
+        const unsigned long long tp1 = prof ? __builtin_amdgcn_s_memtime() : 0;
+        if (prof) pc[0] += tp1 - tp0;
         // weighted_norm2(model .- data, weight) / N  (src/Modulation.jl:299-305, 325)
         double s[1];
         const c64 aa = {a_re, a_im};
-        cr_sum<1>(
-            [&](long long i, double (&a)[1]) {
-                c64 m;
-                double w;
-                if (mcg) {  // the same thread wrote element i in the first pass
-                    int st;
-                    if (!valid(V, i, st)) return;
-                    w = weight_of(st);
-                    m = c64{mcg[i - s0].re, mcg[i - s0].im};
-                } else {
+        auto resid = [&](const c64 &m, const c64 &dd, double w, double (&a)[1]) {
+            c64 mm = cmul(aa, m);
+            if (OFFS) {
+                mm.re = c_re + mm.re;
+                mm.im = c_im + mm.im;
+            }
+            const double rr = mm.re - dd.re, ri = mm.im - dd.im;
+            a[0] += w * (rr * rr + ri * ri);
+        };
+        if (mcg) {  // the model the same thread wrote for element i in the first pass
+            cr_sum2<1>([&](long long i, Raw &r) { load_res(V, i, r); },
+                       [&](long long i, const Raw &r, double (&a)[1]) {
+                           if (!valid_st(V, r.st)) return;
+                           resid(r.f, r.d, weight_of(r.st), a);
+                       },
+                       s);
+        } else {
+            cr_sum<1>(
+                [&](long long i, double (&a)[1]) {
                     c64 p;
+                    double w;
                     if (!load(V, i, p, w)) return;
-                    m = model(V, i, p, b, phi);
-                }
-                c64 mm = cmul(aa, m);
-                if (OFFS) {
-                    mm.re = c_re + mm.re;
-                    mm.im = c_im + mm.im;
-                }
-                const c64 dd = d_of(V, doff + i);
-                const double rr = mm.re - dd.re, ri = mm.im - dd.im;
-                a[0] += w * (rr * rr + ri * ri);
-            },
-            s);
+                    resid(model(V, i, p, b, phi), d_of(V, doff + i), w, a);
+                },
+                s);
+        }
+        if (prof) pc[1] += __builtin_amdgcn_s_memtime() - tp1;
         return s[0] / nvalid;
     }
 };
@@ -1912,6 +2025,8 @@ __device__ __forceinline__ void setup_exact(F &f, const Problem &pb, long long k
     f.x = x;
     f.nbar = 0;
     f.sync_fail = false;
+    f.prof = (pb.flags & F_PROF) != 0;
+    f.pc[0] = f.pc[1] = f.pc[2] = 0;
     if (pb.win > 0) {
         double c[1];
         f.cr_sum([&](long long i, double (&a)[1]) {
@@ -1966,10 +2081,17 @@ __global__ __launch_bounds__(EXACT_WG) void k_fit_exact(Problem pb, const Info *
         f.nfev = 0;
         double x[2];
         int status = ST_EXACT | extra_status;
+        const unsigned long long tf = f.prof ? __builtin_amdgcn_s_memtime() : 0;
         drive_fit(f, pb, x, status, nwx[threadIdx.x >> 6]);
         const double chi2 = f(x);
         if (g == 0 && threadIdx.x == 0)
             store_param(out, raw, k, f.c_re, f.c_im, f.a_re, f.a_im, x[0], x[1], chi2, f.nfev, status);
+        if (f.prof && threadIdx.x == 0) {
+            atomicAdd(&g_fitprof[0], f.pc[0]);
+            atomicAdd(&g_fitprof[1], f.pc[1]);
+            atomicAdd(&g_fitprof[2], f.pc[2]);
+            atomicAdd(&g_fitprof[3], __builtin_amdgcn_s_memtime() - tf);
+        }
         return;
     }
     const long long total = list ? (long long)(*count) : pb.P;

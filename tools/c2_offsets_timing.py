@@ -15,7 +15,11 @@ import gpdemod_loader  # noqa: E402
 import synth  # noqa: E402
 
 gpd = gpdemod_loader.load()
-B = synth.make_batch(100000, 32, seed=42, offsets=True)
+# --mjd: real exposures' timestamps, t = TIME·1e-6 + 86400·MJD (src/GPPupilDemodulation.jl:139),
+# so ω t ≈ 3.3e10 rad and every χ² evaluation of the exact path reduces its arguments by
+# Payne–Hanek
+T0 = 86400.0 * 60000.0 if "--mjd" in sys.argv else 0.0
+B = synth.make_batch(100000, 32, seed=42, offsets=True, t0=T0)
 args = (B["t"], B["d"], B["fc"], B["fc_of_pixel"])
 cases = [(False, "auto", None)] + [(off, "exact", g) for off in (False, True)
                                      for g in ("1", "2", "4", "8")]
@@ -28,6 +32,6 @@ for off, method, g in cases:
     t0 = time.perf_counter()
     for _ in range(3):
         gpd.fit_batch(*args, fitoffsets=off, method=method)
-    print(json.dumps({"fitoffsets": off, "method": method, "G": g,
+    print(json.dumps({"t0": T0, "fitoffsets": off, "method": method, "G": g,
                       "ms": round((time.perf_counter() - t0) / 3 * 1e3, 3),
                       "kernels_ms": {k: round(v, 3) for k, v in gpd.timings(0).items()}}))
