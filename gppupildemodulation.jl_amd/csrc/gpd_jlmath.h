@@ -56,30 +56,28 @@ JLM_FN double jlm_fma(double a, double b, double c) { return __builtin_fma(a, b,
 /* ---- argument reduction (base/special/rem_pio2.jl) -------------------------------------- */
 
 /* 1/(2π) in 64-bit words, most significant first: 1/(2π) = Σ_i W_i 2^(-64(i+1)), i = 0..18
- * (oracle/tools/inv2pi.py derives them from an exact integer expansion of π). */
+ * (oracle/tools/inv2pi.py derives them from an exact integer expansion of π).  An indexed table
+ * (device: constant memory) — a switch compiled to ~200 compare-and-branch instructions per
+ * Payne–Hanek reduction on the device. */
+#define JLM_INV2PI_WORDS                                                                      \
+    {0x28be60db9391054aull, 0x7f09d5f47d4d3770ull, 0x36d8a5664f10e410ull,                    \
+     0x7f9458eaf7aef158ull, 0x6dc91b8e909374b8ull, 0x01924bba82746487ull,                    \
+     0x3f877ac72c4a69cfull, 0xba208d7d4baed121ull, 0x3a671c09ad17df90ull,                    \
+     0x4e64758e60d4ce7dull, 0x272117e2ef7e4a0eull, 0xc7fe25fff7816603ull,                    \
+     0xfbcbc462d6829b47ull, 0xdb4d9fb3c9f2c26dull, 0xd3d18fd9a797fa8bull,                    \
+     0x5d49eeb1faf97c5eull, 0xcf41ce7de294a4baull, 0x9afed7ec47e35742ull,                    \
+     0x1580cc11bf1edaeaull}
+#if defined(__HIP__)
+__device__ __constant__ static const uint64_t jlm_inv2pi_dev[19] = JLM_INV2PI_WORDS;
+#endif
+static const uint64_t jlm_inv2pi_host[19] = JLM_INV2PI_WORDS;
 JLM_FN uint64_t jlm_inv2pi(int i) {
-    switch (i) {
-    case 0: return 0x28be60db9391054aull;
-    case 1: return 0x7f09d5f47d4d3770ull;
-    case 2: return 0x36d8a5664f10e410ull;
-    case 3: return 0x7f9458eaf7aef158ull;
-    case 4: return 0x6dc91b8e909374b8ull;
-    case 5: return 0x01924bba82746487ull;
-    case 6: return 0x3f877ac72c4a69cfull;
-    case 7: return 0xba208d7d4baed121ull;
-    case 8: return 0x3a671c09ad17df90ull;
-    case 9: return 0x4e64758e60d4ce7dull;
-    case 10: return 0x272117e2ef7e4a0eull;
-    case 11: return 0xc7fe25fff7816603ull;
-    case 12: return 0xfbcbc462d6829b47ull;
-    case 13: return 0xdb4d9fb3c9f2c26dull;
-    case 14: return 0xd3d18fd9a797fa8bull;
-    case 15: return 0x5d49eeb1faf97c5eull;
-    case 16: return 0xcf41ce7de294a4baull;
-    case 17: return 0x9afed7ec47e35742ull;
-    case 18: return 0x1580cc11bf1edaeaull;
-    default: return 0;
-    }
+    if (i < 0 || i > 18) return 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    return jlm_inv2pi_dev[i];
+#else
+    return jlm_inv2pi_host[i];
+#endif
 }
 
 /* Julia's shifts: a negative count shifts the other way, a count ≥ the width gives 0 */

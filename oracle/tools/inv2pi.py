@@ -48,6 +48,6 @@ def hypot_thresholds() -> dict:
 
 
 if __name__ == "__main__":
-    for i, w in enumerate(inv2pi_words()):
-        print(f"    case {i}: return 0x{w:016x}ull;")
+    ws = inv2pi_words()  # the JLM_INV2PI_WORDS table of csrc/gpd_jlmath.h
+    print(",\n".join(", ".join(f"0x{w:016x}ull" for w in ws[i:i + 3]) for i in range(0, len(ws), 3)))
     print(hypot_thresholds())
