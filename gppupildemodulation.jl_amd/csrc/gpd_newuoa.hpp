@@ -276,6 +276,7 @@ struct Newuoa {
             int isave = 0;
             const int iu = 49;
             const double dang = kTwoPi / (double)(iu + 1);
+            #pragma unroll 7  // 49 = 7·7 trial angles: independent values, ILP across 7
             for (int i = 1; i <= iu; ++i) {
                 const double cth = kAngCos[i], sth = kAngSin[i];
                 qnew = (sg + cf * cth) * cth + (dg + dhs * cth) * sth;
@@ -419,6 +420,7 @@ struct Newuoa {
             int isave = 0;
             const int iu = 49;
             const double dang = kTwoPi / (double)(iu + 1);
+            #pragma unroll 7  // 49 = 7·7 trial angles: independent values, ILP across 7
             for (int i = 1; i <= iu; ++i) {
                 const double cth = kAngCos[i], sth = kAngSin[i];
                 tau = cf1 + (cf2 + cf4 * cth) * cth + (cf3 + cf5 * cth) * sth;
@@ -644,6 +646,7 @@ struct Newuoa {
             const int iu = 49;
             const double dang = kTwoPi / (double)(iu + 1);
             par[0] = 1.0;
+            #pragma unroll 7  // 49 = 7·7 trial angles: independent values, ILP across 7
             for (int i = 1; i <= iu; ++i) {
                 par[1] = kAngCos[i];
                 par[2] = kAngSin[i];
