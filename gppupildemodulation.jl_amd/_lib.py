@@ -139,7 +139,8 @@ def check(rc: int, errbuf=None):
         raise GpdError(rc, f"{L.gpd_strerror(rc).decode()}: {msg}")
 
 
-LIBM_FN = {"sin": 0, "cos": 1, "sincos": 2, "atan": 3, "atan2": 4, "hypot": 5, "rem_pio2": 6, "hypot_nb": 7}
+LIBM_FN = {"sin": 0, "cos": 1, "sincos": 2, "atan": 3, "atan2": 4, "hypot": 5, "rem_pio2": 6, "hypot_nb": 7,
+           "sin_sel": 8, "sincos_sel": 9}
 
 
 def libm_eval(fn: str, x, y=None, device: int = 0):
@@ -148,7 +149,7 @@ def libm_eval(fn: str, x, y=None, device: int = 0):
     code = LIBM_FN[fn]
     x = np.ascontiguousarray(x, dtype=np.float64).ravel()
     yy = None if y is None else np.ascontiguousarray(y, dtype=np.float64).ravel()
-    width = {2: 2, 6: 3}.get(code, 1)
+    width = {2: 2, 6: 3, 9: 2}.get(code, 1)
     out = np.empty(x.size * width)
     check(load().gpd_libm_eval(code, x.size, ptr(x), ptr(yy), ptr(out), device))
     return out.reshape(-1, width) if width > 1 else out

@@ -1069,7 +1069,7 @@ int gpd_process_volt(int64_t n_samples, const double *t, const float *volt, int6
 int gpd_libm_eval(int fn, int64_t n, const double *x, const double *y, double *out, int device) {
     char *errbuf = nullptr;
     size_t errlen = 0;
-    if (fn < 0 || fn > 7 || n < 0 || (n > 0 && (!x || !out)) ||
+    if (fn < 0 || fn > 9 || n < 0 || (n > 0 && (!x || !out)) ||
         ((fn == 4 || fn == 5 || fn == 7) && n > 0 && !y))
         return GPD_E_ARG;
     const int ndev = gpd_device_count();
@@ -1077,7 +1077,7 @@ int gpd_libm_eval(int fn, int64_t n, const double *x, const double *y, double *o
     if (device < 0 || device >= ndev) return GPD_E_ARG;
     if (n == 0) return GPD_OK;
     HIP_TRY(hipSetDevice(device));
-    const int width = fn == 2 ? 2 : fn == 6 ? 3 : 1;
+    const int width = (fn == 2 || fn == 9) ? 2 : fn == 6 ? 3 : 1;
     double *dx = nullptr, *dy = nullptr, *dout = nullptr;
     auto release = [&]() {
         (void)hipFree(dx);

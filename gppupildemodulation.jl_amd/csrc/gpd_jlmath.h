@@ -324,6 +324,173 @@ JLM_FN void jl_sincos(double x, double *s, double *c) {
     }
 }
 
+/* ---- branch-free forms, one argument regime each ----------------------------------------
+ * The same operations as jl_sin / jl_sincos above, with every branch of the regime evaluated and
+ * the result selected (no control flow), so that a batch of independent arguments compiles to
+ * one basic block the scheduler can interleave (the exact evaluator's per-sample model at one
+ * wave per SIMD).  The caller tests the regime (jlm_*_in) and otherwise calls the general
+ * function; inside its regime each form gives that function's bits. */
+JLM_FN uint64_t jlm_inv2pi_nb(int i) {
+    const int j = i < 0 ? 0 : (i > 18 ? 18 : i);
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint64_t v = jlm_inv2pi_dev[j];
+#else
+    const uint64_t v = jlm_inv2pi_host[j];
+#endif
+    return (i < 0 || i > 18) ? 0ull : v;
+}
+JLM_FN int jlm_clz128_nb(jlm_u128 x) {
+    const uint64_t hi = (uint64_t)(x >> 64), lo = (uint64_t)x;
+    const int ch = __builtin_clzll(hi | 1ull), cl = __builtin_clzll(lo | 1ull);
+    return hi ? ch : (lo ? 64 + cl : 128);
+}
+/* jlm_shr128 for |n| < 128 */
+JLM_FN jlm_u128 jlm_shr128_nb(jlm_u128 x, int n) {
+    const jlm_u128 r = x >> (n & 127), l = x << ((-n) & 127);
+    return n >= 0 ? r : l;
+}
+JLM_FN void jlm_fromfraction_nb(jlm_i128 f, double *z1, double *z2) {
+    const uint64_t s = (uint64_t)(f < 0) << 63;
+    const jlm_u128 x = f < 0 ? (jlm_u128)0 - (jlm_u128)f : (jlm_u128)f;
+    const jlm_u128 xs = x | (jlm_u128)(x == 0); /* f = 0: any shape, the result is selected */
+    const int n1 = 128 - jlm_clz128_nb(xs);
+    const uint64_t m1 = (uint64_t)jlm_shr128_nb(xs, n1 - 26) << 27;
+    const uint64_t d1 = (uint64_t)(int64_t)(n1 - 128 + 1021) << 52;
+    const jlm_u128 x2 = xs - jlm_shr128_nb((jlm_u128)m1, 53 - n1);
+    const jlm_u128 x2s = x2 | (jlm_u128)(x2 == 0);
+    const int n2 = 128 - jlm_clz128_nb(x2s);
+    const uint64_t m2 = (uint64_t)jlm_shr128_nb(x2s, n2 - 53);
+    const uint64_t d2 = (uint64_t)(int64_t)(n2 - 128 + 1021) << 52;
+    *z1 = f == 0 ? 0.0 : jlm_from_bits(s | (d1 + m1));
+    *z2 = (f == 0 || x2 == 0) ? 0.0 : jlm_from_bits(s | (d2 + m2));
+}
+/* jlm_paynehanek; regime |x| ≥ 2^20·π/2, finite */
+JLM_FN int jlm_paynehanek_nb(double x, double *yhi, double *ylo) {
+    const uint64_t u = jlm_bits(x);
+    const uint64_t X = (u & 0x000fffffffffffffull) | (1ull << 52);
+    const int k = (int)((u & 0x7ff0000000000000ull) >> 52) - 1023 - 52;
+    const int idx = k >> 6;
+    const int shift = k - idx * 64; /* 0..63; shift 0 takes the words unshifted */
+    const uint64_t v0 = jlm_inv2pi_nb(idx), v1 = jlm_inv2pi_nb(idx + 1),
+                   v2 = jlm_inv2pi_nb(idx + 2), v3 = jlm_inv2pi_nb(idx + 3);
+    const uint64_t a1 = (v0 << shift) | ((v1 >> 1) >> (63 - shift));
+    const uint64_t a2 = (v1 << shift) | ((v2 >> 1) >> (63 - shift));
+    const uint64_t a3 = (v2 << shift) | ((v3 >> 1) >> (63 - shift));
+    const jlm_u128 w1 = (jlm_u128)(X * a1) << 64;
+    const jlm_u128 w2 = (jlm_u128)X * a2;
+    const jlm_u128 w3 = ((jlm_u128)X * a3) >> 64;
+    const jlm_u128 wp = w1 + w2 + w3;
+    const jlm_u128 w = __builtin_signbit(x) ? (jlm_u128)0 - wp : wp;
+    const int q = (int)(((int64_t)(uint64_t)(w >> 125) + 1) >> 1);
+    const jlm_i128 f = (jlm_i128)(w << 2);
+    double zhi, zlo;
+    jlm_fromfraction_nb(f, &zhi, &zlo);
+    const double pio2 = 1.5707963267948966, pio2_hi = 1.5707963407039642,
+                 pio2_lo = -1.3909067614167116e-8;
+    const double yh = (zhi + zlo) * pio2;
+    *yhi = yh;
+    *ylo = (((zhi * pio2_hi - yh) + zhi * pio2_lo) + zlo * pio2_hi) + zlo * pio2_lo;
+    return q;
+}
+/* jlm_cwext; regime 9π/4 ≲ |x| < 2^20·π/2 (every iteration evaluated, the needed one kept) */
+JLM_FN int jlm_cwext_nb(double x, uint32_t xhp, double *yhi, double *ylo) {
+    const double fn = __builtin_rint(x * 0x1.45f306dc9c883p-1);
+    const double r1 = jlm_fma(-fn, JLM_PIO2_1, x);
+    const double w1 = fn * JLM_PIO2_1T;
+    const uint32_t j = xhp >> 20;
+    const double y11 = r1 - w1;
+    const uint32_t i1 = j - ((jlm_highword(y11) >> 20) & 0x7ffu);
+    const double w2a = fn * JLM_PIO2_2;
+    const double r2 = r1 - w2a;
+    const double w2 = jlm_fma(fn, JLM_PIO2_2T, -((r1 - r2) - w2a));
+    const double y12 = r2 - w2;
+    const uint32_t i2 = j - ((jlm_highword(y12) >> 20) & 0x7ffu);
+    const double w3a = fn * JLM_PIO2_3;
+    const double r3 = r2 - w3a;
+    const double w3 = jlm_fma(fn, JLM_PIO2_3T, -((r2 - r3) - w3a));
+    const double y13 = r3 - w3;
+    const int it = i1 > 16u ? (i2 > 49u ? 3 : 2) : 1;
+    const double r = it == 1 ? r1 : (it == 2 ? r2 : r3);
+    const double w = it == 1 ? w1 : (it == 2 ? w2 : w3);
+    const double y1 = it == 1 ? y11 : (it == 2 ? y12 : y13);
+    *yhi = y1;
+    *ylo = (r - y1) - w;
+    return (int)fn;
+}
+/* jlm_sin_kernel with `plain` a value: both forms evaluated */
+JLM_FN double jlm_sin_kernel_sel(double hi, double lo, int plain) {
+    const double y2 = hi * hi, y4 = y2 * y2;
+    const double r = jlm_fma(y2, jlm_fma(y2, JLM_DS4, JLM_DS3), JLM_DS2) +
+                     y2 * y4 * jlm_fma(y2, JLM_DS6, JLM_DS5);
+    const double y3 = y2 * hi;
+    const double p = hi + y3 * (JLM_DS1 + y2 * r);
+    const double d = hi - ((y2 * (0.5 * lo - y3 * r) - lo) - y3 * JLM_DS1);
+    return plain ? p : d;
+}
+JLM_FN double jlm_sin_quadrant(int n, double hi, double lo) {
+    const double si = jlm_sin_kernel(hi, lo, 0), co = jlm_cos_kernel(hi, lo);
+    n &= 3;
+    return n == 0 ? si : (n == 1 ? co : (n == 2 ? -si : -co));
+}
+/* regimes of jl_sin for |x| ≥ π/4: Payne–Hanek (MJD-scale ωt) and Cody–Waite extended */
+JLM_FN int jlm_sin_ph_in(double x) {
+    const uint32_t xhp = jlm_poshighword(x);
+    return xhp >= 0x413921fbu && xhp < 0x7ff00000u;
+}
+JLM_FN int jlm_sin_cwx_in(double x) {
+    const uint32_t xhp = jlm_poshighword(x);
+    return xhp > 0x401c463bu && xhp < 0x413921fbu;
+}
+JLM_FN double jl_sin_ph_nb(double x) {
+    double hi, lo;
+    const int n = jlm_paynehanek_nb(x, &hi, &lo);
+    return jlm_sin_quadrant(n, hi, lo);
+}
+JLM_FN double jl_sin_cwx_nb(double x) {
+    double hi, lo;
+    const int n = jlm_cwext_nb(x, jlm_poshighword(x), &hi, &lo);
+    return jlm_sin_quadrant(n, hi, lo);
+}
+/* jl_sincos for |x| ≲ 9π/4 outside the extended-precision points (|x| ≈ π/2, π, 3π/2, 2π) */
+JLM_FN int jlm_sincos_small_in(double x) {
+    const uint32_t xhp = jlm_poshighword(x);
+    const int ext = xhp <= 0x400f6a7au ? (xhp & 0xfffffu) == 0x921fbu
+                                       : (xhp == 0x4012d97cu || xhp == 0x401921fbu);
+    return xhp <= 0x401c463bu && !(__builtin_fabs(x) >= JLM_PI_4 && ext);
+}
+JLM_FN void jl_sincos_small_nb(double x, double *s, double *c) {
+    const uint32_t xhp = jlm_poshighword(x);
+    const int plain = __builtin_fabs(x) < JLM_PI_4;
+    const double fm = xhp <= 0x4002d97cu ? 1.0
+                      : xhp <= 0x400f6a7au ? 2.0
+                      : xhp <= 0x4015fdbcu ? 3.0
+                                           : 4.0;
+    const double fn = x > 0.0 ? fm : -fm;
+    const double z = jlm_fma(-fn, JLM_PIO2_1, x);
+    const double y1 = jlm_fma(-fn, JLM_PIO2_1T, z);
+    const double l1 = jlm_fma(-fn, JLM_PIO2_1T, z - y1);
+    const double hi = plain ? x : y1, lo = plain ? 0.0 : l1;
+    const int n = plain ? 0 : ((int)fn & 3);
+    const double si = jlm_sin_kernel_sel(hi, lo, plain), co = jlm_cos_kernel(hi, lo);
+    const double ss = n == 0 ? si : (n == 1 ? co : (n == 2 ? -si : -co));
+    const double cc = n == 0 ? co : (n == 1 ? -si : (n == 2 ? -co : si));
+    *s = x == 0.0 ? x : ss;
+    *c = x == 0.0 ? 1.0 : cc;
+}
+/* per-argument dispatch onto the forms above (the tests' view of them: = jl_sin, jl_sincos) */
+JLM_FN double jl_sin_sel(double x) {
+    if (jlm_sin_ph_in(x)) return jl_sin_ph_nb(x);
+    if (jlm_sin_cwx_in(x)) return jl_sin_cwx_nb(x);
+    return jl_sin(x);
+}
+JLM_FN void jl_sincos_sel(double x, double *s, double *c) {
+    if (jlm_sincos_small_in(x)) {
+        jl_sincos_small_nb(x, s, c);
+        return;
+    }
+    jl_sincos(x, s, c);
+}
+
 /* ---- atan, atan(y, x) (base/special/trig.jl, msun s_atan.c / e_atan2.c) ----------------- */
 JLM_FN double jlm_atan_hi(int id) {
     return id == 0   ? 4.63647609000806093515e-01

@@ -1763,11 +1763,56 @@ struct ExactChi2 {
             w = 1.0;
         }
     }
-    __device__ __forceinline__ c64 model_t(double t, const c64 &p, double b, double phi) const {
-        double th = pb->omega * t;
-        th = th + phi;
-        const double beta = b * jl_sin(th);
-        return cmul(p, cisj(beta));  // power * exp(ȷ b sin(ωt+ϕ)) (src/Modulation.jl:137)
+    // model() of U loaded samples at once: when every lane's U arguments lie in one regime of
+    // jl_sin (MJD-scale Payne–Hanek, Cody–Waite extended) and of jl_sincos (|β| ≲ 9π/4), the
+    // regime's branch-free form runs for all U in one basic block; otherwise the general
+    // functions.  Either way each sample's model has model()'s bits (gpd_jlmath.h).
+    template <int U>
+    __device__ __forceinline__ void model_batch(const Raw (&X)[U], double b, double phi,
+                                                c64 (&m)[U]) const {
+        double th[U], s[U], be[U];
+        int ph = 1, cw = 1, sm = 1;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            th[u] = pb->omega * X[u].t;
+            th[u] = th[u] + phi;
+            ph &= jlm_sin_ph_in(th[u]);
+            cw &= jlm_sin_cwx_in(th[u]);
+        }
+        if (__all(ph)) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) s[u] = jl_sin_ph_nb(th[u]);
+        } else if (__all(cw)) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) s[u] = jl_sin_cwx_nb(th[u]);
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) s[u] = jl_sin(th[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            be[u] = b * s[u];
+            sm &= jlm_sincos_small_in(be[u]);
+        }
+        c64 e[U];
+        if (__all(sm)) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                double ss, cc;
+                jl_sincos_small_nb(be[u], &ss, &cc);
+                e[u] = c64{cc, ss};  // cisj: exp(ȷβ), β = 0 → (1, β)
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) e[u] = cisj(be[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            c64 p;
+            double w;
+            pw_of(X[u], p, w);
+            m[u] = cmul(p, e[u]);  // power * exp(ȷ b sin(ωt+ϕ)) (src/Modulation.jl:137)
+        }
     }
     __device__ __forceinline__ c64 model(const View &v, long long i, const c64 &p, double b,
                                          double phi) const {
@@ -1862,6 +1907,15 @@ struct ExactChi2 {
     // sums as cr_sum (one wave per SIMD: nothing else hides the memory latency of a chain).
     template <int NV, int U = CR_U, class L, class A>
     __device__ __forceinline__ void cr_sum2(L &&load, A &&accum, double (&tot)[NV]) {
+        cr_sum2m<NV, U>(
+            load, [](const Raw (&)[U], c64 (&)[U]) {},
+            [&](long long i, const Raw &r, const c64 &, double (&a)[NV]) { accum(i, r, a); }, tot);
+    }
+    // cr_sum2 with a batch step: batch(X, m) computes the U samples' models together (one basic
+    // block, independent chains for the scheduler) before accum(i, X[u], m[u], acc) adds them
+    // in chain order.
+    template <int NV, int U = CR_U, class L, class B, class A>
+    __device__ __forceinline__ void cr_sum2m(L &&load, B &&batch, A &&accum, double (&tot)[NV]) {
         cr_sum_blocks<NV>(
             [&](long long i0, double (&acc)[NV]) {
                 const int M = i0 < s1 ? (int)((s1 - 1 - i0) / CR_SLOTS + 1) : 0;
@@ -1875,10 +1929,12 @@ struct ExactChi2 {
                     }
                 };
                 auto run = [&](const Raw (&X)[U], int m0) {
+                    c64 mb[U];
+                    batch(X, mb);
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         if (m0 + u >= M) break;
-                        accum(i0 + (long long)(m0 + u) * CR_SLOTS, X[u], acc);
+                        accum(i0 + (long long)(m0 + u) * CR_SLOTS, X[u], mb[u], acc);
                     }
                 };
                 issue(A_, 0);
@@ -1902,14 +1958,14 @@ struct ExactChi2 {
         const unsigned long long tp0 = prof ? __builtin_amdgcn_s_memtime() : 0;
         if (OFFS) {
             double v[8];  // a11, a12(2), a22, b1(2), b2(2)
-            cr_sum2<8>(
+            cr_sum2m<8>(
                 [&](long long i, Raw &r) { load_raw(V, i, r); },
-                [&](long long i, const Raw &r, double (&a)[8]) {
+                [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch(X, b, phi, mb); },
+                [&](long long i, const Raw &r, const c64 &m, double (&a)[8]) {
                     if (!valid_st(V, r.st)) return;
                     c64 p;
                     double w;
                     pw_of(r, p, w);
-                    const c64 m = model_t(r.t, p, b, phi);
                     if (mcg) {
                         mcg[i - s0].re = m.re;
                         mcg[i - s0].im = m.im;
@@ -1941,14 +1997,14 @@ struct ExactChi2 {
             a_im = aa.im;
         } else {
             double v[4];  // num(2), den(2)
-            cr_sum2<4>(
+            cr_sum2m<4>(
                 [&](long long i, Raw &r) { load_raw(V, i, r); },
-                [&](long long i, const Raw &r, double (&a)[4]) {
+                [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch(X, b, phi, mb); },
+                [&](long long i, const Raw &r, const c64 &m, double (&a)[4]) {
                     if (!valid_st(V, r.st)) return;
                     c64 p;
                     double w;
                     pw_of(r, p, w);
-                    const c64 m = model_t(r.t, p, b, phi);
                     if (mcg) {
                         mcg[i - s0].re = m.re;
                         mcg[i - s0].im = m.im;
@@ -2311,6 +2367,14 @@ __global__ __launch_bounds__(256) void k_libm(int fn, long long n, const double 
     case 4: out[i] = jl_atan2(x[i], y[i]); break;
     case 5: out[i] = jl_hypot(x[i], y[i]); break;
     case 7: out[i] = jl_hypot_nb(x[i], y[i]); break;
+    case 8: out[i] = jl_sin_sel(x[i]); break;
+    case 9: {
+        double s, c;
+        jl_sincos_sel(x[i], &s, &c);
+        out[2 * i] = s;
+        out[2 * i + 1] = c;
+        break;
+    }
     default: {
         double hi, lo;
         const int q = jl_rem_pio2(x[i], &hi, &lo);

@@ -281,7 +281,10 @@ int gpd_synth_fill_dev(int64_t n_samples, int64_t n_pixels, int64_t pixel_offset
  * the restatement the exact evaluator applies per sample, src/Modulation.jl:137,388,419-421,
  * src/Faint.jl:95-97), for host-vs-device bit-for-bit checks.  fn: 0 sin, 1 cos, 2 sincos (out
  * holds n (s, c) pairs), 3 atan, 4 atan(x[i], y[i]), 5 hypot(x[i], y[i]), 6 rem_pio2 (n triples
- * (quadrant, hi, lo)), 7 hypot(x[i], y[i]) in its branch-free form (the faint statistics').  Host arrays (y may be NULL for the one-argument functions), synchronous.
+ * (quadrant, hi, lo)), 7 hypot(x[i], y[i]) in its branch-free form (the faint statistics'),
+ * 8 sin and 9 sincos (pairs) through the branch-free per-regime forms the exact evaluator
+ * batches (= fn 0 and 2).  Host arrays (y may be NULL for the one-argument functions),
+ * synchronous.
  */
 int gpd_libm_eval(int fn, int64_t n, const double *x, const double *y, double *out, int device);
 

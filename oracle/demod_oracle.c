@@ -590,7 +590,8 @@ int oracle_fit_batch(int64_t n_samples, int64_t n_pixels, const double *t, const
 
 /* Elementwise evaluation of the shared Julia-libm restatement (tests/test_jlmath.py).
  * fn: 0 sin, 1 cos, 2 sincos → (s, c) pairs in out[2i..2i+1], 3 atan, 4 atan(x[i], y[i]),
- *     5 hypot(x[i], y[i]), 6 rem_pio2 → (n, hi, lo) triples in out[3i..3i+2] */
+ *     5 hypot(x[i], y[i]), 6 rem_pio2 → (n, hi, lo) triples in out[3i..3i+2], 7 hypot_nb,
+ *     8 sin through the branch-free regime forms, 9 sincos likewise (pairs) */
 int oracle_jl_eval(int fn, int64_t n, const double *x, const double *y, double *out) {
     for (int64_t i = 0; i < n; ++i) {
         switch (fn) {
@@ -601,6 +602,8 @@ int oracle_jl_eval(int fn, int64_t n, const double *x, const double *y, double *
         case 4: out[i] = jl_atan2(x[i], y[i]); break;
         case 5: out[i] = jl_hypot(x[i], y[i]); break;
         case 7: out[i] = jl_hypot_nb(x[i], y[i]); break;
+        case 8: out[i] = jl_sin_sel(x[i]); break;
+        case 9: jl_sincos_sel(x[i], &out[2 * i], &out[2 * i + 1]); break;
         case 6: {
             double hi, lo;
             const int q = jl_rem_pio2(x[i], &hi, &lo);

@@ -162,7 +162,8 @@ def mean_var_power_series(states, d, onlyhigh=False):
     return m5, w5
 
 
-JL_FN = {"sin": 0, "cos": 1, "sincos": 2, "atan": 3, "atan2": 4, "hypot": 5, "rem_pio2": 6, "hypot_nb": 7}
+JL_FN = {"sin": 0, "cos": 1, "sincos": 2, "atan": 3, "atan2": 4, "hypot": 5, "rem_pio2": 6, "hypot_nb": 7,
+         "sin_sel": 8, "sincos_sel": 9}
 
 
 def jl_eval(fn, x, y=None):
@@ -172,7 +173,7 @@ def jl_eval(fn, x, y=None):
     code = JL_FN[fn]
     x = np.ascontiguousarray(x, dtype=np.float64).ravel()
     yy = None if y is None else np.ascontiguousarray(y, dtype=np.float64).ravel()
-    width = {2: 2, 6: 3}.get(code, 1)
+    width = {2: 2, 6: 3, 9: 2}.get(code, 1)
     out = np.empty(x.size * width)
     if lib().oracle_jl_eval(code, x.size, _ptr(x), _ptr(yy), _ptr(out)) != 0:
         raise ValueError(fn)

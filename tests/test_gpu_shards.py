@@ -78,3 +78,39 @@ def test_records_independent_of_batch_and_grid(gpu, monkeypatch):
     for upw in ("1", "2", "3", "7"):
         monkeypatch.setenv("GPD_UPW", upw)
         _same(gpu.fit_batch(*args, method="harmonic"), ref)
+
+
+def test_full_length_shard_invariance_device(gpu):
+    """At the full exposure length (N = 1e5, the C3/C4 series) on device buffers: the records of
+    a 512-series shard taken from the middle of a 2048-series batch (offset 1024, as rank 2 of 4
+    would hold it) equal the batch's own records for those series, bit for bit — the C4 split's
+    property at C4's series length, through gpd_fit_batch_dev."""
+    import ctypes
+    import torch
+    L = gpu.load()
+    dev = torch.device("cuda", 0)
+    sptr = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    N, P = 100_000, 2048
+    t = torch.empty(N, dtype=torch.float64, device=dev)
+    d = torch.empty((P, N, 2), dtype=torch.float64, device=dev)
+    fc = torch.empty((P // 4, N, 2), dtype=torch.float64, device=dev)
+    fcop = torch.empty(P, dtype=torch.int32, device=dev)
+    gpu._lib.check(L.gpd_synth_fill_dev(N, P, 0, 7, 0.0, 0.002, 0.1, 0, gpu.M_2PI, t.data_ptr(),
+                                        d.data_ptr(), N, fc.data_ptr(), N, fcop.data_ptr(), None,
+                                        0, sptr))
+    err = ctypes.create_string_buffer(512)
+
+    def fit(p0, p1):
+        out = torch.empty((p1 - p0, 64), dtype=torch.uint8, device=dev)
+        fo = (fcop[p0:p1] - p0 // 4).contiguous()
+        gpu._lib.check(L.gpd_fit_batch_dev(N, p1 - p0, t.data_ptr(), d[p0].data_ptr(), N,
+                                           fc[p0 // 4].data_ptr(), (p1 - p0) // 4, N,
+                                           fo.data_ptr(), None, gpu.M_2PI, None,
+                                           gpu.GPD_RECENTER, 60, out.data_ptr(), None, N, 0,
+                                           sptr, err, len(err)), err)
+        torch.cuda.synchronize(dev)
+        return out.cpu().numpy().reshape(-1).view(gpu.PARAM_DTYPE)
+
+    whole = fit(0, P)
+    _same(fit(1024, 1536), whole[1024:1536])
+    assert not np.any(whole["status"] & gpu.GPD_ST_NAN)

@@ -231,3 +231,40 @@ def test_device_libm_equals_oracle_bitwise(gpu, oracle):
         assert same_bits(gpu.libm_eval(fn, xs, ys), oracle.jl_eval(fn, xs, ys)), fn
     hx, hy = _hypot_args(rng, 200000)
     assert same_bits(gpu.libm_eval("hypot_nb", hx, hy), oracle.jl_eval("hypot", hx, hy))
+
+
+def _trig_regime_args(rng, n):
+    """Arguments of every regime the branch-free forms cover and of their edges: MJD-scale ωt
+    (Payne–Hanek, shift 0 exponents included), Cody–Waite extended, |β| ≲ 9π/4 with the
+    extended-precision points π/2, π, 3π/2, 2π and their neighbours, ±0, tiny, inf, NaN."""
+    k = np.arange(1, 9) * (np.pi / 2)
+    near = np.concatenate([np.nextafter(k, np.inf), np.nextafter(k, -np.inf), k,
+                           k * (1 + 1e-7), k * (1 - 1e-7)])
+    edges = np.array([2.0 ** 20 * np.pi / 2, np.nextafter(2.0 ** 20 * np.pi / 2, 0), 9 * np.pi / 4,
+                      np.nextafter(9 * np.pi / 4, 0), np.nextafter(9 * np.pi / 4, 10), np.pi / 4,
+                      np.nextafter(np.pi / 4, 0), 0.0, -0.0, 5e-324, 1e-300, 2.0 ** -27,
+                      np.inf, -np.inf, np.nan, 2.0 ** 1023, 1.7e308])
+    shift0 = np.ldexp(1.0 + rng.random(2000), rng.integers(1, 16, 2000) * 64 + 11)  # k ≡ 0 mod 64
+    sets = [rng.uniform(3.2e10, 3.5e10, n) + rng.uniform(-np.pi, np.pi, n),  # MJD·ω + ϕ
+            np.exp(rng.uniform(np.log(7.0), np.log(1.6e6), n)) * rng.choice([-1, 1], n),
+            rng.uniform(-7.2, 7.2, n), rng.uniform(-2.6, 2.6, n),
+            np.exp(rng.uniform(np.log(1.7e6), 700, n // 4)), shift0, near, -near, edges, -edges]
+    return np.concatenate(sets)
+
+
+def test_branch_free_sin_sincos_equal_the_general_functions(oracle):
+    """jl_sin_ph_nb / jl_sin_cwx_nb / jl_sincos_small_nb (every branch of the regime evaluated,
+    the exact evaluator's batched model) give jl_sin's and jl_sincos's bits inside their regimes;
+    outside them the dispatch falls back to the general functions."""
+    x = _trig_regime_args(np.random.default_rng(29), 300000)
+    assert same_bits(oracle.jl_eval("sin_sel", x), oracle.jl_eval("sin", x))
+    assert same_bits(oracle.jl_eval("sincos_sel", x), oracle.jl_eval("sincos", x))
+
+
+@pytest.mark.gpu
+def test_device_branch_free_trig_equals_oracle(gpu, oracle):
+    """The device's branch-free regime forms (the exact evaluator's batched model) = jl_sin and
+    jl_sincos of the oracle, bit for bit, on every regime and edge."""
+    x = _trig_regime_args(np.random.default_rng(31), 200000)
+    assert same_bits(gpu.libm_eval("sin_sel", x), oracle.jl_eval("sin", x))
+    assert same_bits(gpu.libm_eval("sincos_sel", x), oracle.jl_eval("sincos", x))
