@@ -364,18 +364,23 @@ JLM_FN void jlm_fromfraction_nb(jlm_i128 f, double *z1, double *z2) {
     *z1 = f == 0 ? 0.0 : jlm_from_bits(s | (d1 + m1));
     *z2 = (f == 0 || x2 == 0) ? 0.0 : jlm_from_bits(s | (d2 + m2));
 }
-/* jlm_paynehanek; regime |x| ≥ 2^20·π/2, finite */
-JLM_FN int jlm_paynehanek_nb(double x, double *yhi, double *ylo) {
-    const uint64_t u = jlm_bits(x);
-    const uint64_t X = (u & 0x000fffffffffffffull) | (1ull << 52);
-    const int k = (int)((u & 0x7ff0000000000000ull) >> 52) - 1023 - 52;
+/* Payne–Hanek's three words of 2/π for the binade of biased exponent e (k = e - 1075; shift 0
+ * takes the words unshifted) */
+JLM_FN void jlm_ph_words(int e, uint64_t *a1, uint64_t *a2, uint64_t *a3) {
+    const int k = e - 1023 - 52;
     const int idx = k >> 6;
-    const int shift = k - idx * 64; /* 0..63; shift 0 takes the words unshifted */
+    const int shift = k - idx * 64;
     const uint64_t v0 = jlm_inv2pi_nb(idx), v1 = jlm_inv2pi_nb(idx + 1),
                    v2 = jlm_inv2pi_nb(idx + 2), v3 = jlm_inv2pi_nb(idx + 3);
-    const uint64_t a1 = (v0 << shift) | ((v1 >> 1) >> (63 - shift));
-    const uint64_t a2 = (v1 << shift) | ((v2 >> 1) >> (63 - shift));
-    const uint64_t a3 = (v2 << shift) | ((v3 >> 1) >> (63 - shift));
+    *a1 = (v0 << shift) | ((v1 >> 1) >> (63 - shift));
+    *a2 = (v1 << shift) | ((v2 >> 1) >> (63 - shift));
+    *a3 = (v2 << shift) | ((v3 >> 1) >> (63 - shift));
+}
+JLM_FN int jlm_biased_exponent(double x) { return (int)((jlm_bits(x) >> 52) & 0x7ffu); }
+/* jlm_paynehanek on x's binade words; regime |x| ≥ 2^20·π/2, finite */
+JLM_FN int jlm_paynehanek_w(double x, uint64_t a1, uint64_t a2, uint64_t a3, double *yhi,
+                            double *ylo) {
+    const uint64_t X = (jlm_bits(x) & 0x000fffffffffffffull) | (1ull << 52);
     const jlm_u128 w1 = (jlm_u128)(X * a1) << 64;
     const jlm_u128 w2 = (jlm_u128)X * a2;
     const jlm_u128 w3 = ((jlm_u128)X * a3) >> 64;
@@ -391,6 +396,11 @@ JLM_FN int jlm_paynehanek_nb(double x, double *yhi, double *ylo) {
     *yhi = yh;
     *ylo = (((zhi * pio2_hi - yh) + zhi * pio2_lo) + zlo * pio2_hi) + zlo * pio2_lo;
     return q;
+}
+JLM_FN int jlm_paynehanek_nb(double x, double *yhi, double *ylo) {
+    uint64_t a1, a2, a3;
+    jlm_ph_words(jlm_biased_exponent(x), &a1, &a2, &a3);
+    return jlm_paynehanek_w(x, a1, a2, a3, yhi, ylo);
 }
 /* jlm_cwext; regime 9π/4 ≲ |x| < 2^20·π/2 (every iteration evaluated, the needed one kept) */
 JLM_FN int jlm_cwext_nb(double x, uint32_t xhp, double *yhi, double *ylo) {
@@ -444,6 +454,12 @@ JLM_FN int jlm_sin_cwx_in(double x) {
 JLM_FN double jl_sin_ph_nb(double x) {
     double hi, lo;
     const int n = jlm_paynehanek_nb(x, &hi, &lo);
+    return jlm_sin_quadrant(n, hi, lo);
+}
+/* the same with the binade's words given (arguments sharing one exponent) */
+JLM_FN double jl_sin_ph_w(double x, uint64_t a1, uint64_t a2, uint64_t a3) {
+    double hi, lo;
+    const int n = jlm_paynehanek_w(x, a1, a2, a3, &hi, &lo);
     return jlm_sin_quadrant(n, hi, lo);
 }
 JLM_FN double jl_sin_cwx_nb(double x) {

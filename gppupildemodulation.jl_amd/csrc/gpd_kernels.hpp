@@ -1603,7 +1603,10 @@ constexpr int CR_BLOCKS = 8;
 static_assert(FS_G == CR_BLOCKS, "the one-pass faint statistics split a series along the CR8 blocks");
 constexpr int CR_SLOTS = CR_BLOCKS * EXACT_WG;  // 2048
 constexpr int CR_NV = 8;                        // values per block total (offsets: 8)
-constexpr int CR_U = 4;                         // cr_sum2: samples per prefetched batch
+#ifndef GPD_CR_U
+#define GPD_CR_U 4  // A/B builds: -DGPD_CR_U=n
+#endif
+constexpr int CR_U = GPD_CR_U;                  // cr_sum2: samples per prefetched batch
 constexpr int CR_FLAG = (EXACT_WG / 64) * 8;    // LDS word after block_sum's partials
 constexpr int EXACT_LDS = CR_FLAG + 1;          // doubles of LDS per exact-path workgroup
 
@@ -1780,8 +1783,21 @@ struct ExactChi2 {
             cw &= jlm_sin_cwx_in(th[u]);
         }
         if (__all(ph)) {
+            // one binade for the whole wave (MJD-scale ωt spans one or two): its three words of
+            // 2/π fetched once, wave-uniform, instead of per lane and sample
+            const int e0 = __builtin_amdgcn_readfirstlane(jlm_biased_exponent(th[0]));
+            int one = 1;
 #pragma unroll
-            for (int u = 0; u < U; ++u) s[u] = jl_sin_ph_nb(th[u]);
+            for (int u = 0; u < U; ++u) one &= jlm_biased_exponent(th[u]) == e0;
+            if (__all(one)) {
+                uint64_t a1, a2, a3;
+                jlm_ph_words(e0, &a1, &a2, &a3);
+#pragma unroll
+                for (int u = 0; u < U; ++u) s[u] = jl_sin_ph_w(th[u], a1, a2, a3);
+            } else {
+#pragma unroll
+                for (int u = 0; u < U; ++u) s[u] = jl_sin_ph_nb(th[u]);
+            }
         } else if (__all(cw)) {
 #pragma unroll
             for (int u = 0; u < U; ++u) s[u] = jl_sin_cwx_nb(th[u]);

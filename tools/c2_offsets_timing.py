@@ -21,8 +21,8 @@ gpd = gpdemod_loader.load()
 T0 = 86400.0 * 60000.0 if "--mjd" in sys.argv else 0.0
 B = synth.make_batch(100000, 32, seed=42, offsets=True, t0=T0)
 args = (B["t"], B["d"], B["fc"], B["fc_of_pixel"])
-cases = [(False, "auto", None)] + [(off, "exact", g) for off in (False, True)
-                                     for g in ("1", "2", "4", "8")]
+GS = ("8",) if "--g8" in sys.argv else ("1", "2", "4", "8")  # --g8: the default split only
+cases = [(False, "auto", None)] + [(off, "exact", g) for off in (False, True) for g in GS]
 for off, method, g in cases:
     if g is None:
         os.environ.pop("GPD_EXACT_G", None)
@@ -32,6 +32,6 @@ for off, method, g in cases:
     t0 = time.perf_counter()
     for _ in range(3):
         gpd.fit_batch(*args, fitoffsets=off, method=method)
-    print(json.dumps({"t0": T0, "fitoffsets": off, "method": method, "G": g,
+    print(json.dumps({"lib": os.environ.get("GPD_LIB", ""), "t0": T0, "fitoffsets": off, "method": method, "G": g,
                       "ms": round((time.perf_counter() - t0) / 3 * 1e3, 3),
                       "kernels_ms": {k: round(v, 3) for k, v in gpd.timings(0).items()}}))
