@@ -1607,6 +1607,10 @@ constexpr int CR_NV = 8;                        // values per block total (offse
 #define GPD_CR_U 4  // A/B builds: -DGPD_CR_U=n
 #endif
 constexpr int CR_U = GPD_CR_U;                  // cr_sum2: samples per prefetched batch
+#ifndef GPD_CR_UR
+#define GPD_CR_UR 4
+#endif
+constexpr int CR_UR = GPD_CR_UR;                // the same for the residual pass (loads only)
 constexpr int CR_FLAG = (EXACT_WG / 64) * 8;    // LDS word after block_sum's partials
 constexpr int EXACT_LDS = CR_FLAG + 1;          // doubles of LDS per exact-path workgroup
 
@@ -2054,7 +2058,7 @@ struct ExactChi2 {
             a[0] += w * (rr * rr + ri * ri);
         };
         if (mcg) {  // the model the same thread wrote for element i in the first pass
-            cr_sum2<1>([&](long long i, Raw &r) { load_res(V, i, r); },
+            cr_sum2<1, CR_UR>([&](long long i, Raw &r) { load_res(V, i, r); },
                        [&](long long i, const Raw &r, double (&a)[1]) {
                            if (!valid_st(V, r.st)) return;
                            resid(r.f, r.d, weight_of(r.st), a);
