@@ -405,3 +405,17 @@ def test_one_exposure_exact_every_split(gpu, oracle, monkeypatch, fitoffsets):
               f"(host call, PCIe included)")
     for G, r in recs.items():
         print(assert_exact_bitwise(r, ref, label=f"C2 exact G={G or 'auto'} offsets={fitoffsets}"))
+
+
+@pytest.mark.parametrize("xinit,b_range", [(None, (0.3, 2.5)), ((8.0, 0.3), (0.3, 2.5)),
+                                           (None, (6.0, 7.5))])
+def test_exact_model_regime_boundaries(gpu, oracle, xinit, b_range):
+    """The exact evaluator's batched model switches per wave between the branch-free forms of
+    Julia's sin (Payne–Hanek, extended Cody–Waite) and the general function: ωt crossing
+    2^20·π/2 (t = 2^18 s at ω = 2π) inside each series mixes both regimes in some waves, and a
+    start at b = 8 or true b ∈ [6, 7.5] put β = b sin θ beyond sincos's small regime (|β| ≲ 9π/4).
+    Records stay the oracle's bits."""
+    B = synth.make_batch(20_000, 8, seed=71, t0=2.0 ** 18 - 20.0, b_range=b_range)
+    xi = None if xinit is None else np.array(xinit)
+    ref = oracle_fit(oracle, B, xinit=xi)
+    print(assert_exact_bitwise(fit(gpu, B, method="exact", xinit=xi), ref, label="regimes/exact"))
