@@ -1,0 +1,243 @@
+"""FITS output of processmetrology: the METROLOGY binary table and its header
+written the way the reference's FITSIO/CFITSIO calls lay them out (src/GPPupilDemodulation.jl:
+174-189, 239-253 build the keywords and columns; src/FitsUtils.jl:61-156 writes the HDUs), plus
+a reader for the same subset (round trips in tests/test_fits.py, and reading METROLOGY tables of
+exposures).
+
+The image has no CFITSIO, FITSIO or astropy, so this is a small numpy restatement of the FITS
+standard's parts the path uses — an empty primary HDU (FitsUtils.jl:40-58 creates it with
+BITPIX 16, NAXIS 0), one BINTABLE extension per table, 2880-byte blocks, big-endian rows:
+- columns: Float32 → E, Float64 → D, Int8 → B with TZERO = -128 (CFITSIO's signed-byte
+  convention for Julia's Int8 STATE column), UInt8 → B, Int16/32/64 → I/J/K, Bool → L,
+  ComplexF32/64 → C/M; an (N, r) array is one r-vector per row (Julia's r × N column, e.g. VOLT
+  80E or 144E with keepraw, ABSA/ARGA/B/PHI/X0/Y0 32E in window mode);
+- keywords longer than 8 characters or containing spaces use the HIERARCH convention CFITSIO
+  writes ("HIERARCH DEMODULATION SIN AMPLITUDE FT T1 D1 = 1.23…"); floats with 15 significant
+  digits as CFITSIO's ffd2e does (so values round-trip to ~1e-15 relative, not bit for bit),
+  integers and logicals right-justified to column 30, strings quoted.
+The column order is the table's insertion order (the reference's Dict order is unspecified).
+This is host I/O beside the GPU path, not part of it."""
+from __future__ import annotations
+
+import numpy as np
+
+BLOCK = 2880
+CARD = 80
+
+_TFORM = {np.dtype(np.float32): "E", np.dtype(np.float64): "D", np.dtype(np.uint8): "B",
+          np.dtype(np.int8): "B", np.dtype(np.int16): "I", np.dtype(np.int32): "J",
+          np.dtype(np.int64): "K", np.dtype(np.bool_): "L", np.dtype(np.complex64): "C",
+          np.dtype(np.complex128): "M"}
+_CODE = {"E": ">f4", "D": ">f8", "B": "u1", "I": ">i2", "J": ">i4", "K": ">i8", "L": "S1",
+         "C": ">c8", "M": ">c16"}
+_STRUCTURAL = ("SIMPLE", "XTENSION", "BITPIX", "NAXIS", "PCOUNT", "GCOUNT", "TFIELDS", "EXTEND",
+               "TTYPE", "TFORM", "TZERO", "TSCAL", "TDIM", "TUNIT", "EXTNAME", "END")
+
+
+def _is_structural(key: str) -> bool:
+    return any(key == s or (key.startswith(s) and key[len(s):].isdigit()) for s in _STRUCTURAL)
+
+
+def format_float(v: float) -> str:
+    """CFITSIO's ffd2e with 15 significant digits (FITSIO's Float64 keywords): %.15G, with a
+    decimal point always present."""
+    s = "%.15G" % v
+    if not np.isfinite(v):
+        raise ValueError(f"FITS keywords cannot hold {v!r}")
+    if "." not in s:
+        s = s.replace("E", ".E") if "E" in s else s + "."
+    return s
+
+
+def _value(v) -> str:
+    if isinstance(v, (bool, np.bool_)):
+        return "%20s" % ("T" if v else "F")
+    if isinstance(v, (int, np.integer)):
+        return "%20d" % int(v)
+    if isinstance(v, (float, np.floating)):
+        return "%20s" % format_float(float(v))
+    if isinstance(v, str):
+        q = "'" + v.replace("'", "''").ljust(8) + "'"
+        return q
+    raise TypeError(f"unsupported keyword value {v!r}")
+
+
+def card(key: str, value=None, comment: str | None = None) -> str:
+    """One 80-character header card."""
+    if key in ("COMMENT", "HISTORY", ""):
+        text = key.ljust(8) + str(value or "")
+    elif len(key) <= 8 and " " not in key and key == key.upper():
+        text = key.ljust(8) + "= " + _value(value)
+    else:
+        v = _value(value).strip() if not isinstance(value, str) else _value(value)
+        text = f"HIERARCH {key} = {v}"
+    if comment:
+        text += " / " + comment
+    if len(text) > CARD:
+        if comment:
+            return card(key, value)
+        raise ValueError(f"keyword card longer than 80 characters: {text!r}")
+    if not text.isascii():
+        raise ValueError(f"non-ASCII header card: {text!r}")
+    return text.ljust(CARD)
+
+
+def _header_bytes(cards: list[str]) -> bytes:
+    raw = "".join(cards) + "END".ljust(CARD)
+    raw += " " * (-len(raw) % BLOCK)
+    return raw.encode("ascii")
+
+
+def _columns(table: dict):
+    """(name, tform, tzero, big-endian field dtype, data as field values) per column."""
+    n = None
+    cols = []
+    for name, a in table.items():
+        a = np.asarray(a)
+        if a.ndim == 0 or a.ndim > 2:
+            raise ValueError(f"column {name}: (N,) or (N, r) arrays only, got shape {a.shape}")
+        if n is None:
+            n = a.shape[0]
+        elif a.shape[0] != n:
+            raise ValueError(f"column {name}: {a.shape[0]} rows, expected {n}")
+        if a.dtype not in _TFORM:
+            raise TypeError(f"column {name}: unsupported dtype {a.dtype}")
+        letter = _TFORM[a.dtype]
+        r = 1 if a.ndim == 1 else a.shape[1]
+        tzero = None
+        if a.dtype == np.int8:
+            tzero = -128
+            a = (a.astype(np.int16) + 128).astype(np.uint8)
+        elif a.dtype == np.bool_:
+            a = np.where(a, b"T", b"F")
+        fdt = np.dtype(_CODE[letter]) if a.ndim == 1 else np.dtype((_CODE[letter], (r,)))
+        cols.append((name, f"{r}{letter}", tzero, fdt, a))
+    return n or 0, cols
+
+
+def bintable_hdu(table: dict, header: dict | None = None, *, extname: str | None = None,
+                 units: dict | None = None) -> bytes:
+    """One BINTABLE extension (header + data blocks)."""
+    n, cols = _columns(table)
+    rec = np.dtype([(name, fdt) for name, _, _, fdt, _ in cols])
+    data = np.zeros(n, dtype=rec)
+    for name, _, _, _, a in cols:
+        data[name] = a
+    cards = [card("XTENSION", "BINTABLE"), card("BITPIX", 8), card("NAXIS", 2),
+             card("NAXIS1", rec.itemsize), card("NAXIS2", n), card("PCOUNT", 0),
+             card("GCOUNT", 1), card("TFIELDS", len(cols))]
+    for i, (name, tform, tzero, _, _) in enumerate(cols, 1):
+        cards += [card(f"TTYPE{i}", name), card(f"TFORM{i}", tform)]
+        if tzero is not None:
+            cards.append(card(f"TZERO{i}", tzero))
+        if units and name in units:
+            cards.append(card(f"TUNIT{i}", units[name]))
+    if extname is not None:
+        cards.append(card("EXTNAME", extname))
+    for k, v in (header or {}).items():
+        if not _is_structural(k):
+            cards.append(card(k, v))
+    body = data.tobytes()
+    body += b"\0" * (-len(body) % BLOCK)
+    return _header_bytes(cards) + body
+
+
+def primary_hdu(header: dict | None = None) -> bytes:
+    """The empty primary HDU (FitsUtils.jl:40-58: BITPIX 16, NAXIS 0) with the given keywords."""
+    cards = [card("SIMPLE", True), card("BITPIX", 16), card("NAXIS", 0), card("EXTEND", True)]
+    for k, v in (header or {}).items():
+        if not _is_structural(k):
+            cards.append(card(k, v))
+    return _header_bytes(cards)
+
+
+def write_metrology(path: str, table: dict, header: dict, *, primary_header: dict | None = None,
+                    units: dict | None = None, extname: str = "METROLOGY") -> None:
+    """processmetrology's (table, hdr) as a FITS file: primary HDU + the METROLOGY table."""
+    with open(path, "wb") as f:
+        f.write(primary_hdu(primary_header))
+        f.write(bintable_hdu(table, header, extname=extname, units=units))
+
+
+# ------------------------------------------------------------------------------- reading
+def _parse_value(s: str):
+    s = s.strip()
+    if s.startswith("'"):
+        out, i = [], 1
+        while i < len(s):
+            if s[i] == "'":
+                if i + 1 < len(s) and s[i + 1] == "'":
+                    out.append("'")
+                    i += 2
+                    continue
+                break
+            out.append(s[i])
+            i += 1
+        return "".join(out).rstrip()
+    s = s.split("/", 1)[0].strip()
+    if s in ("T", "F"):
+        return s == "T"
+    if s == "":
+        return None
+    try:
+        return int(s)
+    except ValueError:
+        return float(s.replace("D", "E"))
+
+
+def parse_card(text: str):
+    """(key, value) of one card; (None, None) for commentary and blank cards."""
+    if text.startswith("HIERARCH "):
+        key, _, rest = text[9:].partition("=")
+        return key.strip(), _parse_value(rest)
+    key = text[:8].strip()
+    if text[8:10] != "= " or key in ("COMMENT", "HISTORY", ""):
+        return None, None
+    return key, _parse_value(text[10:])
+
+
+def read_fits(path: str):
+    """[(header dict, data)] per HDU: None for an empty HDU, a dict of columns for a BINTABLE
+    ((N,) or (N, r) arrays in native byte order; TZERO -128 bytes back to Int8)."""
+    raw = open(path, "rb").read()
+    pos, hdus = 0, []
+    while pos < len(raw):
+        hdr, done = {}, False
+        while not done:
+            block = raw[pos:pos + BLOCK].decode("ascii")
+            pos += BLOCK
+            for j in range(0, BLOCK, CARD):
+                c = block[j:j + CARD]
+                if c.startswith("END") and c[3:].strip() == "":
+                    done = True
+                    break
+                k, v = parse_card(c)
+                if k is not None:
+                    hdr[k] = v
+        data = None
+        if hdr.get("XTENSION") == "BINTABLE":
+            n, width, k = hdr["NAXIS2"], hdr["NAXIS1"], hdr["TFIELDS"]
+            fields = []
+            for i in range(1, k + 1):
+                tform = hdr[f"TFORM{i}"].strip()
+                r, letter = (int(tform[:-1]) if len(tform) > 1 else 1), tform[-1]
+                fields.append((hdr[f"TTYPE{i}"], _CODE[letter] if r == 1 else (_CODE[letter], (r,))))
+            rec = np.dtype(fields)
+            if rec.itemsize != width:
+                raise ValueError(f"NAXIS1 {width} != row size {rec.itemsize}")
+            rows = np.frombuffer(raw, dtype=rec, count=n, offset=pos)
+            data = {}
+            for i, (name, _) in enumerate(fields, 1):
+                a = rows[name]
+                if hdr.get(f"TZERO{i}") == -128 and a.dtype == np.uint8:
+                    a = (a.astype(np.int16) - 128).astype(np.int8)
+                elif a.dtype.kind == "S":
+                    a = a == b"T"
+                else:
+                    a = a.astype(a.dtype.newbyteorder("="))
+                data[name] = a
+            pos += n * width + (-(n * width) % BLOCK)
+        elif hdr.get("NAXIS", 0) != 0:
+            raise NotImplementedError("image HDUs with data are not read")
+        hdus.append((hdr, data))
+    return hdus

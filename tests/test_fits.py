@@ -1,0 +1,125 @@
+"""FITS output of processmetrology (§8f rank 4; src/GPPupilDemodulation.jl:174-189, 239-253,
+src/FitsUtils.jl:40-156): the METROLOGY table and its keywords written in the layout FITSIO /
+CFITSIO give them, read back by the same module.  No FITS library exists in the image, so the
+layout is checked against the FITS standard directly (2880-byte blocks, 80-character cards,
+HIERARCH keywords, TFORM / TZERO, big-endian rows); parity with a CFITSIO-written file is
+unpinned (no such file in the reference)."""
+import numpy as np
+import pytest
+
+
+@pytest.fixture(scope="module")
+def fits():
+    import gpdemod_loader
+    return gpdemod_loader.load().fits
+
+
+def _window_table(N=1000, seed=5, fitoffsets=True, keepraw=False):
+    """A window-mode processmetrology table: TIME, VOLT (80 or 144 per row), the per-sample
+    Float32 parameter columns (N, 32), STATE (Int8, TRANSIENT = -1 included)."""
+    rng = np.random.default_rng(seed)
+    tab = {"TIME": np.arange(N, dtype=np.int32) * 2000,
+           "VOLT": rng.standard_normal((N, 144 if keepraw else 80)).astype(np.float32)}
+    for k in (["X0", "Y0"] if fitoffsets else []) + ["ABSA", "ARGA", "B", "PHI"]:
+        tab[k] = rng.standard_normal((N, 32)).astype(np.float32)
+    tab["STATE"] = rng.integers(-1, 4, N).astype(np.int8)
+    tab["STATE"][:3] = [-128, 127, -1]
+    return tab
+
+
+def _header(seed=6):
+    rng = np.random.default_rng(seed)
+    hdr = {"EXTNAME": "METROLOGY", "MJD-OBS": 58849.123456789, "ESO INS MET MODE": "FAINT",
+           "PROCSOFT": "GPPupilDemodulation.jl", "NSAMPLES": 1000, "FLAG": True}
+    for side in ("FT", "SC"):
+        for tel in range(1, 5):
+            for d in ("D1", "D2", "D3", "D4"):
+                name = f"{side} T{tel} {d}"
+                hdr[f"DEMODULATION AMPLITUDE ABS {name}"] = float(rng.random())
+                hdr[f"DEMODULATION AMPLITUDE ARG {name}"] = float(rng.uniform(-np.pi, np.pi))
+                hdr[f"DEMODULATION SIN AMPLITUDE {name}"] = float(rng.uniform(0.3, 2.5))
+                hdr[f"DEMODULATION SIN PHASE {name}"] = float(rng.uniform(-np.pi, np.pi) * 1e-7)
+                hdr[f"DEMODULATION CENTER X0 {name}"] = float(rng.standard_normal() * 1e3)
+    return hdr
+
+
+@pytest.mark.parametrize("keepraw", [False, True])
+def test_metrology_table_round_trip(fits, tmp_path, keepraw):
+    tab, hdr = _window_table(keepraw=keepraw), _header()
+    path = str(tmp_path / "m.fits")
+    fits.write_metrology(path, tab, hdr, primary_header={"ESO INS PMC1 MODULATE": True},
+                         units={"TIME": "us", "VOLT": "V"})
+    raw = open(path, "rb").read()
+    assert len(raw) % 2880 == 0
+    (h0, d0), (h1, d1) = fits.read_fits(path)
+    assert d0 is None and h0["SIMPLE"] is True and h0["BITPIX"] == 16 and h0["NAXIS"] == 0
+    assert h0["ESO INS PMC1 MODULATE"] is True
+    assert h1["XTENSION"] == "BINTABLE" and h1["EXTNAME"] == "METROLOGY"
+    assert h1["NAXIS2"] == 1000 and h1["TFIELDS"] == len(tab)
+    assert list(d1) == list(tab)  # insertion order
+    for k, a in tab.items():
+        assert d1[k].dtype == a.dtype and d1[k].shape == a.shape, k
+        assert d1[k].tobytes() == a.tobytes(), k  # Float32 and Int8 bit for bit
+    forms = {h1[f"TTYPE{i}"]: h1[f"TFORM{i}"] for i in range(1, h1["TFIELDS"] + 1)}
+    assert forms["VOLT"] == ("144E" if keepraw else "80E") and forms["ABSA"] == "32E"
+    assert forms["STATE"] == "1B" and forms["TIME"] == "1J"
+    i_state = [h1[f"TTYPE{i}"] for i in range(1, h1["TFIELDS"] + 1)].index("STATE") + 1
+    assert h1[f"TZERO{i_state}"] == -128
+    assert h1["TUNIT1"] == "us" and h1["TUNIT2"] == "V"
+    for k, v in hdr.items():
+        if isinstance(v, float):
+            assert h1[k] == pytest.approx(v, rel=1e-14, abs=0), k  # 15 significant digits
+        else:
+            assert h1[k] == v, k
+
+
+def test_header_cards_follow_the_standard(fits, tmp_path):
+    hdr = _header()
+    path = str(tmp_path / "h.fits")
+    fits.write_metrology(path, {"TIME": np.arange(4, dtype=np.float64)}, hdr)
+    text = open(path, "rb").read()[2880:]
+    cards = []
+    for i in range(0, len(text), 80):
+        c = text[i:i + 80].decode("ascii")
+        if c.rstrip() == "END":
+            break
+        cards.append(c)
+    assert cards[0].startswith("XTENSION= 'BINTABLE'")
+    assert all(len(c) == 80 for c in cards)
+    hier = [c for c in cards if c.startswith("HIERARCH DEMODULATION SIN AMPLITUDE FT T1 D1 = ")]
+    assert len(hier) == 1
+    # fixed-format values end in column 30
+    naxis2 = next(c for c in cards if c.startswith("NAXIS2  = "))
+    assert naxis2[29] == "4" and naxis2[30:].strip() == ""
+    assert next(c for c in cards if c.startswith("PROCSOFT= ")).startswith(
+        "PROCSOFT= 'GPPupilDemodulation.jl'")
+
+
+def test_float_keyword_format(fits):
+    """CFITSIO's 15 significant digits with a decimal point."""
+    assert fits.format_float(1.0) == "1."
+    assert fits.format_float(0.1) == "0.1"
+    assert fits.format_float(1e20) == "1.E+20"
+    assert fits.format_float(-1.23456789012345678e-7) == "-1.23456789012346E-07"
+    with pytest.raises(ValueError):
+        fits.format_float(float("nan"))
+    with pytest.raises(ValueError):
+        fits.card("DEMODULATION AMPLITUDE ABS FT T1 D1 WITH A VERY LONG NAME THAT OVERFLOWS", 1.5)
+
+
+def test_processmetrology_header_written(fits, tmp_path):
+    """processmetrology's own keyword names (built by demod.py) survive the file: 6 per diode
+    with fitoffsets, 4 without, and PROCSOFT."""
+    import gpdemod_loader
+    gpd = gpdemod_loader.load()
+    keys = []
+    for side, tel, diode in gpd.demod._diode_order():
+        name = f"{side.name} T{tel} {diode.name}"
+        keys += [f"DEMODULATION CENTER X0 {name}", f"DEMODULATION SIN PHASE {name}"]
+    hdr = {k: 0.5 for k in keys}
+    hdr["PROCSOFT"] = "GPPupilDemodulation.jl"
+    path = str(tmp_path / "p.fits")
+    fits.write_metrology(path, {"VOLT": np.zeros((2, 80), np.float32)}, hdr)
+    (_, _), (h1, d1) = fits.read_fits(path)
+    assert all(h1[k] == 0.5 for k in keys) and h1["PROCSOFT"] == "GPPupilDemodulation.jl"
+    assert d1["VOLT"].shape == (2, 80)

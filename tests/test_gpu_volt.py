@@ -99,3 +99,23 @@ def test_processmetrology_table_and_header(gpu):
     assert not any(k.startswith("DEMODULATION") for k in hdr4)
     assert tab4["B"].shape == (t.size, 32) and tab4["B"].dtype == np.float32
     assert tab4["STATE"].dtype == np.int8 and set(np.unique(tab4["STATE"])) <= {-1, 1, 2, 3}
+
+
+def test_processmetrology_fits_file(gpu, tmp_path):
+    """processmetrology's (table, hdr) through the FITS writer and back (fits.py): the
+    demodulated VOLT rows and window columns bit for bit, the DEMODULATION keywords to 15
+    significant digits."""
+    t, volt, centres, cplx, fop = volt_exposure(gpu, 6000, seed=41)
+    table = {"TIME": np.round((t - t[0]) * 1e6).astype(np.int64), "VOLT": volt}
+    header = {"MJD-OBS": 60123.25, "EXTNAME": "METROLOGY"}
+    for kw in ({"offsets": False}, {"offsets": centres, "window": 4.0, "keepraw": True}):
+        tab, hdr = gpu.processmetrology(table, header, **kw)
+        path = str(tmp_path / "out.fits")
+        gpu.fits.write_metrology(path, tab, hdr)
+        (_, _), (h1, d1) = gpu.fits.read_fits(path)
+        for k, a in tab.items():
+            assert d1[k].tobytes() == np.ascontiguousarray(a).tobytes(), k
+        for k, v in hdr.items():
+            if k.startswith("DEMODULATION"):
+                assert h1[k] == pytest.approx(v, rel=1e-14, abs=1e-300), k
+        assert h1["PROCSOFT"] == "GPPupilDemodulation.jl"
