@@ -18,13 +18,13 @@ from ._lib import (GPD_FIT_OFFSETS, GPD_METHOD_EXACT, GPD_METHOD_HARMONIC, GPD_O
 from .demod import (DAY_TO_SEC, M_2PI, MJD_1970_1_1, Diode, FaintStates, MetState,
                     ModulationNoOffsets, ModulationWithOffsets, Side, buildfaintparameters,
                     buildstates, chi2_batch, compute_mean_var_power, demodulate_windows,
-                    mean_var_power_batch, metrology_times, processmetrology,
+                    mean_var_power_batch, metrology_times, process_exposure, processmetrology,
                     demodulateall, fc_column_of, fit_batch, fit_windows, idx, process_volt,
                     read_stefan_file, window_length, window_tables)
 from . import fits  # processmetrology's FITS output (host I/O)
 
 __all__ = [
-    "fits",
+    "fits", "process_exposure",
     "GPD_FIT_OFFSETS", "GPD_METHOD_EXACT", "GPD_METHOD_HARMONIC", "GPD_ONLY_HIGH", "GPD_RECENTER",
     "GPD_ST_EXACT", "GPD_ST_FALLBACK", "GPD_ST_MAXFUN", "GPD_ST_NAN", "GPD_ST_REFIT",
     "PARAM_DTYPE", "GpdError", "libm_eval", "load", "timings", "M_2PI", "Diode", "FaintStates", "MetState",

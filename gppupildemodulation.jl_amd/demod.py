@@ -103,7 +103,7 @@ DAY_TO_SEC = 24 * 60 * 60  # :16
 def buildfaintparameters(hdr) -> FaintStates:
     """FaintStates from the exposure header (src/GPPupilDemodulation.jl:64-81): timer_i =
     TIMERi + MJD(1970-01-01)·86400 + RATEi·(0:REPEATi-1), ordered by VOLTAGEi.  `hdr` is any
-    mapping with the ESO keywords (e.g. a FITS header read elsewhere; FITS I/O is out of scope)."""
+    mapping with the ESO keywords (e.g. the primary header from fits.read_fits)."""
     timers = []
     for i in (1, 2):
         start = hdr[f"ESO INS ANLO3 TIMER{i}"] + MJD_1970_1_1 * DAY_TO_SEC
@@ -487,7 +487,7 @@ def _diode_order():
 
 
 def processmetrology(table, header, *, window=None, faintparam=None, keepraw=False,
-                     onlyhigh=False, offsets=None, method="auto", device=0):
+                     onlyhigh=False, offsets=None, method="auto", device=0, mjd=None):
     """processmetrology (src/GPPupilDemodulation.jl:128-255) on the GPU, minus FITS I/O.
 
     table: mapping of the METROLOGY columns with at least "TIME" (µs, N) and "VOLT" (N×80
@@ -498,8 +498,9 @@ def processmetrology(table, header, *, window=None, faintparam=None, keepraw=Fal
     row, or 144 with keepraw: raw rows then the 32 demodulated columns), in window mode the
     per-sample Float32 columns ABSA, ARGA, B, PHI (+ X0, Y0) as (N, 32) rows and STATE (Int8) with
     faint states; otherwise the header gains the per-diode DEMODULATION keywords (:172-189);
-    PROCSOFT = "GPPupilDemodulation.jl" in both modes (:253)."""
-    mjd = float(header["MJD-OBS"])
+    PROCSOFT = "GPPupilDemodulation.jl" in both modes (:253).  mjd: the reference's argument
+    (the primary header's MJD-OBS); default header["MJD-OBS"]."""
+    mjd = float(header["MJD-OBS"] if mjd is None else mjd)  # the reference's mjd argument
     times = metrology_times(table["TIME"], mjd)
     state = None
     if faintparam is not None:
@@ -543,3 +544,31 @@ def processmetrology(table, header, *, window=None, faintparam=None, keepraw=Fal
     hdr["PROCSOFT"] = "GPPupilDemodulation.jl"
     tab["VOLT"] = vout
     return tab, hdr
+
+
+def process_exposure(filename, outname, *, offsets, window=None, keepraw=False, onlyhigh=False,
+                     nofaint=False, method="auto", device=0):
+    """One exposure file as the reference's main loop handles it (src/GPPupilDemodulation.jl:
+    357-414, without the argument parsing and directory walk): skipped (returns False) unless the
+    primary header has ESO INS PMC1 MODULATE = T and ESO INS MET MODE is not OFF; FAINT mode
+    builds the faint states from the primary header unless `nofaint`; MJD-OBS gives mjd; the
+    METROLOGY table goes through processmetrology and the file is copied to `outname` with that
+    table and header replaced (FITScopy!, fits.fits_copy).  offsets: the 40 complex centres
+    (Stefan's, or zeros for "uncentered") or False ("fit")."""
+    from . import fits
+    hdus = fits.read_fits(filename)
+    prim = hdus[0][0]
+    if not prim.get("ESO INS PMC1 MODULATE", False):
+        return False
+    metmode = prim.get("ESO INS MET MODE", "ON")
+    if metmode == "OFF":
+        return False
+    faint = buildfaintparameters(prim) if metmode == "FAINT" and not nofaint else None
+    met = next(((h, d) for h, d in hdus if h.get("EXTNAME") == "METROLOGY"), None)
+    if met is None:
+        raise KeyError(f"{filename}: no METROLOGY table")
+    table, hdr = processmetrology(met[1], met[0], window=window, faintparam=faint,
+                                  keepraw=keepraw, onlyhigh=onlyhigh, offsets=offsets,
+                                  method=method, device=device, mjd=float(prim["MJD-OBS"]))
+    fits.fits_copy(outname, filename, {"METROLOGY": table}, {"METROLOGY": hdr})
+    return True

@@ -100,6 +100,10 @@ def _columns(table: dict):
             n = a.shape[0]
         elif a.shape[0] != n:
             raise ValueError(f"column {name}: {a.shape[0]} rows, expected {n}")
+        if a.dtype.kind == "S" and a.ndim == 1:  # character column rA
+            r = max(a.dtype.itemsize, 1)
+            cols.append((name, f"{r}A", None, np.dtype(f"S{r}"), a))
+            continue
         if a.dtype not in _TFORM:
             raise TypeError(f"column {name}: unsupported dtype {a.dtype}")
         letter = _TFORM[a.dtype]
@@ -149,6 +153,80 @@ def primary_hdu(header: dict | None = None) -> bytes:
         if not _is_structural(k):
             cards.append(card(k, v))
     return _header_bytes(cards)
+
+
+_BITPIX_DTYPE = {8: "u1", 16: ">i2", 32: ">i4", 64: ">i8", -32: ">f4", -64: ">f8"}
+_DTYPE_BITPIX = {np.dtype(np.uint8): 8, np.dtype(np.int16): 16, np.dtype(np.int32): 32,
+                 np.dtype(np.int64): 64, np.dtype(np.float32): -32, np.dtype(np.float64): -64}
+
+
+def image_hdu(data, header: dict | None = None, *, primary: bool = False,
+              extname: str | None = None) -> bytes:
+    """An image HDU (primary or IMAGE extension); data None gives the empty HDU.  numpy's C-order
+    shape (…, n2, n1) is NAXIS1 = n1 (Julia's column-major (n1, n2, …) array)."""
+    if data is None:
+        bitpix, shape, body = 16, (), b""
+    else:
+        data = np.asarray(data)
+        if data.dtype not in _DTYPE_BITPIX:
+            raise TypeError(f"unsupported image dtype {data.dtype}")
+        bitpix, shape = _DTYPE_BITPIX[data.dtype], data.shape
+        body = np.ascontiguousarray(data, dtype=_BITPIX_DTYPE[bitpix]).tobytes()
+        body += b"\0" * (-len(body) % BLOCK)
+    cards = [card("SIMPLE", True) if primary else card("XTENSION", "IMAGE"),
+             card("BITPIX", bitpix), card("NAXIS", len(shape))]
+    cards += [card(f"NAXIS{j}", n) for j, n in enumerate(reversed(shape), 1)]
+    cards += [card("EXTEND", True)] if primary else [card("PCOUNT", 0), card("GCOUNT", 1)]
+    if extname is not None and not primary:
+        cards.append(card("EXTNAME", extname))
+    for k, v in (header or {}).items():
+        if not _is_structural(k):
+            cards.append(card(k, v))
+    return _header_bytes(cards) + body
+
+
+def write_fits(path: str, hdus) -> None:
+    """hdus: [(header, data)] — data None or an ndarray (image; the first HDU is the primary),
+    or a dict of columns (BINTABLE; a table first gets an empty primary HDU before it).  The
+    EXTNAME of each header is kept."""
+    with open(path, "wb") as f:
+        for j, (hdr, data) in enumerate(hdus):
+            hdr = dict(hdr or {})
+            name = hdr.get("EXTNAME")
+            if isinstance(data, dict):
+                if j == 0:
+                    f.write(primary_hdu())
+                f.write(bintable_hdu(data, hdr, extname=name, units=_units_of(hdr)))
+            else:
+                f.write(image_hdu(data, hdr, primary=j == 0, extname=name))
+
+
+def _units_of(hdr: dict) -> dict:
+    """{column name: unit} from TTYPEn / TUNITn (FitsUtils.getunits, src/FitsUtils.jl:14-25)."""
+    return {hdr[f"TTYPE{k[5:]}"]: v for k, v in hdr.items()
+            if k.startswith("TUNIT") and k[5:].isdigit() and f"TTYPE{k[5:]}" in hdr}
+
+
+def fits_copy(dst: str, src: str, content: dict | None = None,
+              headers: dict | None = None) -> None:
+    """FitsUtils.FITScopy!(dst, src, content, header) (src/FitsUtils.jl:96-154): every HDU of src
+    copied to dst, the HDUs named in `content` / `headers` (EXTNAME → table dict or array /
+    header dict) replaced, names absent from src appended after it."""
+    content, headers = dict(content or {}), dict(headers or {})
+    out = []
+    for hdr, data in read_fits(src):
+        name = hdr.get("EXTNAME")
+        h = headers.pop(name, hdr) if name is not None else hdr
+        d = content.pop(name, data) if name is not None else data
+        if isinstance(d, dict) and "TFIELDS" in hdr and h is not hdr:
+            h = {**{k: v for k, v in hdr.items() if k.startswith("TUNIT") or k.startswith("TTYPE")},
+                 **h}
+        out.append((dict(h, EXTNAME=name) if name is not None else h, d))
+    for name, d in content.items():
+        out.append((dict(headers.pop(name, {}), EXTNAME=name), d))
+    for name, h in headers.items():
+        out.append((dict(h, EXTNAME=name), None))
+    write_fits(dst, out)
 
 
 def write_metrology(path: str, table: dict, header: dict, *, primary_header: dict | None = None,
@@ -221,6 +299,11 @@ def read_fits(path: str):
             for i in range(1, k + 1):
                 tform = hdr[f"TFORM{i}"].strip()
                 r, letter = (int(tform[:-1]) if len(tform) > 1 else 1), tform[-1]
+                if letter == "A":
+                    fields.append((hdr[f"TTYPE{i}"], f"S{r}"))
+                    continue
+                if letter not in _CODE:
+                    raise NotImplementedError(f"TFORM {tform} (column {hdr[f'TTYPE{i}']})")
                 fields.append((hdr[f"TTYPE{i}"], _CODE[letter] if r == 1 else (_CODE[letter], (r,))))
             rec = np.dtype(fields)
             if rec.itemsize != width:
@@ -231,13 +314,21 @@ def read_fits(path: str):
                 a = rows[name]
                 if hdr.get(f"TZERO{i}") == -128 and a.dtype == np.uint8:
                     a = (a.astype(np.int16) - 128).astype(np.int8)
-                elif a.dtype.kind == "S":
+                elif a.dtype.kind == "S" and hdr[f"TFORM{i}"].strip().endswith("L"):
                     a = a == b"T"
+                elif a.dtype.kind == "S":
+                    a = a.copy()
                 else:
                     a = a.astype(a.dtype.newbyteorder("="))
                 data[name] = a
-            pos += n * width + (-(n * width) % BLOCK)
-        elif hdr.get("NAXIS", 0) != 0:
-            raise NotImplementedError("image HDUs with data are not read")
+            size = n * width + hdr.get("PCOUNT", 0)  # the heap is skipped (no P/Q columns)
+            pos += size + (-size % BLOCK)
+        elif hdr.get("NAXIS", 0) != 0:  # image: raw values, BZERO/BSCALE left in the header
+            shape = tuple(hdr[f"NAXIS{j}"] for j in range(hdr["NAXIS"], 0, -1))
+            dt = np.dtype(_BITPIX_DTYPE[hdr["BITPIX"]])
+            size = int(np.prod(shape)) * dt.itemsize
+            img = np.frombuffer(raw, dtype=dt, count=int(np.prod(shape)), offset=pos)
+            data = img.reshape(shape).astype(dt.newbyteorder("="))
+            pos += size + (-size % BLOCK)
         hdus.append((hdr, data))
     return hdus

@@ -123,3 +123,42 @@ def test_processmetrology_header_written(fits, tmp_path):
     (_, _), (h1, d1) = fits.read_fits(path)
     assert all(h1[k] == 0.5 for k in keys) and h1["PROCSOFT"] == "GPPupilDemodulation.jl"
     assert d1["VOLT"].shape == (2, 80)
+
+
+def test_exposure_copy_replaces_the_metrology_table(fits, tmp_path):
+    """FITScopy!(dst, src, "METROLOGY" => table, "METROLOGY" => hdr) (src/FitsUtils.jl:96-154,
+    called by the reference's main loop): every other HDU — images, other tables with
+    character columns, header keywords — copied unchanged; METROLOGY replaced, its TUNITs kept."""
+    rng = np.random.default_rng(9)
+    img = rng.integers(-300, 300, (6, 5)).astype(np.int16)
+    cube = rng.standard_normal((2, 3, 4)).astype(np.float32)
+    tel = {"TEL_NAME": np.array([b"UT1", b"UT2", b"UT3", b"UT4"]),
+           "STA_INDEX": np.arange(4, dtype=np.int16)}
+    met = {"TIME": np.arange(10, dtype=np.int32), "VOLT": rng.standard_normal((10, 80)).astype(np.float32)}
+    src, dst = str(tmp_path / "src.fits"), str(tmp_path / "dst.fits")
+    fits.write_fits(src, [({"ESO INS PMC1 MODULATE": True, "MJD-OBS": 58849.5}, img),
+                          ({"EXTNAME": "OI_ARRAY", "ARRNAME": "VLTI"}, tel),
+                          ({"EXTNAME": "IMAGING_DATA", "BZERO": 0.0}, cube),
+                          ({"EXTNAME": "METROLOGY", "TUNIT1": "us", "TTYPE1": "TIME",
+                            "TTYPE2": "VOLT"}, met)])
+    hdus = fits.read_fits(src)
+    assert [h.get("EXTNAME") for h, _ in hdus] == [None, "OI_ARRAY", "IMAGING_DATA", "METROLOGY"]
+    np.testing.assert_array_equal(hdus[0][1], img)
+    np.testing.assert_array_equal(hdus[2][1], cube)
+    assert list(hdus[1][1]["TEL_NAME"]) == [b"UT1", b"UT2", b"UT3", b"UT4"]
+    assert hdus[3][0]["TUNIT1"] == "us"
+    new = dict(met, VOLT=(met["VOLT"] * 2).astype(np.float32), B=np.ones((10, 32), np.float32))
+    newhdr = dict(hdus[3][0], PROCSOFT="GPPupilDemodulation.jl")
+    fits.fits_copy(dst, src, {"METROLOGY": new}, {"METROLOGY": newhdr, "EXTRA": {"X": 1}})
+    out = fits.read_fits(dst)
+    assert [h.get("EXTNAME") for h, _ in out] == [None, "OI_ARRAY", "IMAGING_DATA", "METROLOGY",
+                                                  "EXTRA"]
+    assert out[0][0] == hdus[0][0] and out[1][0] == hdus[1][0] and out[2][0] == hdus[2][0]
+    np.testing.assert_array_equal(out[0][1], img)
+    np.testing.assert_array_equal(out[2][1], cube)
+    for k in tel:
+        np.testing.assert_array_equal(out[1][1][k], tel[k])
+    h3, d3 = out[3]
+    assert h3["PROCSOFT"] == "GPPupilDemodulation.jl" and h3["TUNIT1"] == "us"
+    assert d3["VOLT"].tobytes() == new["VOLT"].tobytes() and d3["B"].shape == (10, 32)
+    assert out[4][0]["X"] == 1 and out[4][1] is None

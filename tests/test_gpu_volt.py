@@ -119,3 +119,35 @@ def test_processmetrology_fits_file(gpu, tmp_path):
             if k.startswith("DEMODULATION"):
                 assert h1[k] == pytest.approx(v, rel=1e-14, abs=1e-300), k
         assert h1["PROCSOFT"] == "GPPupilDemodulation.jl"
+
+
+def test_process_exposure_file(gpu, tmp_path):
+    """The reference's per-file step (src/GPPupilDemodulation.jl:357-414): keyword gating, MJD-OBS
+    from the primary header, METROLOGY replaced by processmetrology's table and header, the
+    other HDUs copied."""
+    t, volt, centres, cplx, fop = volt_exposure(gpu, 6000, seed=43)
+    mjd = 60123.25
+    times_us = np.round((t - t[0]) * 1e6).astype(np.int64)
+    met_hdr = {"EXTNAME": "METROLOGY", "TTYPE1": "TIME", "TUNIT1": "us"}
+    prim = {"ESO INS PMC1 MODULATE": True, "ESO INS MET MODE": "ON", "MJD-OBS": mjd}
+    other = np.arange(12, dtype=np.float32).reshape(3, 4)
+    src, dst = str(tmp_path / "exp.fits"), str(tmp_path / "exp_demod.fits")
+    gpu.fits.write_fits(src, [(prim, None), ({"EXTNAME": "OTHER"}, other),
+                              (met_hdr, {"TIME": times_us, "VOLT": volt})])
+    assert gpu.process_exposure(src, dst, offsets=centres)
+    out = gpu.fits.read_fits(dst)
+    assert [h.get("EXTNAME") for h, _ in out] == [None, "OTHER", "METROLOGY"]
+    np.testing.assert_array_equal(out[1][1], other)
+    tab, hdr = gpu.processmetrology({"TIME": times_us, "VOLT": volt}, met_hdr, offsets=centres,
+                                    mjd=mjd)
+    h, d = out[2]
+    assert d["VOLT"].tobytes() == tab["VOLT"].tobytes() and h["TUNIT1"] == "us"
+    assert h["DEMODULATION SIN AMPLITUDE SC T3 D2"] == pytest.approx(
+        hdr["DEMODULATION SIN AMPLITUDE SC T3 D2"], rel=1e-14)
+    # gating: MODULATE false, MET MODE OFF → nothing written
+    for bad in ({"ESO INS PMC1 MODULATE": False}, {"ESO INS MET MODE": "OFF"}):
+        p2 = str(tmp_path / "skip.fits")
+        gpu.fits.write_fits(p2, [(dict(prim, **bad), None), (met_hdr, {"TIME": times_us,
+                                                                        "VOLT": volt})])
+        assert not gpu.process_exposure(p2, str(tmp_path / "never.fits"), offsets=centres)
+    assert not (tmp_path / "never.fits").exists()
