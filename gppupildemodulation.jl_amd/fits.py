@@ -275,9 +275,16 @@ def parse_card(text: str):
 
 
 def read_fits(path: str):
-    """[(header dict, data)] per HDU: None for an empty HDU, a dict of columns for a BINTABLE
+    """[(header dict, data)] per HDU (path may be gzip-compressed, .gz): None for an empty HDU,
+    an ndarray for an image, a dict of columns for a BINTABLE
     ((N,) or (N, r) arrays in native byte order; TZERO -128 bytes back to Int8)."""
-    raw = open(path, "rb").read()
+    if str(path).endswith(".gz"):  # the reference's SUFFIXES include .fits.gz (CFITSIO reads it)
+        import gzip
+        with gzip.open(path, "rb") as f:
+            raw = f.read()
+    else:
+        with open(path, "rb") as f:
+            raw = f.read()
     pos, hdus = 0, []
     while pos < len(raw):
         hdr, done = {}, False

@@ -162,3 +162,15 @@ def test_exposure_copy_replaces_the_metrology_table(fits, tmp_path):
     assert h3["PROCSOFT"] == "GPPupilDemodulation.jl" and h3["TUNIT1"] == "us"
     assert d3["VOLT"].tobytes() == new["VOLT"].tobytes() and d3["B"].shape == (10, 32)
     assert out[4][0]["X"] == 1 and out[4][1] is None
+
+
+def test_gzip_input(fits, tmp_path):
+    """.fits.gz exposures (the reference's SUFFIXES, src/GPPupilDemodulation.jl:14) read as is."""
+    import gzip
+    tab = _window_table(N=50)
+    p = str(tmp_path / "a.fits")
+    fits.write_metrology(p, tab, {"X": 1})
+    with open(p, "rb") as f, gzip.open(p + ".gz", "wb") as g:
+        g.write(f.read())
+    (_, _), (h, d) = fits.read_fits(p + ".gz")
+    assert h["X"] == 1 and all(d[k].tobytes() == tab[k].tobytes() for k in tab)
