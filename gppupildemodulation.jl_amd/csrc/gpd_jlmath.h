@@ -349,20 +349,27 @@ JLM_FN jlm_u128 jlm_shr128_nb(jlm_u128 x, int n) {
     const jlm_u128 r = x >> (n & 127), l = x << ((-n) & 127);
     return n >= 0 ? r : l;
 }
+/* 128-bit left shift by 0 ≤ c < 128 */
+JLM_FN jlm_u128 jlm_shl128_nb(jlm_u128 x, int c) { return x << (c & 127); }
+/* jlm_fromfraction through normalised forms: y = |f| << clz(|f|) puts the leading bit at 127, so
+ * z1's 26 bits are y's top 26 (= |f| >> (n1 - 26)) and the remainder x2 = |f| - (those bits) is
+ * y's lower 102 bits >> clz(|f|) — no bit is lost in either shift, so x2's leading 53 bits (z2's
+ * truncated mantissa; zero-padded when x2 has fewer) are those of y2 = y mod 2^102 normalised. */
 JLM_FN void jlm_fromfraction_nb(jlm_i128 f, double *z1, double *z2) {
     const uint64_t s = (uint64_t)(f < 0) << 63;
     const jlm_u128 x = f < 0 ? (jlm_u128)0 - (jlm_u128)f : (jlm_u128)f;
-    const jlm_u128 xs = x | (jlm_u128)(x == 0); /* f = 0: any shape, the result is selected */
-    const int n1 = 128 - jlm_clz128_nb(xs);
-    const uint64_t m1 = (uint64_t)jlm_shr128_nb(xs, n1 - 26) << 27;
+    const int c = jlm_clz128_nb(x | 1); /* f = 0: any shape, the result is selected */
+    const jlm_u128 y = jlm_shl128_nb(x, c);
+    const int n1 = 128 - c;
+    const uint64_t m1 = (uint64_t)(y >> 102) << 27;
     const uint64_t d1 = (uint64_t)(int64_t)(n1 - 128 + 1021) << 52;
-    const jlm_u128 x2 = xs - jlm_shr128_nb((jlm_u128)m1, 53 - n1);
-    const jlm_u128 x2s = x2 | (jlm_u128)(x2 == 0);
-    const int n2 = 128 - jlm_clz128_nb(x2s);
-    const uint64_t m2 = (uint64_t)jlm_shr128_nb(x2s, n2 - 53);
+    const jlm_u128 y2 = y & (((jlm_u128)1 << 102) - 1);
+    const int c2 = jlm_clz128_nb(y2 | 1);
+    const int n2 = 128 - c - c2; /* 128 - clz(x2): clz(x2) = clz(y2) + c */
+    const uint64_t m2 = (uint64_t)(jlm_shl128_nb(y2, c2) >> 75);
     const uint64_t d2 = (uint64_t)(int64_t)(n2 - 128 + 1021) << 52;
     *z1 = f == 0 ? 0.0 : jlm_from_bits(s | (d1 + m1));
-    *z2 = (f == 0 || x2 == 0) ? 0.0 : jlm_from_bits(s | (d2 + m2));
+    *z2 = (f == 0 || y2 == 0) ? 0.0 : jlm_from_bits(s | (d2 + m2));
 }
 /* Payne–Hanek's three words of 2/π for the binade of biased exponent e (k = e - 1075; shift 0
  * takes the words unshifted) */

@@ -245,10 +245,16 @@ def _trig_regime_args(rng, n):
                       np.nextafter(np.pi / 4, 0), 0.0, -0.0, 5e-324, 1e-300, 2.0 ** -27,
                       np.inf, -np.inf, np.nan, 2.0 ** 1023, 1.7e308])
     shift0 = np.ldexp(1.0 + rng.random(2000), rng.integers(1, 16, 2000) * 64 + 11)  # k ≡ 0 mod 64
+    # Payne–Hanek arguments close to multiples of π/2 (small fractions: short normalisations in
+    # fromfraction), and the classic hardest case of double-precision reduction
+    k2 = np.ldexp(np.pi / 2, np.arange(21, 1000))
+    close = np.concatenate([k2, np.nextafter(k2, np.inf), np.nextafter(k2, 0),
+                            [6381956970095103.0 * 2.0 ** 797]])
     sets = [rng.uniform(3.2e10, 3.5e10, n) + rng.uniform(-np.pi, np.pi, n),  # MJD·ω + ϕ
             np.exp(rng.uniform(np.log(7.0), np.log(1.6e6), n)) * rng.choice([-1, 1], n),
             rng.uniform(-7.2, 7.2, n), rng.uniform(-2.6, 2.6, n),
-            np.exp(rng.uniform(np.log(1.7e6), 700, n // 4)), shift0, near, -near, edges, -edges]
+            np.exp(rng.uniform(np.log(1.7e6), 700, n // 4)), shift0, close, -close, near, -near,
+            edges, -edges]
     return np.concatenate(sets)
 
 
