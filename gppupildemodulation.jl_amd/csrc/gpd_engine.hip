@@ -109,18 +109,23 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
         off += align_up(bytes);
         return o;
     };
-    // moment-pass grid: (series groups) × (sample chunks).  The samples are cut into U ≤ 32
+    // moment-pass grid: (series groups) × (sample chunks).  The samples are cut into U ≤ 26
     // fixed units (whole 32-sample tiles, a function of N only) and every unit gets its own set
     // of partial moments, reduced in unit order — so a series' moments do not depend on P, i.e.
     // on the batch or the shard it is in (a sharded run gives the 1-GPU records bit for bit).
     // A workgroup of the producer/consumer kernel (one per CU) streams `upw` consecutive units;
     // upw is chosen to fill the last wave of workgroups: the smallest number of unit-times
     // ceil(npg·ceil(U/upw) / n_cu)·upw, ties to the larger upw (fewer, longer workgroups).
-    // C3 (782 series groups, 256 CUs): upw 2 → 12512 workgroups = 48.9 waves; 12 500 series
-    // per GPU (C4 on 8 GPUs, 98 groups): upw 1 → 3136 = 12.25 waves.
+    // C3 (782 series groups, 256 CUs, U = 26): upw 1 or 2 → 79.4 / 39.7 waves; 12 500 series
+    // per GPU (C4 on 8 GPUs, 98 groups): upw 1 → 2548 workgroups = 9.95 waves (with 32 units:
+    // 12.25 waves, a 0.75-wave tail).
     const long long per = mfma ? MM_PIX : 64;
     const long long npg = (P + per - 1) / per;
-    long long U = std::min<long long>(32, std::max<long long>(1, (N + 255) / 256));
+    // at most 26 units: 26 (not 32) makes both the C3 batch (782 groups: 79.4 waves) and its
+    // 8-way shard of 12 500 series (98 groups: 9.95 waves) fill their last wave of workgroups
+    long long umax = 26;
+    if (const char *e = getenv("GPD_UNITS")) umax = std::max(1LL, atoll(e));  // A/B only
+    long long U = std::min<long long>(umax, std::max<long long>(1, (N + 255) / 256));
     long long ulen = (N + U - 1) / U;
     ulen = (ulen + MM_TS - 1) / MM_TS * MM_TS;
     U = (N + ulen - 1) / ulen;
