@@ -344,11 +344,6 @@ JLM_FN int jlm_clz128_nb(jlm_u128 x) {
     const int ch = __builtin_clzll(hi | 1ull), cl = __builtin_clzll(lo | 1ull);
     return hi ? ch : (lo ? 64 + cl : 128);
 }
-/* jlm_shr128 for |n| < 128 */
-JLM_FN jlm_u128 jlm_shr128_nb(jlm_u128 x, int n) {
-    const jlm_u128 r = x >> (n & 127), l = x << ((-n) & 127);
-    return n >= 0 ? r : l;
-}
 /* 128-bit left shift by 0 ≤ c < 128 */
 JLM_FN jlm_u128 jlm_shl128_nb(jlm_u128 x, int c) { return x << (c & 127); }
 /* jlm_fromfraction through normalised forms: y = |f| << clz(|f|) puts the leading bit at 127, so
