@@ -57,7 +57,7 @@ def _run_bench(nproc, extra, tmp, tag):
     return json.loads(lines[0]), np.load(dump)
 
 
-@pytest.mark.parametrize("nproc", [2, 3])
+@pytest.mark.parametrize("nproc", [2, 3, 4])
 def test_bench_multi_rank_strong_scaling_bitwise(tmp_path, nproc):
     """The multi-rank path of bench.py (torch.distributed.run, barrier, max-over-ranks time,
     gather of the records to rank 0, one JSON line from rank 0) with `nproc` ranks sharing
