@@ -452,7 +452,7 @@ __global__ __launch_bounds__(256) void k_faint_stats(Problem pb, double *__restr
 // same chains as k_faint_stats, so the same bits: a series is split into its FS_G = 8 canonical
 // blocks (part g owns the samples i ≡ 256g + t (mod 2048), t = thread, M = ⌈N/2048⌉ per thread).
 //   k_faint_p1  per (series, part): loads each sample once (non-temporal, two register batches
-//               of FS_U loads in flight), |d| = hypot (branch-free form, 8 evaluations
+//               of FS_U loads in flight), |d| = hypot (branch-free form, FS_U evaluations
 //               interleaved), count / Σ|d| / Σ|d|² per state along the slot chain → the part's
 //               block totals; |d| is written to a scratch buffer;
 //   k_faint_p2  per (series, part): m = the 8 block totals added in block order, then
@@ -464,7 +464,10 @@ __global__ __launch_bounds__(256) void k_faint_stats(Problem pb, double *__restr
 // version holding |d| in LDS ran at one wave per SIMD and spent 4.7 ms on C5, latency-bound).
 // Whole-exposure series; windows take k_faint_stats (per-window spans).
 constexpr int FS_G = 8;  // = CR_BLOCKS, the canonical order's blocks
-constexpr int FS_U = 8;
+#ifndef GPD_FS_U
+#define GPD_FS_U 2  // A/B builds: -DGPD_FS_U=n (C5 statistics: 4 +4 %, 8 +18 %, 16 +95 %)
+#endif
+constexpr int FS_U = GPD_FS_U;
 constexpr int FS_NV = 16;  // payload doubles per block total (15 used)
 
 // Add (1, a, b) to the sums of state q (no state: q < 0) — the chains of k_faint_stats.  A
