@@ -468,6 +468,10 @@ constexpr int FS_G = 8;  // = CR_BLOCKS, the canonical order's blocks
 #define GPD_FS_U 2  // A/B builds: -DGPD_FS_U=n (C5 statistics: 4 +4 %, 8 +18 %, 16 +95 %)
 #endif
 constexpr int FS_U = GPD_FS_U;
+#ifndef GPD_FS_U2
+#define GPD_FS_U2 4  // k_faint_p2 scratch loads per batch (A/B -DGPD_FS_U2=n; 8: +7 %, 16: +24 % on C5)
+#endif
+constexpr int FS_U2 = GPD_FS_U2;
 constexpr int FS_NV = 16;  // payload doubles per block total (15 used)
 
 // Add (1, a, b) to the sums of state q (no state: q < 0) — the chains of k_faint_stats.  A
@@ -615,11 +619,11 @@ __global__ __launch_bounds__(256) void k_faint_p2(Problem pb, int Mmax,
     for (int s = 0; s < 5; ++s) mu[s] = mus[s];
     gd *sp = (gd *)scr + (long long)blockIdx.x * Mmax * 256 + t;
     double sv[5] = {0, 0, 0, 0, 0};
-    for (int mb = 0; mb < M; mb += 8) {
-        int qq[8];
-        double aa[8];
+    for (int mb = 0; mb < M; mb += FS_U2) {
+        int qq[FS_U2];
+        double aa[FS_U2];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < FS_U2; ++u) {
             const int m = mb + u < M ? mb + u : M - 1;
             const int c = gld(pb.state + i0 + 2048LL * m);
             const bool ok = c != -1 && (!only_high || c == 3 || c == 2);
@@ -627,7 +631,7 @@ __global__ __launch_bounds__(256) void k_faint_p2(Problem pb, int Mmax,
             aa[u] = __builtin_nontemporal_load(&sp[(long long)m * 256]);
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < FS_U2; ++u) {
             const int q = qq[u];
             const int q0 = __builtin_amdgcn_readfirstlane(q);
             if (__builtin_amdgcn_ballot_w64(q != q0) == 0) {  // one state across the wave
