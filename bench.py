@@ -58,6 +58,11 @@ def parse():
                     help="0: the CPUs this process may run on (sched_getaffinity), capped by "
                          "OMP_NUM_THREADS when the pool sets it (the box's CPU share)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dist-always", action="store_true",
+                    help="initialise torch.distributed even at world size 1 (launch with "
+                         "torch.distributed.run --nproc-per-node 1) and send the records through "
+                         "the gather and the time through all_reduce: the RCCL branch of an "
+                         "8-GPU run, exercised on one GPU")
     ap.add_argument("--storage", default="c64", choices=["c64", "c32"],
                     help="c32: series/FC kept as ComplexF32 in HBM (FITS VOLT precision, "
                          "gpd_fit_batch_c32_dev; arithmetic stays fp64)")
@@ -88,7 +93,8 @@ def main():
     if backend != "nccl":
         local = local % max(1, torch.cuda.device_count())
     dist = None
-    if world > 1:
+    use_dist = world > 1 or args.dist_always
+    if use_dist:
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
@@ -154,10 +160,10 @@ def main():
                     fcop.data_ptr(), None, gpd.M_2PI, None, flags, 60,
                     params.data_ptr(), None, N, local, sptr, err, len(err))
         gpd._lib.check(r, err)
-        if backend != "nccl" and world > 1:
-            g = shard.gather_records(params.cpu(), world, rank, counts=counts)
+        if backend != "nccl" and use_dist:
+            g = shard.gather_records(params.cpu(), world, rank, counts=counts, force=use_dist)
             return None if g is None else g.to(dev)
-        return shard.gather_records(params, world, rank, counts=counts)
+        return shard.gather_records(params, world, rank, counts=counts, force=use_dist)
 
     log = (lambda msg: print(f"[bench] rank {rank}: {msg}", file=sys.stderr, flush=True))
     log(f"{P} series x {N} samples resident; {args.warmup} warmup + {args.steps} timed steps")
@@ -191,7 +197,7 @@ def main():
             dist.destroy_process_group()
         return
     if args.dump_records:
-        recs = (gathered if world > 1 else params).cpu().numpy().reshape(-1).view(gpd.PARAM_DTYPE)
+        recs = (gathered if use_dist else params).cpu().numpy().reshape(-1).view(gpd.PARAM_DTYPE)
         np.save(args.dump_records, recs)
 
     # --- roofline of the dominant kernel (harmonic moment pass) ---------------------------
@@ -275,7 +281,7 @@ def main():
                    "series_per_gpu": P, "samples": N, "total_series": P_total,
                    "method": args.method, "t0": args.t0, "storage": args.storage,
                    "parallelism": f"series-shard x{world}",
-                   "gather": ("none" if world == 1 else "RCCL gather of 64-B records to rank 0"
+                   "gather": ("none" if not use_dist else "RCCL gather of 64-B records to rank 0"
                               if backend == "nccl" else f"{backend} gather (multi-rank rehearsal)")},
         "roofline": roofline, "cpu_baseline": cpu, "kernels_ms": kernels, "fits": fits,
         "all_f64_moments": f64_all,

@@ -32,15 +32,18 @@ def weak_offset(per_rank: int, rank: int) -> int:
     return rank * per_rank
 
 
-def gather_records(local, world: int, rank: int, dst: int = 0, group=None, counts=None):
+def gather_records(local, world: int, rank: int, dst: int = 0, group=None, counts=None,
+                   force: bool = False):
     """Gather record tensors (uint8, n×64) to `dst`; returns the concatenation in rank order on
     dst, None elsewhere.  `counts` (records per rank, e.g. from shard_range) allows unequal
     shards: every rank sends max(counts) rows (one collective, the padding trimmed on dst).
-    Works for CUDA tensors under nccl (RCCL) and CPU tensors under gloo."""
+    Works for CUDA tensors under nccl (RCCL) and CPU tensors under gloo.  At world size 1 the
+    records are returned as they are, unless `force` (an initialised process group of one rank:
+    the collective then runs, e.g. bench.py --dist-always)."""
     import torch
     import torch.distributed as dist
 
-    if world == 1:
+    if world == 1 and not force:
         return local
     n = local.shape[0]
     if counts is None:

@@ -34,12 +34,12 @@ def test_bench_json_contract():
     assert out["fits"]["nan"] == 0
 
 
-def _run_bench(nproc, extra, tmp, tag):
+def _run_bench(nproc, extra, tmp, tag, backend="gloo", launcher=None):
     import socket
     dump = os.path.join(tmp, f"rec_{tag}.npy")
     args = [os.path.join(ROOT, "bench.py"), "--pixels", "520", "--samples", "4096", "--steps", "2",
             "--warmup", "1", "--no-cpu", "--no-f64", "--dump-records", dump, *extra]
-    if nproc == 1:
+    if nproc == 1 and not launcher:
         cmd = [sys.executable, *args]
     else:
         with socket.socket() as so:  # a free rendezvous port on this box
@@ -48,7 +48,7 @@ def _run_bench(nproc, extra, tmp, tag):
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
                str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(port), *args,
                "--gpus", str(nproc)]
-    env = dict(os.environ, GPD_DIST_BACKEND="gloo")
+    env = dict(os.environ, GPD_DIST_BACKEND=backend)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -76,3 +76,17 @@ def test_bench_multi_rank_strong_scaling_bitwise(tmp_path, nproc):
 def test_bench_weak_scaling_label(tmp_path):
     out, rn = _run_bench(2, ["--scaling", "weak"], str(tmp_path), "w")
     assert out["scaling"] == "weak" and out["config"]["total_series"] == 1040 and len(rn) == 1040
+
+
+def test_bench_rccl_branch_at_world_one(tmp_path):
+    """The branch an 8-GPU node runs (BASELINE C4), executed on one GPU: bench.py under
+    torch.distributed.run with one rank and the default "nccl" backend (= RCCL), --dist-always
+    sending the records through shard.gather_records (dist.gather of device uint8 records), the
+    barriers and the max-over-ranks time through a device all_reduce.  The gathered records
+    equal the plain run's byte for byte (src/Modulation.jl:387-389: series are independent)."""
+    one, r1 = _run_bench(1, [], str(tmp_path), "plain")
+    out, rd = _run_bench(1, ["--dist-always"], str(tmp_path), "rccl", backend="nccl",
+                         launcher="torchrun")
+    assert out["config"]["gather"].startswith("RCCL gather"), out["config"]
+    assert out["n_gpus"] == 1 and out["value"] > 0
+    assert len(rd) == 520 and r1.tobytes() == rd.tobytes(), "RCCL-gathered records differ"
