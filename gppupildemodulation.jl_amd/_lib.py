@@ -28,6 +28,7 @@ GPD_ST_MAXFUN = 0x2
 GPD_ST_NAN = 0x4
 GPD_ST_EXACT = 0x8
 GPD_ST_FALLBACK = 0x10
+GPD_ST_SYNC = 0x20
 
 GPD_OK = 0
 GPD_E_ARG = -1

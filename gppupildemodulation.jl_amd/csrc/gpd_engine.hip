@@ -595,8 +595,11 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             k_phasor<<<g, 256, 0, stream>>>(pb, ph);
             mark("phasor");
         }
-        if (exact_g > 1)
+        if (exact_g > 1) {
             HIP_TRY(hipMemsetAsync(ws + L.xcnt, 0, (size_t)(P + 3) / 4 * 16, stream));
+            // GPD_XSPIN_TEST=1 (tests): the per-series barrier gives up at once (poison path)
+            if (getenv("GPD_XSPIN_TEST") && atoi(getenv("GPD_XSPIN_TEST")) > 0) pb.flags |= F_XSPIN_TEST;
+        }
         // GPD_FIT_PROF (diagnostics): per-phase cycles of the multi-workgroup exact fit
         static const bool xprof = getenv("GPD_FIT_PROF") != nullptr;
         unsigned long long zx[4] = {0, 0, 0, 0};
@@ -1123,7 +1126,10 @@ int gpd_mean_var_power(int64_t n_samples, int64_t n_series, const gpd_c64 *d, in
         set_err(errbuf, errlen, "gpd_mean_var_power: no HIP device visible");
         return GPD_E_NODEV;
     }
-    if (device < 0 || device >= ndev) return GPD_E_ARG;
+    if (device < 0 || device >= ndev) {
+        set_err(errbuf, errlen, "gpd_mean_var_power: device %d out of range", device);
+        return GPD_E_ARG;
+    }
     HIP_TRY(hipSetDevice(device));
     const long long N = n_samples, P = n_series;
     const bool fs1 =

@@ -33,9 +33,13 @@ __device__ __constant__ const double c_phi_grid[8] = {
     0x1.cb91f3bbba140p-2,  0x1.58ad76cccb8f0p+0,  0x1.1f3b3855544c8p+1,  0x1.921fb54442d18p+1};
 
 // status bits (mirror include/gpdemod.h)
-constexpr int ST_REFIT = 0x1, ST_MAXFUN = 0x2, ST_NAN = 0x4, ST_EXACT = 0x8, ST_FALLBACK = 0x10;
+constexpr int ST_REFIT = 0x1, ST_MAXFUN = 0x2, ST_NAN = 0x4, ST_EXACT = 0x8, ST_FALLBACK = 0x10,
+              ST_SYNC = 0x20;
 constexpr uint32_t F_OFFSETS = 0x1u, F_RECENTER = 0x2u, F_ONLY_HIGH = 0x4u;
 constexpr uint32_t F_PROF = 0x80000000u;  // internal: k_fit_harmonic cycle split (GPD_FIT_PROF)
+// internal (tests, GPD_XSPIN_TEST=1): the multi-workgroup exact fit's barrier gives up at once
+// instead of after ~1 s, so the give-up path (poisoned series, GPD_ST_SYNC) runs on demand
+constexpr uint32_t F_XSPIN_TEST = 0x40000000u;
 __device__ unsigned long long g_fitprof[4];  // [0] objective cycles, [1] whole-fit cycles, [2] evals
 
 struct Param {  // == gpd_param
@@ -1653,7 +1657,7 @@ struct ExactChi2 {
     int G, g;
     Xchg x;
     unsigned nbar;  // barriers passed
-    bool sync_fail; // a barrier spin gave up (never observed; the series reports NaN)
+    bool sync_fail; // the series' barrier was poisoned (never observed; NaN, GPD_ST_SYNC)
     // GPD_FIT_PROF (diagnostics): cycles of the first pass, the residual pass, the G > 1
     // exchange (barrier) and the whole fit, per workgroup
     bool prof;
@@ -1850,24 +1854,38 @@ struct ExactChi2 {
     }
 
     // Per-series barrier of the G workgroups (G > 1); the caller has issued its payload stores.
+    // A part that waits too long (~1 s: a sibling is not resident — never observed) poisons the
+    // series' arrival counter with XPOISON by compare-and-swap, unless the last sibling arrived
+    // meanwhile.  Every part of the series reads the poison at this same barrier (its own add or
+    // its wait returns the poisoned count), so all G parts set sync_fail together, skip every
+    // later pass and barrier (NaN totals), and the record carries GPD_ST_SYNC | GPD_ST_NAN.
+    static constexpr unsigned XPOISON = 0x80000000u;
     __device__ __forceinline__ void xbarrier() {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
         __syncthreads();
         ++nbar;
         if (threadIdx.x == 0) {
-            __hip_atomic_fetch_add((gu32 *)x.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned target = nbar * (unsigned)G;
+            const unsigned spin_max = (pb->flags & F_XSPIN_TEST) ? 0u : (1u << 24);
+            unsigned c = __hip_atomic_fetch_add((gu32 *)x.cnt, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT) + 1u;
             unsigned spins = 0;
-            while (__hip_atomic_load((gu32 *)x.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                   target) {
-                __builtin_amdgcn_s_sleep(2);
-                if (++spins > (1u << 24)) {  // ~1 s: a sibling is not resident (never expected)
-                    sync_fail = true;
-                    break;
+            while (!(c & XPOISON) && c < target) {
+                if (++spins > spin_max) {
+                    // give up, unless the count moved on (c is refreshed by a failed CAS)
+                    if (__hip_atomic_compare_exchange_strong((gu32 *)x.cnt, &c, c | XPOISON,
+                                                             __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT)) {
+                        c |= XPOISON;
+                        break;
+                    }
+                    continue;
                 }
+                __builtin_amdgcn_s_sleep(2);
+                c = __hip_atomic_load((gu32 *)x.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            ((ldouble *)lds)[CR_FLAG] = sync_fail ? 1.0 : 0.0;
+            ((ldouble *)lds)[CR_FLAG] = (c & XPOISON) ? 1.0 : 0.0;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -1888,6 +1906,11 @@ struct ExactChi2 {
     template <int NV, class C>
     __device__ __forceinline__ void cr_sum_blocks(C &&chain, double (&tot)[NV]) {
         ldouble *lp = (ldouble *)lds;
+        if (sync_fail) {  // the series' barrier was poisoned: every part stops passing samples
+#pragma unroll
+            for (int k = 0; k < NV; ++k) tot[k] = __builtin_nan("");
+            return;
+        }
         const int nb = CR_BLOCKS / G, b0 = g * nb;
         for (int blk = b0; blk < b0 + nb; ++blk) {
             double acc[NV];
@@ -2167,6 +2190,7 @@ __global__ __launch_bounds__(EXACT_WG) void k_fit_exact(Problem pb, const Info *
         const unsigned long long tf = f.prof ? __builtin_amdgcn_s_memtime() : 0;
         drive_fit(f, pb, x, status, nwx[threadIdx.x >> 6]);
         const double chi2 = f(x);
+        if (f.sync_fail) status |= ST_SYNC;
         if (g == 0 && threadIdx.x == 0)
             store_param(out, raw, k, f.c_re, f.c_im, f.a_re, f.a_im, x[0], x[1], chi2, f.nfev, status);
         if (f.prof && threadIdx.x == 0) {

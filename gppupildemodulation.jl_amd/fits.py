@@ -27,15 +27,32 @@ CARD = 80
 _TFORM = {np.dtype(np.float32): "E", np.dtype(np.float64): "D", np.dtype(np.uint8): "B",
           np.dtype(np.int8): "B", np.dtype(np.int16): "I", np.dtype(np.int32): "J",
           np.dtype(np.int64): "K", np.dtype(np.bool_): "L", np.dtype(np.complex64): "C",
-          np.dtype(np.complex128): "M"}
+          np.dtype(np.complex128): "M", np.dtype(np.uint16): "I", np.dtype(np.uint32): "J",
+          np.dtype(np.uint64): "K"}
 _CODE = {"E": ">f4", "D": ">f8", "B": "u1", "I": ">i2", "J": ">i4", "K": ">i8", "L": "S1",
          "C": ">c8", "M": ">c16"}
+# the standard's unsigned-integer convention (CFITSIO writes it for UInt16/32/64 columns):
+# stored signed value + TZERO; flipping the sign bit is exactly that offset
+_UNSIGNED = {"I": (np.uint16, np.int16, 1 << 15), "J": (np.uint32, np.int32, 1 << 31),
+             "K": (np.uint64, np.int64, 1 << 63)}
+# bytes per repeat of the column types read as raw bytes (variable-length descriptors, bits)
+_RAW_WIDTH = {"P": 8, "Q": 16}
 _STRUCTURAL = ("SIMPLE", "XTENSION", "BITPIX", "NAXIS", "PCOUNT", "GCOUNT", "TFIELDS", "EXTEND",
-               "TTYPE", "TFORM", "TZERO", "TSCAL", "TDIM", "TUNIT", "EXTNAME", "END")
+               "TTYPE", "TFORM", "TZERO", "TSCAL", "TDIM", "TUNIT", "EXTNAME", "END",
+               # column-bound or content-bound cards CFITSIO reserves: a re-encoded table gets
+               # new column numbers and new data, so old TDISPn / TNULLn / THEAP and the
+               # checksums of the old bytes would be wrong (FITSIO's write_header drops them)
+               "TDISP", "TNULL", "THEAP", "CHECKSUM", "DATASUM")
+COMMENTARY = "__commentary__"  # header key of the COMMENT / HISTORY cards (raw 80-char cards)
 
 
 def _is_structural(key: str) -> bool:
-    return any(key == s or (key.startswith(s) and key[len(s):].isdigit()) for s in _STRUCTURAL)
+    return key == COMMENTARY or any(
+        key == s or (key.startswith(s) and key[len(s):].isdigit()) for s in _STRUCTURAL)
+
+
+def _commentary_cards(header: dict | None) -> list[str]:
+    return list((header or {}).get(COMMENTARY, []))
 
 
 def format_float(v: float) -> str:
@@ -112,6 +129,10 @@ def _columns(table: dict):
         if a.dtype == np.int8:
             tzero = -128
             a = (a.astype(np.int16) + 128).astype(np.uint8)
+        elif a.dtype.kind == "u" and letter in _UNSIGNED:
+            ut, st, off = _UNSIGNED[letter]
+            tzero = off
+            a = (a ^ ut(off)).view(st)
         elif a.dtype == np.bool_:
             a = np.where(a, b"T", b"F")
         fdt = np.dtype(_CODE[letter]) if a.ndim == 1 else np.dtype((_CODE[letter], (r,)))
@@ -141,6 +162,7 @@ def bintable_hdu(table: dict, header: dict | None = None, *, extname: str | None
     for k, v in (header or {}).items():
         if not _is_structural(k):
             cards.append(card(k, v))
+    cards += _commentary_cards(header)
     body = data.tobytes()
     body += b"\0" * (-len(body) % BLOCK)
     return _header_bytes(cards) + body
@@ -152,7 +174,7 @@ def primary_hdu(header: dict | None = None) -> bytes:
     for k, v in (header or {}).items():
         if not _is_structural(k):
             cards.append(card(k, v))
-    return _header_bytes(cards)
+    return _header_bytes(cards + _commentary_cards(header))
 
 
 _BITPIX_DTYPE = {8: "u1", 16: ">i2", 32: ">i4", 64: ">i8", -32: ">f4", -64: ">f8"}
@@ -182,7 +204,7 @@ def image_hdu(data, header: dict | None = None, *, primary: bool = False,
     for k, v in (header or {}).items():
         if not _is_structural(k):
             cards.append(card(k, v))
-    return _header_bytes(cards) + body
+    return _header_bytes(cards + _commentary_cards(header)) + body
 
 
 def write_fits(path: str, hdus) -> None:
@@ -211,22 +233,47 @@ def fits_copy(dst: str, src: str, content: dict | None = None,
               headers: dict | None = None) -> None:
     """FitsUtils.FITScopy!(dst, src, content, header) (src/FitsUtils.jl:96-154): every HDU of src
     copied to dst, the HDUs named in `content` / `headers` (EXTNAME → table dict or array /
-    header dict) replaced, names absent from src appended after it."""
+    header dict) replaced, names absent from src appended after it.  HDUs that are not replaced
+    are copied byte for byte (any column type, scaling, checksum or commentary card stays as the
+    source holds it).  A replaced table keeps the source's TUNITs and COMMENT/HISTORY cards; a
+    header-only replacement keeps the source's column cards and data bytes."""
     content, headers = dict(content or {}), dict(headers or {})
+    raw = _read_raw(src)
     out = []
-    for hdr, data in read_fits(src):
+    for a, hb, e, hdr in _hdu_spans(raw):
         name = hdr.get("EXTNAME")
-        h = headers.pop(name, hdr) if name is not None else hdr
-        d = content.pop(name, data) if name is not None else data
-        if isinstance(d, dict) and "TFIELDS" in hdr and h is not hdr:
-            h = {**{k: v for k, v in hdr.items() if k.startswith("TUNIT") or k.startswith("TTYPE")},
-                 **h}
-        out.append((dict(h, EXTNAME=name) if name is not None else h, d))
+        if name is None or (name not in content and name not in headers):
+            out.append(raw[a:e])
+            continue
+        h = headers.pop(name, hdr)
+        if COMMENTARY not in h and hdr.get(COMMENTARY):
+            h = dict(h, **{COMMENTARY: hdr[COMMENTARY]})
+        if name in content:
+            d = content.pop(name)
+            if isinstance(d, dict) and "TFIELDS" in hdr and h is not hdr:
+                h = {**{k: v for k, v in hdr.items()
+                        if k.startswith("TUNIT") or k.startswith("TTYPE")}, **h}
+            h = dict(h, EXTNAME=name)
+            if isinstance(d, dict):
+                out.append(bintable_hdu(d, h, extname=name, units=_units_of(h)))
+            else:
+                out.append(image_hdu(d, h, primary=a == 0, extname=name))
+            continue
+        # header only: the source's structural / column cards and its data bytes, new keywords
+        keep = [raw[j:j + CARD].decode("ascii") for j in range(a, hb, CARD)]
+        keep = [c for c in keep if _card_key(c) is not None and _is_structural(_card_key(c))
+                and _card_key(c) not in ("END", "CHECKSUM", "DATASUM")]
+        cards = keep + [card(k, v) for k, v in h.items() if not _is_structural(k)]
+        out.append(_header_bytes(cards + _commentary_cards(h)) + raw[hb:e])
     for name, d in content.items():
-        out.append((dict(headers.pop(name, {}), EXTNAME=name), d))
+        h = dict(headers.pop(name, {}), EXTNAME=name)
+        out.append(bintable_hdu(d, h, extname=name, units=_units_of(h)) if isinstance(d, dict)
+                   else image_hdu(d, h, extname=name))
     for name, h in headers.items():
-        out.append((dict(h, EXTNAME=name), None))
-    write_fits(dst, out)
+        out.append(image_hdu(None, dict(h, EXTNAME=name), extname=name))
+    with open(dst, "wb") as f:
+        for b in out:
+            f.write(b)
 
 
 def write_metrology(path: str, table: dict, header: dict, *, primary_header: dict | None = None,
@@ -274,20 +321,40 @@ def parse_card(text: str):
     return key, _parse_value(text[10:])
 
 
-def read_fits(path: str):
-    """[(header dict, data)] per HDU (path may be gzip-compressed, .gz): None for an empty HDU,
-    an ndarray for an image, a dict of columns for a BINTABLE
-    ((N,) or (N, r) arrays in native byte order; TZERO -128 bytes back to Int8)."""
+def _card_key(text: str):
+    if text.startswith("HIERARCH "):
+        return text[9:].partition("=")[0].strip()
+    key = text[:8].strip()
+    if key == "END":
+        return key
+    return key if text[8:10] == "= " else None
+
+
+def _read_raw(path: str) -> bytes:
     if str(path).endswith(".gz"):  # the reference's SUFFIXES include .fits.gz (CFITSIO reads it)
         import gzip
         with gzip.open(path, "rb") as f:
-            raw = f.read()
-    else:
-        with open(path, "rb") as f:
-            raw = f.read()
-    pos, hdus = 0, []
+            return f.read()
+    with open(path, "rb") as f:
+        return f.read()
+
+
+def _data_size(hdr: dict) -> int:
+    if hdr.get("XTENSION") == "BINTABLE":
+        return hdr["NAXIS2"] * hdr["NAXIS1"] + hdr.get("PCOUNT", 0)
+    n = hdr.get("NAXIS", 0)
+    if n == 0:
+        return 0
+    count = int(np.prod([hdr[f"NAXIS{j}"] for j in range(1, n + 1)]))
+    return (count * abs(hdr["BITPIX"]) // 8 + hdr.get("PCOUNT", 0)) * hdr.get("GCOUNT", 1)
+
+
+def _hdu_spans(raw: bytes):
+    """(start, end of header, end of data, header dict) of every HDU; the header dict holds the
+    COMMENT / HISTORY cards as raw text under COMMENTARY."""
+    pos = 0
     while pos < len(raw):
-        hdr, done = {}, False
+        a, hdr, comm, done = pos, {}, [], False
         while not done:
             block = raw[pos:pos + BLOCK].decode("ascii")
             pos += BLOCK
@@ -299,43 +366,77 @@ def read_fits(path: str):
                 k, v = parse_card(c)
                 if k is not None:
                     hdr[k] = v
+                elif c[:8].strip() in ("COMMENT", "HISTORY"):
+                    comm.append(c)
+        if comm:
+            hdr[COMMENTARY] = comm
+        size = _data_size(hdr)
+        e = pos + size + (-size % BLOCK)
+        yield a, pos, e, hdr
+        pos = e
+
+
+def _column(a, hdr: dict, i: int, letter: str):
+    """Field values of column i with the header's TZERO / TSCAL applied as CFITSIO does
+    (Int8 and unsigned-integer offsets exactly, other scalings as Float64)."""
+    tz, ts = hdr.get(f"TZERO{i}"), hdr.get(f"TSCAL{i}", 1)
+    a = a.astype(a.dtype.newbyteorder("="))
+    if tz is None and ts == 1:
+        return a
+    if letter == "B" and tz == -128 and ts == 1:
+        return (a.astype(np.int16) - 128).astype(np.int8)
+    if letter in _UNSIGNED and ts == 1 and tz == _UNSIGNED[letter][2]:
+        ut, _, off = _UNSIGNED[letter]
+        return a.view(ut) ^ ut(off)
+    return a.astype(np.float64) * ts + (tz or 0)
+
+
+def read_fits(path: str):
+    """[(header dict, data)] per HDU (path may be gzip-compressed, .gz): None for an empty HDU,
+    an ndarray for an image, a dict of columns for a BINTABLE ((N,) or (N, r) arrays in native
+    byte order, TZERO/TSCAL applied: Int8 and UInt16/32/64 offsets exactly; variable-length
+    (P/Q) descriptors and bit (X) columns as raw bytes, the heap not read)."""
+    raw = _read_raw(path)
+    hdus = []
+    for _, pos, _, hdr in _hdu_spans(raw):
         data = None
         if hdr.get("XTENSION") == "BINTABLE":
             n, width, k = hdr["NAXIS2"], hdr["NAXIS1"], hdr["TFIELDS"]
-            fields = []
+            fields, letters = [], []
             for i in range(1, k + 1):
                 tform = hdr[f"TFORM{i}"].strip()
-                r, letter = (int(tform[:-1]) if len(tform) > 1 else 1), tform[-1]
+                letter = tform.lstrip("0123456789")[:1]
+                rs = tform[:len(tform) - len(tform.lstrip("0123456789"))]
+                r = int(rs) if rs else 1
+                letters.append(letter)
+                name = hdr.get(f"TTYPE{i}", f"COL{i}")
                 if letter == "A":
-                    fields.append((hdr[f"TTYPE{i}"], f"S{r}"))
-                    continue
-                if letter not in _CODE:
-                    raise NotImplementedError(f"TFORM {tform} (column {hdr[f'TTYPE{i}']})")
-                fields.append((hdr[f"TTYPE{i}"], _CODE[letter] if r == 1 else (_CODE[letter], (r,))))
+                    fields.append((name, f"S{r}"))
+                elif letter in _CODE:
+                    fields.append((name, _CODE[letter] if r == 1 else (_CODE[letter], (r,))))
+                elif letter in _RAW_WIDTH or letter == "X":
+                    nb = r * _RAW_WIDTH[letter] if letter in _RAW_WIDTH else (r + 7) // 8
+                    fields.append((name, f"V{nb}"))
+                else:
+                    raise NotImplementedError(f"TFORM {tform} (column {name})")
             rec = np.dtype(fields)
             if rec.itemsize != width:
                 raise ValueError(f"NAXIS1 {width} != row size {rec.itemsize}")
             rows = np.frombuffer(raw, dtype=rec, count=n, offset=pos)
             data = {}
-            for i, (name, _) in enumerate(fields, 1):
+            for i, ((name, _), letter) in enumerate(zip(fields, letters), 1):
                 a = rows[name]
-                if hdr.get(f"TZERO{i}") == -128 and a.dtype == np.uint8:
-                    a = (a.astype(np.int16) - 128).astype(np.int8)
-                elif a.dtype.kind == "S" and hdr[f"TFORM{i}"].strip().endswith("L"):
+                if letter == "L":
                     a = a == b"T"
-                elif a.dtype.kind == "S":
+                elif a.dtype.kind in "SV":
                     a = a.copy()
                 else:
-                    a = a.astype(a.dtype.newbyteorder("="))
+                    a = _column(a, hdr, i, letter)
                 data[name] = a
-            size = n * width + hdr.get("PCOUNT", 0)  # the heap is skipped (no P/Q columns)
-            pos += size + (-size % BLOCK)
         elif hdr.get("NAXIS", 0) != 0:  # image: raw values, BZERO/BSCALE left in the header
             shape = tuple(hdr[f"NAXIS{j}"] for j in range(hdr["NAXIS"], 0, -1))
             dt = np.dtype(_BITPIX_DTYPE[hdr["BITPIX"]])
-            size = int(np.prod(shape)) * dt.itemsize
             img = np.frombuffer(raw, dtype=dt, count=int(np.prod(shape)), offset=pos)
             data = img.reshape(shape).astype(dt.newbyteorder("="))
-            pos += size + (-size % BLOCK)
         hdus.append((hdr, data))
     return hdus

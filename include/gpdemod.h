@@ -64,6 +64,9 @@ typedef struct {
 #define GPD_ST_NAN 0x4      /* final χ² is NaN (e.g. a 1-sample faint state, src/Faint.jl:97)*/
 #define GPD_ST_EXACT 0x8    /* fitted with the exact per-sample evaluator                    */
 #define GPD_ST_FALLBACK 0x10 /* harmonic evaluator left its safe |b| range → exact re-fit     */
+#define GPD_ST_SYNC 0x20    /* multi-workgroup exact fit: a per-series barrier gave up (a part
+                               not resident after ~1 s; never observed) — every part stopped,
+                               the record is NaN (with GPD_ST_NAN)                            */
 
 /* error codes (negative) */
 #define GPD_OK 0

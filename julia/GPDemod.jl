@@ -37,6 +37,7 @@ const GPD_ST_MAXFUN = 0x2
 const GPD_ST_NAN = 0x4
 const GPD_ST_EXACT = 0x8
 const GPD_ST_FALLBACK = 0x10
+const GPD_ST_SYNC = 0x20
 
 """Throw on a negative status, with the library's message (as `fits_assert_ok`)."""
 function gpd_assert_ok(rc::Integer, err::Vector{UInt8})
@@ -127,17 +128,23 @@ function demodulateall_gpu(timestamp::AbstractVector, data::AbstractMatrix{Compl
         end
         gpd_assert_ok(rc, err)
     end
-    output = copy(data)                 # FC columns 33..40 pass through, eltype kept (:353)
-    output[:, 1:32] .= demod
-    param = fitoffsets ? [ModulationWithOffsets{T}(p.c, p.a, p.b, p.ϕ, M_2PI) for p in params] :
-                         [ModulationNoOffsets{T}(p.a, p.b, p.ϕ, M_2PI) for p in params]
-    return (output, param, [p.chi2 for p in params])
+    # the reference's return types (src/Modulation.jl:353-359, 434): output = copy(data) keeps
+    # Matrix{Complex{T}} (FC columns 33..40 pass through), param::Vector{Modulation…{T}},
+    # likelihood::Vector{T}; the library's Float64 results are converted to T
+    output = copy(data)
+    output[:, 1:32] .= Complex{T}.(demod)
+    param = fitoffsets ?
+        ModulationWithOffsets{T}[ModulationWithOffsets{T}(p.c, p.a, p.b, p.ϕ, M_2PI) for p in params] :
+        ModulationNoOffsets{T}[ModulationNoOffsets{T}(p.a, p.b, p.ϕ, M_2PI) for p in params]
+    likelihood = T[p.chi2 for p in params]
+    return (output, param, likelihood)
 end
 
 """χ²(b, ϕ) of the 32 diodes at caller-given points (the `lkl` functor, src/Modulation.jl:318-330)."""
-function chi2_gpu(timestamp::AbstractVector, data::AbstractMatrix, bphi::AbstractMatrix;
+function chi2_gpu(timestamp::AbstractVector, data::AbstractMatrix{Complex{T}}, bphi::AbstractMatrix;
                   faintparam=nothing, onlyhigh::Bool=false, fitoffsets::Bool=false,
-                  preswitchdelay=0.01, postwitchdelay=0.3, method::Symbol=:auto, n_gpus::Integer=1)
+                  preswitchdelay=0.01, postwitchdelay=0.3, method::Symbol=:auto,
+                  n_gpus::Integer=1) where {T<:AbstractFloat}
     N = size(data, 1)
     t = Vector{Float64}(timestamp)
     d = Matrix{ComplexF64}(data)
@@ -158,7 +165,7 @@ function chi2_gpu(timestamp::AbstractVector, data::AbstractMatrix, bphi::Abstrac
                    err, length(err))
         gpd_assert_ok(rc, err)
     end
-    return [p.chi2 for p in params]
+    return T[p.chi2 for p in params]    # lkl returns T (src/Modulation.jl:318-326)
 end
 
 """

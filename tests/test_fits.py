@@ -174,3 +174,77 @@ def test_gzip_input(fits, tmp_path):
         g.write(f.read())
     (_, _), (h, d) = fits.read_fits(p + ".gz")
     assert h["X"] == 1 and all(d[k].tobytes() == tab[k].tobytes() for k in tab)
+
+
+def _hdu(fits, cards, body=b""):
+    body = body + b"\0" * (-len(body) % fits.BLOCK)
+    return fits._header_bytes([c if len(c) == 80 else fits.card(*c) for c in cards]) + body
+
+
+def test_copy_keeps_untouched_hdus_byte_for_byte(fits, tmp_path):
+    """FITScopy! passes every HDU it does not replace through CFITSIO unchanged: an unsigned
+    (TZERO = 32768) column, a variable-length (P) column with its heap and a CHECKSUM card in an
+    unrelated table come out byte for byte.  The replaced METROLOGY table drops the old
+    CHECKSUM/DATASUM and column-bound TDISPn/TNULLn (new columns, new bytes) and keeps its
+    COMMENT/HISTORY cards; a header-only replacement keeps the data bytes."""
+    import struct
+    rows = b"".join(struct.pack(">iiH", 2, 2 * j, u ^ 0x8000) for j, u in enumerate((0, 40000, 65535)))
+    heap = bytes([1, 2, 3, 4, 5, 6])
+    other = _hdu(fits, [("XTENSION", "BINTABLE"), ("BITPIX", 8), ("NAXIS", 2), ("NAXIS1", 10),
+                        ("NAXIS2", 3), ("PCOUNT", len(heap)), ("GCOUNT", 1), ("TFIELDS", 2),
+                        ("TTYPE1", "VARCOL"), ("TFORM1", "1PB(2)"), ("TTYPE2", "U"),
+                        ("TFORM2", "1I"), ("TZERO2", 32768), ("EXTNAME", "OI_OTHER"),
+                        ("CHECKSUM", "9aJ5AaG49aG4AaG4"), ("DATASUM", "12345")], rows + heap)
+    met = {"TIME": np.arange(4, dtype=np.int32), "VOLT": np.ones((4, 80), np.float32)}
+    mb = fits.bintable_hdu(met, {"TUNIT1": "us"}, extname="METROLOGY", units={"TIME": "us"})
+    hdr_end = mb.index(b"END" + b" " * 77)
+    extra = "".join(fits.card(*c) for c in [("TDISP2", "E15.7"), ("TNULL1", -1),
+                                            ("CHECKSUM", "0000000000000000"), ("DATASUM", "42")])
+    extra += fits.card("COMMENT", "metrology of the four telescopes")
+    extra += fits.card("HISTORY", "written by the instrument")
+    mb = mb[:hdr_end] + extra.encode() + mb[hdr_end:]
+    # re-block the header (the inserted cards may overflow its last block)
+    cards = [mb[j:j + 80].decode() for j in range(0, mb.index(b"END" + b" " * 77), 80)]
+    data_at = (mb.index(b"END" + b" " * 77) // 2880 + 1) * 2880
+    mb = _hdu(fits, cards, mb[data_at:].rstrip(b"\0") or b"")
+    src, dst, dst2 = (str(tmp_path / n) for n in ("s.fits", "d.fits", "h.fits"))
+    with open(src, "wb") as f:
+        f.write(fits.primary_hdu({"MJD-OBS": 58849.5}) + other + mb)
+    hdus = fits.read_fits(src)
+    u = hdus[1][1]["U"]
+    assert u.dtype == np.uint16 and list(u) == [0, 40000, 65535]
+    assert hdus[1][1]["VARCOL"].dtype.kind == "V"
+    h_met = hdus[2][0]
+    assert h_met["CHECKSUM"] == "0000000000000000" and len(h_met[fits.COMMENTARY]) == 2
+    new = dict(met, B=np.zeros((4, 32), np.float32))
+    fits.fits_copy(dst, src, {"METROLOGY": new}, {"METROLOGY": dict(h_met, PROCSOFT="x")})
+    raw_src, raw_dst = open(src, "rb").read(), open(dst, "rb").read()
+    assert raw_dst[:2880 + len(other)] == raw_src[:2880 + len(other)]  # primary + OI_OTHER
+    out = fits.read_fits(dst)
+    h3, d3 = out[2]
+    for k in ("CHECKSUM", "DATASUM", "TDISP2", "TNULL1"):
+        assert k not in h3, k
+    assert h3["PROCSOFT"] == "x" and h3["TUNIT1"] == "us"
+    assert [c[:8].strip() for c in h3[fits.COMMENTARY]] == ["COMMENT", "HISTORY"]
+    assert d3["B"].shape == (4, 32) and list(out[1][1]["U"]) == [0, 40000, 65535]
+    # header-only replacement: the column cards and the data bytes of the source
+    fits.fits_copy(dst2, src, None, {"OI_OTHER": {"ARRNAME": "VLTI"}})
+    o2 = fits.read_fits(dst2)
+    assert o2[1][0]["ARRNAME"] == "VLTI" and o2[1][0]["TZERO2"] == 32768
+    assert "CHECKSUM" not in o2[1][0]
+    assert list(o2[1][1]["U"]) == [0, 40000, 65535]
+    assert o2[1][1]["VARCOL"].tobytes() == hdus[1][1]["VARCOL"].tobytes()
+    raw2 = open(dst2, "rb").read()
+    assert raw2[-len(mb):] == raw_src[-len(mb):]  # METROLOGY untouched this time: byte for byte
+
+
+def test_unsigned_columns_round_trip(fits, tmp_path):
+    """UInt16/32/64 columns are written with the standard TZERO offsets and read back exactly."""
+    tab = {"A": np.array([0, 1, 65535], np.uint16), "B": np.array([0, 2**31, 2**32 - 1], np.uint32),
+           "C": np.array([0, 2**63, 2**64 - 1], np.uint64)}
+    p = str(tmp_path / "u.fits")
+    fits.write_metrology(p, tab, {})
+    (_, _), (h, d) = fits.read_fits(p)
+    assert (h["TZERO1"], h["TZERO2"], h["TZERO3"]) == (32768, 2**31, 2**63)
+    for k in tab:
+        assert d[k].dtype == tab[k].dtype and np.array_equal(d[k], tab[k]), k

@@ -419,3 +419,27 @@ def test_exact_model_regime_boundaries(gpu, oracle, xinit, b_range):
     xi = None if xinit is None else np.array(xinit)
     ref = oracle_fit(oracle, B, xinit=xi)
     print(assert_exact_bitwise(fit(gpu, B, method="exact", xinit=xi), ref, label="regimes/exact"))
+
+
+def test_split_barrier_give_up_poisons_the_whole_series(gpu, oracle, monkeypatch):
+    """The multi-workgroup exact fit's per-series barrier (G = 8 parts) gives up after ~1 s when a
+    part is not resident (never observed).  GPD_XSPIN_TEST=1 makes it give up at once: a part
+    that finds its siblings missing poisons the series' arrival counter, every part reads the
+    poison at that same barrier, all stop together, and the record is flagged GPD_ST_SYNC with
+    NaN χ² — never a silently different value.  Series whose barriers all completed before any
+    give-up keep the normal records bit for bit."""
+    B = _exposure(20_000, seed=5)
+    monkeypatch.setenv("GPD_EXACT_G", "8")
+    good = fit(gpu, B, method="exact")
+    assert not np.any(good["status"] & gpu.GPD_ST_SYNC)
+    monkeypatch.setenv("GPD_XSPIN_TEST", "1")
+    got = fit(gpu, B, method="exact")
+    monkeypatch.delenv("GPD_XSPIN_TEST")
+    sync = (got["status"] & gpu.GPD_ST_SYNC) != 0
+    assert sync.any(), "the give-up path did not run"
+    assert np.all(np.isnan(got["chi2"][sync])) and np.all(got["status"][sync] & gpu.GPD_ST_NAN)
+    same = got[~sync].tobytes() == good[~sync].tobytes()
+    assert same, "a series without a give-up differs from the normal run"
+    print(f"{sync.sum()}/{len(got)} series poisoned, the rest bit-identical")
+    again = fit(gpu, B, method="exact")  # the library is unaffected afterwards
+    assert again.tobytes() == good.tobytes()

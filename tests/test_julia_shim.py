@@ -141,3 +141,30 @@ def test_integration_md_snippets_match_the_shim(sym):
             assert types == shim[sym], sym
             found = True
     assert found or sym not in md
+
+
+def _function_body(src, name):
+    m = re.search(rf"^function {name}\(.*?^end$", src, flags=re.S | re.M)
+    assert m, name
+    return m.group(0)
+
+
+def test_return_types_follow_the_reference():
+    """demodulateall returns (output::Matrix{Complex{T}} = copy(data), param::Vector{Modulation…{T}},
+    likelihood::Vector{T}) for data::AbstractMatrix{Complex{T}} (src/Modulation.jl:344, 353-359,
+    434): the shim must keep T in all three, not hand back the library's Float64 values."""
+    src = re.sub(r"#.*", "", open(JL).read())
+    body = _function_body(src, "demodulateall_gpu")
+    sig = body.split(")", 1)[0]
+    assert "data::AbstractMatrix{Complex{T}}" in sig
+    assert re.search(r"where\s*\{T<:AbstractFloat\}", body)
+    assert "output = copy(data)" in body
+    assert re.search(r"output\[:, 1:32\] \.= Complex\{T\}\.\(demod\)", body)
+    assert "ModulationWithOffsets{T}[" in body and "ModulationNoOffsets{T}[" in body
+    assert re.search(r"likelihood = T\[p\.chi2 for p in params\]", body)
+    assert re.search(r"return \(output, param, likelihood\)", body)
+    # the χ² functor returns T as lkl does (src/Modulation.jl:318-326)
+    body = _function_body(src, "chi2_gpu")
+    assert "data::AbstractMatrix{Complex{T}}" in body
+    assert re.search(r"return T\[p\.chi2 for p in params\]", body)
+    assert "Vector{Float64}(undef" not in body
