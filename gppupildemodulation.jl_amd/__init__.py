@@ -12,7 +12,7 @@ The package directory name contains a dot, so load it by path, e.g.::
 
 (`gpdemod_loader.load()` at the repo root does exactly this.)
 """
-from ._lib import (GPD_FIT_OFFSETS, GPD_METHOD_EXACT, GPD_METHOD_HARMONIC, GPD_ONLY_HIGH,
+from ._lib import (GPD_FIT_OFFSETS, GPD_FP32, GPD_METHOD_EXACT, GPD_METHOD_HARMONIC, GPD_ONLY_HIGH,
                    GPD_RECENTER, GPD_ST_EXACT, GPD_ST_FALLBACK, GPD_ST_MAXFUN, GPD_ST_NAN,
                    GPD_ST_REFIT, GPD_ST_SYNC, PARAM_DTYPE, GpdError, libm_eval, load, timings)
 from .demod import (DAY_TO_SEC, M_2PI, MJD_1970_1_1, Diode, FaintStates, MetState,
@@ -25,7 +25,7 @@ from . import fits  # processmetrology's FITS output (host I/O)
 
 __all__ = [
     "fits", "process_exposure",
-    "GPD_FIT_OFFSETS", "GPD_METHOD_EXACT", "GPD_METHOD_HARMONIC", "GPD_ONLY_HIGH", "GPD_RECENTER",
+    "GPD_FIT_OFFSETS", "GPD_FP32", "GPD_METHOD_EXACT", "GPD_METHOD_HARMONIC", "GPD_ONLY_HIGH", "GPD_RECENTER",
     "GPD_ST_EXACT", "GPD_ST_FALLBACK", "GPD_ST_MAXFUN", "GPD_ST_NAN", "GPD_ST_REFIT",
     "GPD_ST_SYNC",
     "PARAM_DTYPE", "GpdError", "libm_eval", "load", "timings", "M_2PI", "Diode", "FaintStates", "MetState",

@@ -22,6 +22,7 @@ GPD_RECENTER = 0x2
 GPD_ONLY_HIGH = 0x4
 GPD_METHOD_EXACT = 0x10
 GPD_METHOD_HARMONIC = 0x20
+GPD_FP32 = 0x40  # Float32 per-sample arithmetic (exact evaluator), include/gpdemod.h
 
 GPD_ST_REFIT = 0x1
 GPD_ST_MAXFUN = 0x2

@@ -11,10 +11,15 @@ OUT = os.path.join(HERE, "libgpdemod.so")
 # (GPD_MOMENTS=ws_nomfma|ws_noload|ws_nof0|ws_noq|ws_mfmaonly|ws_prof; results invalid),
 # loaded instead of libgpdemod.so when GPD_LIB=diag (tools/pmc_variants.sh)
 OUT_DIAG = os.path.join(HERE, "libgpdemod_diag.so")
-SOURCES = ["gpd_engine.hip"]
+# translation units compiled in parallel and linked into one library (gpd_kernels.hpp GPD_OWNS:
+# unit 0 = host code + light kernels, the others = the heavy kernel instances)
+# the slowest units first (the exact path's instances), so the pool's tail is short
+SOURCES = ["gpd_part3.hip", "gpd_part4.hip", "gpd_part7.hip", "gpd_part8.hip", "gpd_part5.hip",
+           "gpd_part9.hip", "gpd_part10.hip", "gpd_part11.hip", "gpd_part2.hip", "gpd_part6.hip",
+           "gpd_part1.hip", "gpd_engine.hip"]
 HEADERS = ["gpd_kernels.hpp", "gpd_device.hpp", "gpd_newuoa.hpp", "gpd_states.hpp", "gpd_jlmath.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          # the exact evaluator and NEWUOA must not fuse a*b+c (Julia does not contract);
          # the moment kernel asks for FMAs explicitly with fma().
          "-ffp-contract=off", "-Wall", "-Wno-unused-function"]
@@ -26,20 +31,50 @@ def _stale(out: str) -> bool:
     t = os.path.getmtime(out)
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
     deps.append(os.path.join(HERE, "..", "include", "gpdemod.h"))
+    deps.append(os.path.abspath(__file__))
     return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
 
 
-def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str:
-    out = OUT_DIAG if diag else OUT
+def build(force: bool = False, verbose: bool = False, diag: bool = False, jobs: int = 0,
+          variant: str | None = None, defines: tuple = (), only: tuple = ()) -> str:
+    """variant: an A/B build libgpdemod_<variant>.so with extra -D `defines` (loaded with
+    GPD_LIB=<variant>, tools/ab_*.sh); `only`: compile just these units for the variant and
+    link the other units' objects of the release build; diag: the diagnostics build."""
+    out = (os.path.join(HERE, f"libgpdemod_{variant}.so") if variant
+           else OUT_DIAG if diag else OUT)
     if not force and not _stale(out):
         return out
-    cmd = [HIPCC, *FLAGS, *(["-DGPD_DIAG"] if diag else []), "-o", out + ".tmp",
-           *[os.path.join(CSRC, s) for s in SOURCES]]
+    objdir = os.path.join(HERE, "build", variant or ("diag" if diag else "release"))
+    os.makedirs(objdir, exist_ok=True)
+    extra = (["-DGPD_DIAG"] if diag else []) + [f"-D{d}" for d in defines]
+    jobs = jobs or max(1, min(len(SOURCES), os.cpu_count() or 1))
+    procs, objs, errs = [], [], []
+    pending = [u for u in SOURCES if not only or u in only]
+    if only:  # the other units from the release build
+        rel = os.path.join(HERE, "build", "release")
+        objs += [os.path.join(rel, u.replace(".hip", ".o")) for u in SOURCES if u not in only]
+    while pending or procs:
+        while pending and len(procs) < jobs:
+            src = pending.pop(0)
+            obj = os.path.join(objdir, src.replace(".hip", ".o"))
+            objs.append(obj)
+            cmd = [HIPCC, *FLAGS, *extra, "-c", "-o", obj + ".tmp", os.path.join(CSRC, src)]
+            procs.append((src, obj, subprocess.Popen(cmd, stdout=subprocess.PIPE,
+                                                     stderr=subprocess.PIPE, text=True)))
+        src, obj, p = procs.pop(0)
+        _, err = p.communicate()
+        if p.returncode != 0:
+            errs.append(f"{src}: hipcc failed ({p.returncode}):\n{err[-4000:]}")
+        else:
+            if verbose and err:
+                print(err)
+            os.replace(obj + ".tmp", obj)
+    if errs:
+        raise RuntimeError("\n".join(errs))
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out + ".tmp", *objs]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stderr[-4000:]}")
-    if verbose and r.stderr:
-        print(r.stderr)
+        raise RuntimeError(f"link failed ({r.returncode}):\n{r.stderr[-4000:]}")
     os.replace(out + ".tmp", out)
     return out
 
@@ -47,4 +82,10 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str
 if __name__ == "__main__":
     import sys
 
-    print(build(force=True, verbose=True, diag="--diag" in sys.argv))
+    # build.py [--diag] [--variant NAME -DDEF ...]
+    argv = sys.argv[1:]
+    var = argv[argv.index("--variant") + 1] if "--variant" in argv else None
+    defs = tuple(a[2:] for a in argv if a.startswith("-D"))
+    only = tuple(argv[argv.index("--only") + 1].split(",")) if "--only" in argv else ()
+    print(build(force=True, verbose=True, diag="--diag" in argv, variant=var, defines=defs,
+                only=only))

@@ -17,6 +17,7 @@
 #include <thread>
 #include <vector>
 
+#define GPD_PART 0  // split build: unit 0 (gpd_kernels.hpp GPD_OWNS)
 #include "../../include/gpdemod.h"
 #include "gpd_kernels.hpp"
 #include "gpd_states.hpp"
@@ -88,8 +89,8 @@ DevCtx *ctx_for(int dev) {
 size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
 struct Layout {
-    size_t info, tab, part, mom, aux, fstat, raw, list, phbuf, partG, momG, auxG, fcid, d0, mcache,
-        xtot, xcnt, fsx, fsc, total;
+    size_t info, prof, tab, part, mom, aux, fstat, raw, list, phbuf, partG, momG, auxG, fcid, d0,
+        mcache, xtot, xcnt, fsx, fsc, xr32, total;
     long long mstride;  // model-cache elements per exact-path workgroup (0: no cache)
     int nch;            // sample chunks of the moment grid (grid.y)
     long long chunk;    // samples per chunk (a whole number of units)
@@ -101,7 +102,8 @@ struct Layout {
 };
 
 Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic, bool phbuf,
-            bool mfma, int n_cu, bool harm_offs, bool windowed = false, int exact_g = 1) {
+            bool mfma, int n_cu, bool harm_offs, bool windowed = false, int exact_g = 1,
+            bool fp32 = false) {
     Layout L{};
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -148,6 +150,7 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     L.nch = (int)((U + (L.chunk / ulen) - 1) / (L.chunk / ulen));
     const long long nch = U;  // partial-moment sets
     L.info = take(sizeof(Info));
+    L.prof = take(PROF_LEN * sizeof(unsigned long long));  // diagnostic counters
     // cos/sin table, padded to whole MM_TS-sample tiles (k_table_mix fills the padding)
     L.tab = take(harmonic ? (size_t)((N + MM_TS - 1) / MM_TS * MM_TS) * 2 * KH * sizeof(double) : 0);
     // windowed series: k_moments_win writes mom directly (no partial moments)
@@ -186,6 +189,7 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     L.fs_pc = std::min<long long>(L.fs_pc, (1LL << 31) / FS_G - 1);
     L.fsx = take(L.fs1 ? (size_t)L.fs_pc * FS_G * L.fs_mmax * 256 * sizeof(double) : 0);
     L.fsc = take(L.fs1 ? (size_t)L.fs_pc * FS_G * (FS_NV + 8) * sizeof(double) : 0);
+    L.xr32 = take(fp32 ? (size_t)N * sizeof(float) : 0);  // F_FP32 phase table
     L.total = off;
     return L;
 }
@@ -274,6 +278,12 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         set_err(errbuf, errlen, "gpd_fit_batch_dev: both METHOD bits set");
         return GPD_E_ARG;
     }
+    const bool fp32 = (flags & GPD_FP32) != 0;
+    if (fp32 && (flags & (GPD_FIT_OFFSETS | GPD_METHOD_HARMONIC))) {
+        set_err(errbuf, errlen, "gpd_fit_batch_dev: GPD_FP32 is the exact evaluator without "
+                                "fitoffsets (not with FIT_OFFSETS or METHOD_HARMONIC)");
+        return GPD_E_ARG;
+    }
     int ndev = gpd_device_count();
     if (ndev <= 0) {
         set_err(errbuf, errlen, "gpd_fit_batch_dev: no HIP device visible");
@@ -311,8 +321,10 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     // iterate; METHOD_HARMONIC asks for the fast path anyway (parity ~1e-9).
     // Windows of ≥ HARM_MIN_SPAN samples: harmonic moments from k_moments_win (a shorter last
     // window is re-fitted exactly); shorter windows: the exact evaluator.
+    long long harm_min = HARM_MIN_SPAN;
+    if (const char *e = getenv("GPD_HARM_MIN_SPAN")) harm_min = std::max(1LL, atoll(e));  // sweep only
     const bool want_exact =
-        (flags & GPD_METHOD_EXACT) || (window > 0 && window < HARM_MIN_SPAN) ||
+        fp32 || (flags & GPD_METHOD_EXACT) || (window > 0 && window < harm_min) ||
         (offs && !(harm_offs_ok && window == 0 && (flags & GPD_METHOD_HARMONIC)));
     if ((flags & GPD_METHOD_HARMONIC) && want_exact) {
         set_err(errbuf, errlen, "gpd_fit_batch_dev: harmonic method unavailable here "
@@ -324,7 +336,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     const long long N = n_samples, ncol = n_pixels;
     const long long nwin = window > 0 ? (N + window - 1) / window : 1;
     const long long P = ncol * nwin;  // series
-    const bool phbuf = want_exact && (size_t)n_fc * N * sizeof(c64) <= (size_t(4) << 30);
+    // (F_FP32 forms its Float32 phasor z/|z| from the raw FC columns: no phasor buffer)
+    const bool phbuf = want_exact && !fp32 && (size_t)n_fc * N * sizeof(c64) <= (size_t(4) << 30);
 
     DevCtx *cx = ctx_for(device);
     std::lock_guard<std::mutex> lk(cx->mu);
@@ -344,7 +357,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         }
     }
     const Layout L = plan(N, P, n_fc, faint, harmonic, phbuf, use_mfma, cx->n_cu, harm_offs,
-                          window > 0, exact_g);
+                          window > 0, exact_g, fp32);
     if (cx->ws_cap < L.total) {
         if (cx->ws) {
             HIP_TRY(hipDeviceSynchronize());
@@ -400,6 +413,10 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     pb.x1 = xinit ? xinit[1] : 0.0;
     pb.win = window;
     pb.ncol = ncol;
+    pb.harm_min = harm_min;
+    pb.prof = (unsigned long long *)(ws + L.prof);
+    pb.fit_lanes = 0;
+    pb.xr32 = fp32 ? (const float *)(ws + L.xr32) : nullptr;
     Param *outp = (Param *)out_params;
 
     int nt = 0;
@@ -417,6 +434,13 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         }
     };
     HIP_TRY(hipEventRecord(cx->ev[0], stream));
+    // diagnostic counters (GPD_FIT_PROF, GPD_MOMENTS=ws_prof): zeroed, read back after the kernel
+    unsigned long long prof_h[PROF_LEN] = {};
+    auto prof_reset = [&]() { return hipMemsetAsync(pb.prof, 0, sizeof prof_h, stream); };
+    auto prof_read = [&]() {
+        hipError_t e = hipMemcpyAsync(prof_h, pb.prof, sizeof prof_h, hipMemcpyDeviceToHost, stream);
+        return e == hipSuccess ? hipStreamSynchronize(stream) : e;
+    };
 
     k_prepare<<<1, 1024, 0, stream>>>(pb, info);
     HIP_TRY(hipMemsetAsync(count, 0, sizeof(int), stream));
@@ -484,13 +508,10 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             else if (mk && std::string(mk) == "ws_mfmaonly")
                 k_moments_ws<5><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
             else if (mk && std::string(mk) == "ws_prof") {  // cycle split per role (stderr)
-                unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_wsprof), z, sizeof z, 0,
-                                               hipMemcpyHostToDevice, stream));
+                HIP_TRY(prof_reset());
                 k_moments_ws<6><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
-                HIP_TRY(hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_wsprof), sizeof z, 0,
-                                                 hipMemcpyDeviceToHost, stream));
-                HIP_TRY(hipStreamSynchronize(stream));
+                HIP_TRY(prof_read());
+                const unsigned long long *z = prof_h + PROF_WS;
                 const double pw = 4.0 * g.x * g.y, cw = pw;  // waves per role
                 fprintf(stderr,
                         "ws_prof cycles/wave: producer stage %.3g issue %.3g barrier %.3g | "
@@ -555,19 +576,28 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         }
         static const bool fit_prof = getenv("GPD_FIT_PROF") != nullptr;  // diagnostics only
         if (fit_prof) {
-            unsigned long long z[4] = {0, 0, 0, 0};
-            HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_fitprof), z, sizeof z, 0,
-                                           hipMemcpyHostToDevice, stream));
+            HIP_TRY(prof_reset());
             Problem pp = pb;
             pp.flags |= F_PROF;
-            k_fit_harmonic<<<(unsigned)((P + 63) / 64), 64, 0, stream>>>(pp, info, mom, aux, momG,
+            unsigned fit_wg = (unsigned)((P + 63) / 64);
+#ifdef GPD_DIAG
+            pp.fit_lanes = getenv("GPD_FIT_LANES") ? std::max(1, std::min(64, atoi(getenv("GPD_FIT_LANES")))) : 64;
+            fit_wg = (unsigned)((P + pp.fit_lanes - 1) / pp.fit_lanes);
+#endif
+            k_fit_harmonic<<<fit_wg, 64, 0, stream>>>(pp, info, mom, aux, momG,
                                                                        n_fc, d0, outp, raw, list,
                                                                        count);
-            HIP_TRY(hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_fitprof), sizeof z, 0,
-                                             hipMemcpyDeviceToHost, stream));
-            HIP_TRY(hipStreamSynchronize(stream));
+            HIP_TRY(prof_read());
+            const unsigned long long *z = prof_h + PROF_FIT;
             fprintf(stderr, "fit_prof per series: objective %.3g cycles, whole fit %.3g, evals %.3g\n",
                     (double)z[0] / P, (double)z[1] / P, (double)z[2] / P);
+#ifdef GPD_DIAG
+            const unsigned long long *zn = prof_h + PROF_NW;
+            fprintf(stderr, "fit_prof newuoa per series: trsapp %.3g biglag %.3g bigden %.3g "
+                    "update %.3g init %.3g vlag/beta %.3g model-update %.3g cycles (lanes %d)\n",
+                    (double)zn[0] / P, (double)zn[1] / P, (double)zn[2] / P, (double)zn[3] / P,
+                    (double)zn[4] / P, (double)zn[5] / P, (double)zn[6] / P, pp.fit_lanes);
+#endif
         } else {
             k_fit_harmonic<<<(unsigned)((P + 63) / 64), 64, 0, stream>>>(pb, info, mom, aux, momG,
                                                                        n_fc, d0, outp, raw, list,
@@ -590,6 +620,10 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             mark("refine_exact");
         }
     } else {
+        if (fp32) {
+            k_phase32<<<(unsigned)((N + 255) / 256), 256, 0, stream>>>(t, N, omega, (float *)pb.xr32);
+            mark("phase32");
+        }
         if (phbuf) {
             dim3 g((unsigned)std::min<long long>((N + 255) / 256, 256), (unsigned)n_fc);
             k_phasor<<<g, 256, 0, stream>>>(pb, ph);
@@ -602,11 +636,9 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         }
         // GPD_FIT_PROF (diagnostics): per-phase cycles of the multi-workgroup exact fit
         static const bool xprof = getenv("GPD_FIT_PROF") != nullptr;
-        unsigned long long zx[4] = {0, 0, 0, 0};
         if (xprof && exact_g > 1 && !bphi) {
             pb.flags |= F_PROF;
-            HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_fitprof), zx, sizeof zx, 0,
-                                           hipMemcpyHostToDevice, stream));
+            HIP_TRY(prof_reset());
         }
         const unsigned fit_grid =
             exact_g > 1 ? (unsigned)((P + 7) / 8 * 8 * exact_g) : exact_grid;
@@ -632,9 +664,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         mark(bphi ? "chi2_exact" : "fit_exact");
         if (pb.flags & F_PROF) {
             pb.flags &= ~F_PROF;
-            HIP_TRY(hipMemcpyFromSymbolAsync(zx, HIP_SYMBOL(g_fitprof), sizeof zx, 0,
-                                             hipMemcpyDeviceToHost, stream));
-            HIP_TRY(hipStreamSynchronize(stream));
+            HIP_TRY(prof_read());
+            const unsigned long long *zx = prof_h + PROF_FIT;
             const double nwg = (double)P * exact_g;
             fprintf(stderr, "exact fit_prof cycles per workgroup: pass1 %.4g residual %.4g "
                     "exchange %.4g whole %.4g\n", zx[0] / nwg, zx[1] / nwg, zx[2] / nwg,

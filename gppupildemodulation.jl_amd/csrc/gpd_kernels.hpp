@@ -16,6 +16,23 @@
 #include "gpd_device.hpp"
 #include "gpd_newuoa.hpp"
 
+// Split build: build.py compiles the kernels in several translation units (gpd_engine.hip =
+// unit 0 with the host code and the light kernels, gpd_part*.hip) in parallel.  GPD_PART is
+// the unit being compiled; a kernel body is compiled only in the units of its GPD_OWNS mask,
+// the other units see its declaration and launch it through the host stub the owning unit
+// defines (each unit instantiates the template kernels it owns, gpd_part*.hip).  Without
+// GPD_PART every kernel is defined (single-unit build).
+#ifdef GPD_PART
+#define GPD_OWNS(mask) ((((mask) >> GPD_PART) & 1) != 0)
+#else
+#define GPD_OWNS(mask) 1
+#endif
+#define GPD_U_ENGINE 0x1  // unit 0: gpd_engine.hip
+#define GPD_U_FITH 0x2    // unit 1: k_fit_harmonic, k_chi2_harmonic
+#define GPD_U_MOM 0x44    // units 2, 6: k_moments_ws (Float64 / Float32 storage)
+#define GPD_U_EXACT 0x198  // units 3, 4, 7, 8: k_fit_exact (faint × offsets instances)
+#define GPD_U_CHI2X 0xE20  // units 5, 9, 10, 11: k_chi2_exact, k_refine_exact
+
 namespace gpd {
 
 constexpr int KH = 24;               // harmonics kept (|b| ≤ ~4.3 at 1e-16 tail)
@@ -28,19 +45,22 @@ constexpr int EXACT_WG = 256;        // threads per series in the exact evaluato
 constexpr double PI_F64 = 3.141592653589793;
 
 // ϕrange = range(-π, π, 8) (src/Modulation.jl:360), bit-exact Float64 values.
-__device__ __constant__ const double c_phi_grid[8] = {
+static __device__ __constant__ const double c_phi_grid[8] = {
     -0x1.921fb54442d18p+1, -0x1.1f3b3855544c8p+1, -0x1.58ad76cccb8f0p+0, -0x1.cb91f3bbba140p-2,
     0x1.cb91f3bbba140p-2,  0x1.58ad76cccb8f0p+0,  0x1.1f3b3855544c8p+1,  0x1.921fb54442d18p+1};
 
 // status bits (mirror include/gpdemod.h)
 constexpr int ST_REFIT = 0x1, ST_MAXFUN = 0x2, ST_NAN = 0x4, ST_EXACT = 0x8, ST_FALLBACK = 0x10,
               ST_SYNC = 0x20;
-constexpr uint32_t F_OFFSETS = 0x1u, F_RECENTER = 0x2u, F_ONLY_HIGH = 0x4u;
+constexpr uint32_t F_OFFSETS = 0x1u, F_RECENTER = 0x2u, F_ONLY_HIGH = 0x4u, F_FP32 = 0x40u;
 constexpr uint32_t F_PROF = 0x80000000u;  // internal: k_fit_harmonic cycle split (GPD_FIT_PROF)
 // internal (tests, GPD_XSPIN_TEST=1): the multi-workgroup exact fit's barrier gives up at once
 // instead of after ~1 s, so the give-up path (poisoned series, GPD_ST_SYNC) runs on demand
 constexpr uint32_t F_XSPIN_TEST = 0x40000000u;
-__device__ unsigned long long g_fitprof[4];  // [0] objective cycles, [1] whole-fit cycles, [2] evals
+// Diagnostic cycle counters (GPD_FIT_PROF, GPD_MOMENTS=ws_prof) live in the workspace, reached
+// through Problem::prof: [0..3] fit split (objective, whole fit, evals, exact exchange),
+// [8..15] moment-kernel roles, [16..23] NEWUOA phases (diagnostics build)
+constexpr int PROF_FIT = 0, PROF_WS = 8, PROF_NW = 16, PROF_LEN = 32;
 
 struct Param {  // == gpd_param
     double c_re, c_im, a_re, a_im, b, phi, chi2;
@@ -83,6 +103,12 @@ struct Problem {
     // consecutive windows of win samples (the last one shorter); series k is column k % ncol
     // of window k / ncol.  win = 0: series k is column k over all N samples.
     long long win, ncol;
+    // windows shorter than this many samples are fitted by the exact evaluator (HARM_MIN_SPAN;
+    // GPD_HARM_MIN_SPAN overrides it for the window-length sweep, tools/window_sweep.py)
+    long long harm_min;
+    unsigned long long *prof;  // PROF_LEN diagnostic counters (workspace), or nullptr
+    int fit_lanes;             // diagnostics build: series per k_fit_harmonic wave (0 = 64)
+    const float *xr32;         // F_FP32: rem(fl(ω t_i), 2π) per sample (k_phase32), or nullptr
 };
 
 // Column and sample range [s0, s1) of series k.
@@ -217,7 +243,9 @@ __device__ __forceinline__ void store_param(Param *out, double *raw, long long k
 
 // ---------------------------------------------------------------------------------------
 // k_prepare: one workgroup.  Counts valid samples and classifies fl(ωt) for the harmonic path.
-__global__ __launch_bounds__(1024) void k_prepare(Problem pb, Info *info) {
+__global__ __launch_bounds__(1024) void k_prepare(Problem pb, Info *info)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     __shared__ double red[16 * 3];
     double cnt = 0.0, xmn = 1.0e308, xmx = 0.0;
     for (long long i = threadIdx.x; i < pb.N; i += 1024) {
@@ -274,12 +302,18 @@ __global__ __launch_bounds__(1024) void k_prepare(Problem pb, Info *info) {
         *info = in;
     }
 }
+#else
+;
+#endif
+
 
 // ---------------------------------------------------------------------------------------
 // k_table: c_n(i) = cos(n x_i), s_n(i) = sin(n x_i), n = 1..K, x_i = fl(ω t_i), by the
 // angle-addition recurrence from sincos(x_i) (exact range reduction of x_i; error ~n·eps).
 __global__ __launch_bounds__(256) void k_table(const double *__restrict__ t, long long N,
-                                               double omega, double *__restrict__ tab) {
+                                               double omega, double *__restrict__ tab)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
     if (i >= N) return;
     const double x = omega * t[i];
@@ -297,6 +331,10 @@ __global__ __launch_bounds__(256) void k_table(const double *__restrict__ t, lon
         sn = sn1;
     }
 }
+#else
+;
+#endif
+
 
 // k_table_mix: the table of the mixed-precision moment kernel (k_moments_ws<…, MIX = true>).
 // Same 48-double rows per sample, tiles of MM_TS = 32 samples:
@@ -313,7 +351,9 @@ __device__ __forceinline__ unsigned short bf16_rne(float f) {
     return (unsigned short)(u >> 16);
 }
 __global__ __launch_bounds__(256) void k_table_mix(const double *__restrict__ t, long long N,
-                                                   double omega, double *__restrict__ tab) {
+                                                   double omega, double *__restrict__ tab)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
     const long long npad = (N + 31) / 32 * 32;
     if (i >= npad) return;
@@ -353,13 +393,19 @@ __global__ __launch_bounds__(256) void k_table_mix(const double *__restrict__ t,
         ((unsigned short *)(frag + 16))[j] = lb;
     }
 }
+#else
+;
+#endif
+
 
 // ---------------------------------------------------------------------------------------
 // k_faint_stats: per series and MetState, m = mean(|d|), w = 1/var(|d|; mean=m) (two passes,
 // src/Faint.jl:89-100) over the valid samples, plus Σ|d|² per state.  One workgroup per series;
 // sums in the canonical order CR8 (8 block sweeps of 256 strided slots, the oracle's gsum), so m
 // and w are the oracle's bits.  out[k*16 + ...]: m[5] | w[5] | W2 | DEN | Q2 (state = code + 1).
-__global__ __launch_bounds__(256) void k_faint_stats(Problem pb, double *__restrict__ out) {
+__global__ __launch_bounds__(256) void k_faint_stats(Problem pb, double *__restrict__ out)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     __shared__ double lds[4 * 15];
     const long long k = blockIdx.x;
     const Span sp = span_of(pb, k);  // per window: compute_mean_var_power on state[I] (:205)
@@ -449,6 +495,10 @@ __global__ __launch_bounds__(256) void k_faint_stats(Problem pb, double *__restr
         o[12] = Q2;
     }
 }
+#else
+;
+#endif
+
 
 // ---------------------------------------------------------------------------------------
 // Faint statistics in one pass over the series and one hypot per sample (k_faint_stats re-reads
@@ -512,7 +562,9 @@ __device__ __forceinline__ void fs_accum3(int q, double a, double b, int (&cnt)[
 template <class TS>
 __global__ __launch_bounds__(256) void k_faint_p1(Problem pb, long long k0, int Mmax,
                                                   double *__restrict__ scr,
-                                                  double *__restrict__ xt) {
+                                                  double *__restrict__ xt)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     __shared__ double lds[4 * 16];
     typedef double nv2d __attribute__((ext_vector_type(2)));
     typedef float nv2f __attribute__((ext_vector_type(2)));
@@ -588,6 +640,10 @@ __global__ __launch_bounds__(256) void k_faint_p1(Problem pb, long long k0, int 
         xt[(long long)blockIdx.x * FS_NV + t] = x;
     }
 }
+#else
+;
+#endif
+
 
 // the 8 block totals of series j (cohort-local) added in block order
 __device__ __forceinline__ void fs_totals(const double *__restrict__ xt, long long j, double (&tv)[15]) {
@@ -603,7 +659,9 @@ __device__ __forceinline__ void fs_totals(const double *__restrict__ xt, long lo
 __global__ __launch_bounds__(256) void k_faint_p2(Problem pb, int Mmax,
                                                   const double *__restrict__ scr,
                                                   const double *__restrict__ xt,
-                                                  double *__restrict__ x2) {
+                                                  double *__restrict__ x2)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     __shared__ double lds[4 * 8];
     __shared__ double mus[5];
     typedef const __attribute__((address_space(1))) double gd;
@@ -671,10 +729,16 @@ __global__ __launch_bounds__(256) void k_faint_p2(Problem pb, int Mmax,
         x2[(long long)blockIdx.x * 8 + t] = x;
     }
 }
+#else
+;
+#endif
+
 
 __global__ __launch_bounds__(64) void k_faint_fin(long long k0, const double *__restrict__ xt,
                                                   const double *__restrict__ x2,
-                                                  double *__restrict__ out) {
+                                                  double *__restrict__ out)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     // one wave per series: the lanes fetch the 8 × (15 + 5) block totals, lane 0 adds them in
     // block order and writes the record
     __shared__ double v[FS_G * 20];
@@ -707,14 +771,43 @@ __global__ __launch_bounds__(64) void k_faint_fin(long long k0, const double *__
     o[11] = DEN;
     o[12] = Q2;
 }
+#else
+;
+#endif
+
 
 // ---------------------------------------------------------------------------------------
 // k_phasor: FC phasor buffer for the exact evaluator (only when it fits the workspace).
-__global__ __launch_bounds__(256) void k_phasor(Problem pb, c64 *__restrict__ ph) {
+// F_FP32 phase table: x_i = fl(ω t_i) (the reference's product, src/Modulation.jl:137) reduced
+// modulo 2π in Float64 (Cody–Waite with fma: 2π = P1 + P2), rounded to Float32 — the Float32
+// evaluator's θ = x_i + ϕ then stays within a few radians, where Float32 sin keeps ~1e-7.
+__global__ __launch_bounds__(256) void k_phase32(const double *__restrict__ t, long long N,
+                                                 double omega, float *__restrict__ xr)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= N) return;
+    const double x = omega * t[i];
+    const double k = rint(x * 0.15915494309189535);  // 1/(2π)
+    double r = fma(-k, 6.283185307179586, x);
+    r = fma(-k, 2.4492935982947064e-16, r);
+    xr[i] = (float)r;
+}
+#else
+;
+#endif
+
+__global__ __launch_bounds__(256) void k_phasor(Problem pb, c64 *__restrict__ ph)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     const long long g = blockIdx.y, N = pb.N;
     for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < N; i += (long long)gridDim.x * 256)
         ph[g * N + i] = fc_phasor(fc_at(pb, g * pb.ldfc + i));
 }
+#else
+;
+#endif
+
 
 // ---------------------------------------------------------------------------------------
 // HARMONIC PATH — k_moments: the HBM-streaming pass (roofline kernel).
@@ -725,7 +818,9 @@ __global__ __launch_bounds__(256) void k_phasor(Problem pb, c64 *__restrict__ ph
 template <bool FAINT>
 __global__ __launch_bounds__(64) void k_moments(Problem pb, const double *__restrict__ tab,
                                                 const double *__restrict__ fstat,
-                                                long long chunk_len, double *__restrict__ part) {
+                                                long long chunk_len, double *__restrict__ part)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     __shared__ c64 dtile[MOM_TS][65];
     __shared__ c64 ptile[MOM_TS][65];
     const int lane = threadIdx.x;
@@ -808,6 +903,10 @@ __global__ __launch_bounds__(64) void k_moments(Problem pb, const double *__rest
         for (int q = 0; q < NMOM; ++q) o[(long long)q * pb.P] = acc[q];
     }
 }
+#else
+;
+#endif
+
 
 // ---------------------------------------------------------------------------------------
 // MFMA moment pass (k_moments_ws below): the moments as a dense fp64 contraction on the matrix
@@ -872,7 +971,6 @@ __device__ __forceinline__ TS buf_ld(__amdgpu_buffer_rsrc_t rs, int voff) {
 // DBG == 6 (diagnostics only): per-role cycle split, summed over waves
 //   [0] producer stage, [1] producer issue, [2] producer barrier, [3] consumer MFMA phase,
 //   [4] consumer barrier
-__device__ unsigned long long g_wsprof[8];
 
 template <bool B>
 struct BoolTag {
@@ -928,7 +1026,9 @@ template <int DBG = 0, bool UNIT = false, class TS = c64, int POL = 0, bool MIX 
 __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double *__restrict__ tab,
                                                        long long chunk_len, long long unit_len,
                                                        double *__restrict__ part,
-                                                       const double *__restrict__ fstat = nullptr) {
+                                                       const double *__restrict__ fstat = nullptr)
+#if GPD_OWNS(GPD_U_MOM)
+{
     __shared__ c64 qs[2][MM_TS * MM_ROW];
     __shared__ __attribute__((aligned(16))) double ts[2][MM_TS * 2 * KH];
     __shared__ int fcl[MM_PIX];
@@ -1135,9 +1235,9 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             run(BoolTag<false>{});
         if constexpr (DBG == 6) {
             if (lane == 0) {
-                atomicAdd(&g_wsprof[0], pst);
-                atomicAdd(&g_wsprof[1], pis);
-                atomicAdd(&g_wsprof[2], pbar);
+                atomicAdd(&pb.prof[PROF_WS + 0], pst);
+                atomicAdd(&pb.prof[PROF_WS + 1], pis);
+                atomicAdd(&pb.prof[PROF_WS + 2], pbar);
             }
         }
         // the last iterations re-read the final tile; let those loads land before the wave
@@ -1288,11 +1388,15 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
     }
     if constexpr (DBG == 6) {
         if (lane == 0) {
-            atomicAdd(&g_wsprof[3], cmf);
-            atomicAdd(&g_wsprof[4], cbar);
+            atomicAdd(&pb.prof[PROF_WS + 3], cmf);
+            atomicAdd(&pb.prof[PROF_WS + 4], cbar);
         }
     }
 }
+#else
+;
+#endif
+
 
 // k_reduce_moments: mom[m][k] = Σ_chunk part[chunk][m][k] (fixed order), plus per-series
 // aux[k] = {W2, DEN, Q2, 0}.
@@ -1300,7 +1404,9 @@ __global__ __launch_bounds__(256) void k_reduce_moments(const double *__restrict
                                                         long long P, const Info *__restrict__ info,
                                                         const double *__restrict__ fstat, int faint,
                                                         double *__restrict__ mom,
-                                                        double *__restrict__ aux) {
+                                                        double *__restrict__ aux)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     const long long k = (long long)blockIdx.x * 256 + threadIdx.x;
     const int m = blockIdx.y;
     if (k >= P) return;
@@ -1320,6 +1426,10 @@ __global__ __launch_bounds__(256) void k_reduce_moments(const double *__restrict
         aux[4 * k + 3] = (double)info->nvalid;  // N of the χ² (per series: windows)
     }
 }
+#else
+;
+#endif
+
 
 // Harmonic moments of windowed series (short spans, ≤ ~10k samples): one 256-thread workgroup
 // per (window, column) series; thread = (harmonic group hg of 3 harmonics, sample lane sl of
@@ -1329,7 +1439,9 @@ template <bool FAINT>
 __global__ __launch_bounds__(256) void k_moments_win(Problem pb, const double *__restrict__ tab,
                                                      const double *__restrict__ fstat,
                                                      double *__restrict__ mom,
-                                                     double *__restrict__ aux) {
+                                                     double *__restrict__ aux)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     const long long k = blockIdx.x;
     const Span sp = span_of(pb, k);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1405,6 +1517,10 @@ __global__ __launch_bounds__(256) void k_moments_win(Problem pb, const double *_
         }
     }
 }
+#else
+;
+#endif
+
 
 // χ²(b,ϕ) from the moments of one series (lane).
 struct HarmChi2 {
@@ -1476,11 +1592,65 @@ struct HarmChi2 {
         if (prof) prof_cycles += __builtin_amdgcn_s_memtime() - t0;
         return r;
     }
+    // The series' moments in registers, loaded before the Bessel recurrence so that their
+    // L2/MALL latency hides under it (each evaluation reads the same 98 values).
+    // GPD_PRELOAD_MOM=0 (A/B builds): loads interleaved with the sum (combine).
+#ifndef GPD_PRELOAD_MOM
+#define GPD_PRELOAD_MOM 1
+#endif
+    struct Mom {
+        double f0r, f0i, a[KH], b[KH], c[KH], d[KH];
+    };
+    __device__ __forceinline__ void load_moments(const double *__restrict__ m_, long long ld,
+                                                 long long col, Mom &M) const {
+        gdouble *p = (gdouble *)m_ + col;
+        M.f0r = p[0];
+        M.f0i = p[ld];
+        p += 3 * ld;
+#pragma unroll
+        for (int n = 0; n < KH; ++n) {
+            M.a[n] = p[0];
+            M.b[n] = p[ld];
+            M.c[n] = p[2 * ld];
+            M.d[n] = p[3 * ld];
+            p += 4 * ld;
+        }
+    }
+    // combine() on preloaded moments: the same operations in the same order
+    __device__ __forceinline__ void combine_m(const Mom &M, const double (&J)[KH + 2], double cph,
+                                              double sph, double &Sr, double &Si) const {
+        Sr = J[0] * M.f0r;
+        Si = J[0] * M.f0i;
+        double cn = 1.0, sn = 0.0;
+#pragma unroll
+        for (int n = 1; n <= KH; ++n) {
+            const double c2 = cn * cph - sn * sph;
+            const double s2 = sn * cph + cn * sph;
+            cn = c2;
+            sn = s2;
+            const double A = M.a[n - 1], B = M.b[n - 1], C = M.c[n - 1], D = M.d[n - 1];
+            double tr, ti;
+            if ((n & 1) == 0) {
+                tr = fma(A, cn, -(D * sn));
+                ti = fma(C, cn, -(B * sn));
+            } else {
+                tr = fma(B, cn, C * sn);
+                ti = -fma(D, cn, A * sn);
+            }
+            const double j2 = 2.0 * J[n];
+            Sr = fma(j2, tr, Sr);
+            Si = fma(j2, ti, Si);
+        }
+    }
     __device__ __forceinline__ double eval(const double (&x)[2]) {
         ++nfev;
         if (fallback) return 0.0;
         const double b = x[0];
         double phi = x[1];
+#if GPD_PRELOAD_MOM
+        Mom M;
+        load_moments(mom, P, k, M);
+#endif
         double J[KH + 2];
         bessel_j<KH + 1>(b, J);
         if (!(fabs(b) < 0.45 * KH) || fabs(J[KH + 1]) > tailref) {
@@ -1497,7 +1667,11 @@ struct HarmChi2 {
         double sph, cph;
         jl_sincos(phi, &sph, &cph);
         double Sr, Si;  // S = Σ w m̄ d
+#if GPD_PRELOAD_MOM
+        combine_m(M, J, cph, sph, Sr, Si);
+#else
         combine(mom, P, k, J, cph, sph, Sr, Si);
+#endif
         if (offs) {
             // [Σw  Σw m; Σw m̄  Σw|m|²] [c; a] = [Σw d; Σw m̄ d], StaticArrays 2×2 solve as in the
             // exact evaluator; Nχ² = Σw|d|² − Re(c̄ Σw d + ā S) at the solution
@@ -1549,16 +1723,25 @@ __global__ __launch_bounds__(64) void k_fit_harmonic(Problem pb, const Info *__r
                                                      const double *__restrict__ momG, long long PG,
                                                      const double *__restrict__ d0,
                                                      Param *__restrict__ out, double *__restrict__ raw,
-                                                     int *__restrict__ list, int *__restrict__ count) {
+                                                     int *__restrict__ list, int *__restrict__ count)
+#if GPD_OWNS(GPD_U_FITH)
+{
     // NEWUOA state of each lane in LDS (71 doubles, odd 8-byte stride): its ~1e3 dependent
     // accesses per iteration stay at LDS latency instead of spilling through the caches
     __shared__ Newuoa<2, 5, true> nwpool[64];
+#ifdef GPD_DIAG
+    // GPD_FIT_LANES (diagnostics): only the first `lanes` lanes of each wave hold a series
+    const int lanes = pb.fit_lanes > 0 ? pb.fit_lanes : 64;
+    if ((int)threadIdx.x >= lanes) return;
+    const long long k = (long long)blockIdx.x * lanes + threadIdx.x;
+#else
     const long long k = (long long)blockIdx.x * 64 + threadIdx.x;
+#endif
     if (k >= pb.P) return;
     const Info in = *info;
     const Span sp = span_of(pb, k);
     // harmonic path unusable for these timestamps, or a short (last) window: exact fit
-    if (in.mode == 2 || sp.s1 - sp.s0 < HARM_MIN_SPAN) {
+    if (in.mode == 2 || sp.s1 - sp.s0 < pb.harm_min) {
         list[atomicAdd(count, 1)] = (int)k;
         return;
     }
@@ -1583,12 +1766,20 @@ __global__ __launch_bounds__(64) void k_fit_harmonic(Problem pb, const Info *__r
     const unsigned long long tfit = f.prof ? __builtin_amdgcn_s_memtime() : 0;
     double x[2];
     int status = 0;
+#ifdef GPD_DIAG
+#pragma unroll
+    for (int q = 0; q < 8; ++q) nwpool[threadIdx.x].prof_[q] = 0;
+#endif
     drive_fit(f, pb, x, status, nwpool[threadIdx.x]);
     const double chi2 = f(x);  // likelihood[idx] = lkl(x) (src/Modulation.jl:416)
     if (f.prof) {
-        atomicAdd(&g_fitprof[0], f.prof_cycles);
-        atomicAdd(&g_fitprof[1], __builtin_amdgcn_s_memtime() - tfit);
-        atomicAdd(&g_fitprof[2], (unsigned long long)f.nfev);
+        atomicAdd(&pb.prof[PROF_FIT + 0], f.prof_cycles);
+        atomicAdd(&pb.prof[PROF_FIT + 1], __builtin_amdgcn_s_memtime() - tfit);
+        atomicAdd(&pb.prof[PROF_FIT + 2], (unsigned long long)f.nfev);
+#ifdef GPD_DIAG
+#pragma unroll
+        for (int q = 0; q < 8; ++q) atomicAdd(&pb.prof[PROF_NW + q], nwpool[threadIdx.x].prof_[q]);
+#endif
     }
     if (f.fallback) {
         list[atomicAdd(count, 1)] = (int)k;
@@ -1596,6 +1787,10 @@ __global__ __launch_bounds__(64) void k_fit_harmonic(Problem pb, const Info *__r
     }
     store_param(out, raw, k, f.c_re, f.c_im, f.a_re, f.a_im, x[0], x[1], chi2, f.nfev, status);
 }
+#else
+;
+#endif
+
 
 // ---------------------------------------------------------------------------------------
 // EXACT PATH — a series is fitted by G ∈ {1, 2, 4, 8} workgroups of EXACT_WG threads; NEWUOA
@@ -1640,6 +1835,7 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 
 template <bool FAINT, bool OFFS, bool PHBUF>
 struct ExactChi2 {
+    static constexpr bool kOffs = OFFS;
     const Problem *pb;
     long long doff, foff;         // series column / raw FC column offsets (setup_exact)
     const c64 *__restrict__ src;  // PHBUF: phasor column
@@ -1658,6 +1854,7 @@ struct ExactChi2 {
     Xchg x;
     unsigned nbar;  // barriers passed
     bool sync_fail; // the series' barrier was poisoned (never observed; NaN, GPD_ST_SYNC)
+    bool fp32;      // F_FP32: Float32 per-sample arithmetic (non-offsets only)
     // GPD_FIT_PROF (diagnostics): cycles of the first pass, the residual pass, the G > 1
     // exchange (barrier) and the whole fit, per workgroup
     bool prof;
@@ -1676,6 +1873,7 @@ struct ExactChi2 {
         gc64 *d, *fc, *src;
         gc32 *d32, *fc32;
         gi8 *state;
+        const __attribute__((address_space(1))) float *xr;  // F_FP32 phase table
         double omega;
         bool only_high;
     };
@@ -1690,6 +1888,7 @@ struct ExactChi2 {
         v.state = (gi8 *)pb->state;
         v.omega = pb->omega;
         v.only_high = (pb->flags & F_ONLY_HIGH) != 0;
+        v.xr = (const __attribute__((address_space(1))) float *)(fp32 ? pb->xr32 : nullptr);
         return v;
     }
     typedef __attribute__((address_space(1))) c64 gmc64;
@@ -1747,7 +1946,7 @@ struct ExactChi2 {
     };
     __device__ __forceinline__ void load_raw(const View &v, long long i, Raw &r) const {
         r.st = v.state ? (int)v.state[i] : 0;
-        r.t = v.t[i];
+        r.t = v.xr ? (double)v.xr[i] : v.t[i];  // F_FP32: the reduced phase instead of t
         r.f = PHBUF ? ld(v.src + i) : (v.fc32 ? ld(v.fc32 + foff + i) : ld(v.fc + foff + i));
         r.d = d_of(v, doff + i);
     }
@@ -1851,6 +2050,54 @@ struct ExactChi2 {
         th = th + phi;
         const double beta = b * jl_sin(th);
         return cmul(p, cisj(beta));  // power * exp(ȷ b sin(ωt+ϕ)) (src/Modulation.jl:137)
+    }
+
+    // ---- Float32 per-sample arithmetic (F_FP32; BASELINE config 5's fp32 half, the build's own
+    // experiment — the reference's Float32 path cannot run).  θ = x_i + ϕ with x_i =
+    // fl(ω t_i) reduced modulo 2π once per call in Float64 (k_phase32, shared by all series);
+    // sin, sincos, the FC phasor z/|z|, the model, the products and the residual in Float32;
+    // the sums (canonical order) and NEWUOA in Float64.
+    struct f2 {
+        float re, im;
+    };
+    static __device__ __forceinline__ f2 fmul2(f2 a, f2 b) {
+        return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
+    }
+    __device__ __forceinline__ float weight32(int st) const { return (float)weight_of(st); }
+    __device__ __forceinline__ f2 power_phasor32(const Raw &r) const {
+        const float fr = (float)r.f.re, fi = (float)r.f.im;
+        f2 ph;
+        if (PHBUF) {  // the phasor buffer holds the Float64 phasor
+            ph = {fr, fi};
+        } else {
+            const float inv = 1.0f / sqrtf(fr * fr + fi * fi);
+            ph = {fr * inv, fi * inv};
+        }
+        if (FAINT) {
+            double m = m5[0];
+#pragma unroll
+            for (int q = 1; q < 5; ++q) m = (r.st + 1 == q) ? m5[q] : m;
+            const float mf = (float)m;
+            ph = {mf * ph.re, mf * ph.im};
+        }
+        return ph;
+    }
+    __device__ __forceinline__ f2 model32(float x, const f2 &p, float b, float phi) const {
+        const float th = x + phi;
+        const float be = b * sinf(th);
+        float sn, cs;
+        sincosf(be, &sn, &cs);
+        return fmul2(p, f2{cs, sn});
+    }
+    template <int U>
+    __device__ __forceinline__ void model_batch32(const Raw (&X)[U], double b, double phi,
+                                                  c64 (&m)[U]) const {
+        const float bf = (float)b, pf = (float)phi;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const f2 mm = model32((float)X[u].t, power_phasor32(X[u]), bf, pf);
+            m[u] = c64{(double)mm.re, (double)mm.im};
+        }
     }
 
     // Per-series barrier of the G workgroups (G > 1); the caller has issued its payload stores.
@@ -2045,6 +2292,31 @@ struct ExactChi2 {
             c_im = cc.im;
             a_re = aa.re;
             a_im = aa.im;
+        } else if (fp32) {
+            double v[4];  // num(2), den(2): Float32 products, Float64 sums
+            cr_sum2m<4>(
+                [&](long long i, Raw &r) { load_raw(V, i, r); },
+                [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch32(X, b, phi, mb); },
+                [&](long long i, const Raw &r, const c64 &m, double (&a)[4]) {
+                    if (!valid_st(V, r.st)) return;
+                    if (mcg) {
+                        mcg[i - s0].re = m.re;
+                        mcg[i - s0].im = m.im;
+                    }
+                    const float w = weight32(r.st);
+                    const f2 m2 = {(float)m.re, (float)m.im}, d2 = {(float)r.d.re, (float)r.d.im};
+                    const f2 mwc = {m2.re * w, -(m2.im * w)};
+                    const f2 xv = fmul2(mwc, d2), yv = fmul2(mwc, m2);
+                    a[0] += (double)xv.re;
+                    a[1] += (double)xv.im;
+                    a[2] += (double)yv.re;
+                    a[3] += (double)yv.im;
+                },
+                v);
+            const c64 aa = cdiv(c64{v[0], v[1]}, c64{v[2], v[3]});
+            c_re = c_im = 0.0;
+            a_re = aa.re;
+            a_im = aa.im;
         } else {
             double v[4];  // num(2), den(2)
             cr_sum2m<4>(
@@ -2087,7 +2359,32 @@ struct ExactChi2 {
             const double rr = mm.re - dd.re, ri = mm.im - dd.im;
             a[0] += w * (rr * rr + ri * ri);
         };
-        if (mcg) {  // the model the same thread wrote for element i in the first pass
+        if (fp32) {  // Float32 residual, Float64 sum
+            const f2 a2 = {(float)a_re, (float)a_im};
+            auto resid32 = [&](const f2 &m2, const c64 &dd, float w, double (&a)[1]) {
+                const f2 mm = fmul2(a2, m2);
+                const float rr = mm.re - (float)dd.re, ri = mm.im - (float)dd.im;
+                a[0] += (double)(w * (rr * rr + ri * ri));
+            };
+            if (mcg) {
+                cr_sum2<1, CR_UR>([&](long long i, Raw &r) { load_res(V, i, r); },
+                                  [&](long long i, const Raw &r, double (&a)[1]) {
+                                      if (!valid_st(V, r.st)) return;
+                                      resid32(f2{(float)r.f.re, (float)r.f.im}, r.d,
+                                              weight32(r.st), a);
+                                  },
+                                  s);
+            } else {
+                cr_sum2<1, CR_UR>([&](long long i, Raw &r) { load_raw(V, i, r); },
+                                  [&](long long i, const Raw &r, double (&a)[1]) {
+                                      if (!valid_st(V, r.st)) return;
+                                      const f2 m2 = model32((float)r.t, power_phasor32(r),
+                                                            (float)b, (float)phi);
+                                      resid32(m2, r.d, weight32(r.st), a);
+                                  },
+                                  s);
+            }
+        } else if (mcg) {  // the model the same thread wrote for element i in the first pass
             cr_sum2<1, CR_UR>([&](long long i, Raw &r) { load_res(V, i, r); },
                        [&](long long i, const Raw &r, double (&a)[1]) {
                            if (!valid_st(V, r.st)) return;
@@ -2131,6 +2428,7 @@ __device__ __forceinline__ void setup_exact(F &f, const Problem &pb, long long k
     f.x = x;
     f.nbar = 0;
     f.sync_fail = false;
+    f.fp32 = !F::kOffs && (pb.flags & F_FP32) != 0;
     f.prof = (pb.flags & F_PROF) != 0;
     f.pc[0] = f.pc[1] = f.pc[2] = 0;
     if (pb.win > 0) {
@@ -2152,7 +2450,10 @@ __device__ __forceinline__ long long xser(long long b, int G) { return ((b >> 3)
 __device__ __forceinline__ int xpart(long long b, int G) { return (int)((b >> 3) % G); }
 
 template <bool FAINT, bool OFFS, bool PHBUF>
-__global__ __launch_bounds__(EXACT_WG) void k_fit_exact(Problem pb, const Info *__restrict__ info,
+#ifndef GPD_EXACT_MINB
+#define GPD_EXACT_MINB 1
+#endif
+__global__ __launch_bounds__(EXACT_WG, GPD_EXACT_MINB) void k_fit_exact(Problem pb, const Info *__restrict__ info,
                                                         const c64 *__restrict__ phbuf,
                                                         const double *__restrict__ fstat,
                                                         const int *__restrict__ list,
@@ -2162,7 +2463,9 @@ __global__ __launch_bounds__(EXACT_WG) void k_fit_exact(Problem pb, const Info *
                                                         c64 *__restrict__ mcache = nullptr,
                                                         long long mstride = 0, int G = 1,
                                                         double *__restrict__ xtot = nullptr,
-                                                        unsigned *__restrict__ xcnt = nullptr) {
+                                                        unsigned *__restrict__ xcnt = nullptr)
+#if GPD_OWNS(GPD_U_EXACT)
+{
     __shared__ double lds[EXACT_LDS];
     // NEWUOA state: one copy per wave in LDS (all lanes of a wave run the same iteration and
     // read/write the same addresses), instead of replicated in every thread's registers
@@ -2194,10 +2497,10 @@ __global__ __launch_bounds__(EXACT_WG) void k_fit_exact(Problem pb, const Info *
         if (g == 0 && threadIdx.x == 0)
             store_param(out, raw, k, f.c_re, f.c_im, f.a_re, f.a_im, x[0], x[1], chi2, f.nfev, status);
         if (f.prof && threadIdx.x == 0) {
-            atomicAdd(&g_fitprof[0], f.pc[0]);
-            atomicAdd(&g_fitprof[1], f.pc[1]);
-            atomicAdd(&g_fitprof[2], f.pc[2]);
-            atomicAdd(&g_fitprof[3], __builtin_amdgcn_s_memtime() - tf);
+            atomicAdd(&pb.prof[PROF_FIT + 0], f.pc[0]);
+            atomicAdd(&pb.prof[PROF_FIT + 1], f.pc[1]);
+            atomicAdd(&pb.prof[PROF_FIT + 2], f.pc[2]);
+            atomicAdd(&pb.prof[PROF_FIT + 3], __builtin_amdgcn_s_memtime() - tf);
         }
         return;
     }
@@ -2225,6 +2528,10 @@ __global__ __launch_bounds__(EXACT_WG) void k_fit_exact(Problem pb, const Info *
         __syncthreads();
     }
 }
+#else
+;
+#endif
+
 
 // ---------------------------------------------------------------------------------------
 // χ²(b_k, ϕ_k) for every series at a given point: the Chi2CostFunction functor
@@ -2237,7 +2544,9 @@ template <bool PHBUF>
 __global__ __launch_bounds__(EXACT_WG) void k_refine_exact(Problem pb, const Info *__restrict__ info,
                                                            const c64 *__restrict__ phbuf,
                                                            const double *__restrict__ raw,
-                                                           Param *__restrict__ out) {
+                                                           Param *__restrict__ out)
+#if GPD_OWNS(GPD_U_CHI2X)
+{
     __shared__ double lds[EXACT_LDS];
     for (long long k = blockIdx.x; k < pb.P; k += gridDim.x) {
         if (out[k].status & ST_EXACT) continue;  // uniform per workgroup
@@ -2257,13 +2566,19 @@ __global__ __launch_bounds__(EXACT_WG) void k_refine_exact(Problem pb, const Inf
         __syncthreads();
     }
 }
+#else
+;
+#endif
+
 
 template <bool FAINT, bool OFFS, bool PHBUF>
 __global__ __launch_bounds__(EXACT_WG) void k_chi2_exact(Problem pb, const Info *__restrict__ info,
                                                          const c64 *__restrict__ phbuf,
                                                          const double *__restrict__ fstat,
                                                          const double *__restrict__ bphi,
-                                                         Param *__restrict__ out) {
+                                                         Param *__restrict__ out)
+#if GPD_OWNS(GPD_U_CHI2X)
+{
     __shared__ double lds[EXACT_LDS];
     const long long k = blockIdx.x;
     ExactChi2<FAINT, OFFS, PHBUF> f;
@@ -2292,6 +2607,10 @@ __global__ __launch_bounds__(EXACT_WG) void k_chi2_exact(Problem pb, const Info 
         out[k] = p;
     }
 }
+#else
+;
+#endif
+
 
 __global__ __launch_bounds__(64) void k_chi2_harmonic(Problem pb, const Info *__restrict__ info,
                                                       const double *__restrict__ mom,
@@ -2299,7 +2618,9 @@ __global__ __launch_bounds__(64) void k_chi2_harmonic(Problem pb, const Info *__
                                                       const double *__restrict__ momG, long long PG,
                                                       const double *__restrict__ d0,
                                                       const double *__restrict__ bphi,
-                                                      Param *__restrict__ out) {
+                                                      Param *__restrict__ out)
+#if GPD_OWNS(GPD_U_FITH)
+{
     const long long k = (long long)blockIdx.x * 64 + threadIdx.x;
     if (k >= pb.P) return;
     const Info in = *info;
@@ -2332,16 +2653,28 @@ __global__ __launch_bounds__(64) void k_chi2_harmonic(Problem pb, const Info *__
     p.status = f.fallback ? ST_FALLBACK : 0;
     out[k] = p;
 }
+#else
+;
+#endif
+
 
 // ---------------------------------------------------------------------------------------
 // k_output: demodulated column over ALL samples (src/Modulation.jl:417-425).
-__global__ void k_iota(int32_t *__restrict__ a, long long n) {
+__global__ void k_iota(int32_t *__restrict__ a, long long n)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) a[i] = (int32_t)i;
 }
+#else
+;
+#endif
+
 
 // Σ d over the valid samples of series k (non-faint fitoffsets: b1 = Σ w d, w ≡ 1).
-__global__ __launch_bounds__(256) void k_series_sum(Problem pb, double *__restrict__ d0) {
+__global__ __launch_bounds__(256) void k_series_sum(Problem pb, double *__restrict__ d0)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     __shared__ double lds[4 * 2];
     const long long k = blockIdx.x;
     const Span sp = span_of(pb, k);
@@ -2360,10 +2693,16 @@ __global__ __launch_bounds__(256) void k_series_sum(Problem pb, double *__restri
         d0[2 * k + 1] = v[1];
     }
 }
+#else
+;
+#endif
+
 
 __global__ __launch_bounds__(256) void k_output(Problem pb, const Param *__restrict__ par,
                                                 const double *__restrict__ raw,
-                                                c64 *__restrict__ outd, long long ldo) {
+                                                c64 *__restrict__ outd, long long ldo)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     const long long k = blockIdx.y;
     const Span sp = span_of(pb, k);
     const Param pk = par[k];
@@ -2397,11 +2736,17 @@ __global__ __launch_bounds__(256) void k_output(Problem pb, const Param *__restr
         }
     }
 }
+#else
+;
+#endif
+
 
 // ---------------------------------------------------------------------------------------
 // gpd_libm_eval: the shared Julia-libm restatement evaluated on the device (bitwise tests).
 __global__ __launch_bounds__(256) void k_libm(int fn, long long n, const double *__restrict__ x,
-                                              const double *__restrict__ y, double *__restrict__ out) {
+                                              const double *__restrict__ y, double *__restrict__ out)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     switch (fn) {
@@ -2435,11 +2780,17 @@ __global__ __launch_bounds__(256) void k_libm(int fn, long long n, const double 
     }
     }
 }
+#else
+;
+#endif
+
 
 // ---------------------------------------------------------------------------------------
 // Synthetic data (benchmarks).  Same counter-based RNG streams as tests/synth.py.
 __global__ __launch_bounds__(256) void k_synth_truth(long long P, long long pixel_offset,
-                                                     uint64_t seed, int with_offsets, Param *truth) {
+                                                     uint64_t seed, int with_offsets, Param *truth)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     const long long k = (long long)blockIdx.x * 256 + threadIdx.x;
     if (k >= P) return;
     const uint64_t gk = (uint64_t)(pixel_offset + k);
@@ -2463,9 +2814,15 @@ __global__ __launch_bounds__(256) void k_synth_truth(long long P, long long pixe
     p.status = 0;
     truth[k] = p;
 }
+#else
+;
+#endif
+
 
 __global__ __launch_bounds__(64) void k_synth_fc(long long N, long long n_fc, long long fc_offset,
-                                                 uint64_t seed, c64 *fc, long long ldfc) {
+                                                 uint64_t seed, c64 *fc, long long ldfc)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     const long long g = (long long)blockIdx.x * 64 + threadIdx.x;
     if (g >= n_fc) return;
     const uint64_t gg = (uint64_t)(fc_offset + g);
@@ -2478,13 +2835,19 @@ __global__ __launch_bounds__(64) void k_synth_fc(long long N, long long n_fc, lo
         col[i] = {1.3 * c, 1.3 * s};
     }
 }
+#else
+;
+#endif
+
 
 __global__ __launch_bounds__(256) void k_synth_d(long long N, long long P, long long pixel_offset,
                                                  uint64_t seed, double t0, double dt, double sigma,
                                                  double omega, const Param *__restrict__ truth,
                                                  const c64 *__restrict__ fc, long long ldfc,
                                                  c64 *__restrict__ d, long long ldd,
-                                                 int32_t *__restrict__ fcop) {
+                                                 int32_t *__restrict__ fcop)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     const long long k = blockIdx.y;
     const Param tr = truth[k];
     const uint64_t gk = (uint64_t)(pixel_offset + k);
@@ -2506,11 +2869,21 @@ __global__ __launch_bounds__(256) void k_synth_d(long long N, long long P, long 
         col[i] = {pm.re + sigma * n1 / sqrt(2.0), pm.im + sigma * n2 / sqrt(2.0)};
     }
 }
+#else
+;
+#endif
 
-__global__ __launch_bounds__(256) void k_synth_t(long long N, double t0, double dt, double *t) {
+
+__global__ __launch_bounds__(256) void k_synth_t(long long N, double t0, double dt, double *t)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
     if (i < N) t[i] = t0 + (double)i * dt;
 }
+#else
+;
+#endif
+
 
 // ---------------------------------------------------------------------------------------
 // VOLT ingest / egress (processmetrology, src/GPPupilDemodulation.jl:147-157, 164-171): the FITS
@@ -2521,7 +2894,9 @@ constexpr int VT_ROWS = 64;
 
 __global__ __launch_bounds__(256) void k_volt_ingest(long long N, const float *__restrict__ volt,
                                                      long long ldv, const c64 *__restrict__ centers,
-                                                     c64 *__restrict__ out, long long ldo) {
+                                                     c64 *__restrict__ out, long long ldo)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     __shared__ float tile[VT_ROWS][81];
     const long long r0 = (long long)blockIdx.x * VT_ROWS;
     const int nr = (int)((N - r0) < VT_ROWS ? (N - r0) : VT_ROWS);
@@ -2541,11 +2916,17 @@ __global__ __launch_bounds__(256) void k_volt_ingest(long long N, const float *_
         out[k * ldo + r0 + r] = z;
     }
 }
+#else
+;
+#endif
+
 
 // Demodulated columns 0..31 (dem, ld) + the (centred) FC columns 32..39 (src, ld) → Float32 rows.
 __global__ __launch_bounds__(256) void k_volt_egress(long long N, const c64 *__restrict__ dem,
                                                      const c64 *__restrict__ src, long long ld,
-                                                     float *__restrict__ outv, long long ldov) {
+                                                     float *__restrict__ outv, long long ldov)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     __shared__ float tile[VT_ROWS][81];
     const long long r0 = (long long)blockIdx.x * VT_ROWS;
     const int nr = (int)((N - r0) < VT_ROWS ? (N - r0) : VT_ROWS);
@@ -2562,5 +2943,9 @@ __global__ __launch_bounds__(256) void k_volt_egress(long long N, const c64 *__r
         if (r < nr) outv[(r0 + r) * ldov + c] = tile[r][c];
     }
 }
+#else
+;
+#endif
+
 
 }  // namespace gpd

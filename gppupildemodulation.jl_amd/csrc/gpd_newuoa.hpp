@@ -106,8 +106,21 @@ constexpr double kAngSin[50] = {
 // DIRECT = true: the object lives in LDS (one per lane, k_fit_harmonic), so runtime indices
 // address it directly; false: per-thread objects held in registers, runtime indices become
 // select chains (no scratch).
+// Diagnostics build (build.py --diag, GPD_FIT_PROF=1): cycles of NEWUOA's phases per lane
+// (TRSAPP, BIGLAG, BIGDEN, UPDATE), summed over the fit's lanes by k_fit_harmonic.
+#if defined(GPD_DIAG) && defined(__HIP_DEVICE_COMPILE__)
+#define GPD_NW_T0(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define GPD_NW_T1(v, slot) (prof_[slot] += __builtin_amdgcn_s_memtime() - (v))
+#else
+#define GPD_NW_T0(v)
+#define GPD_NW_T1(v, slot)
+#endif
+
 template <int N, int NPT, bool DIRECT = false>
 struct Newuoa {
+#ifdef GPD_DIAG
+    unsigned long long prof_[8];
+#endif
     template <int L>
     GPD_HD static double rd_(const double (&a)[L], int k) {
         if constexpr (DIRECT) return a[k];
@@ -841,6 +854,7 @@ struct Newuoa {
     template <class F>
     GPD_HDN int run(double (&x)[N], double rhobeg, double rhoend, int maxfun, F &fun,
                    double &fx) {
+        GPD_NW_T0(tinit_);
         const int nftest = maxfun > 1 ? maxfun : 1;
         const int np = N + 1;
 #pragma unroll
@@ -969,6 +983,7 @@ struct Newuoa {
             }
         }
         int nf = NPT;
+        GPD_NW_T1(tinit_, 4);
 
         // ---------------------------------------- iterations
         double rho = rhobeg, delta = rho;
@@ -987,7 +1002,11 @@ struct Newuoa {
         nfsav = nf;
     L100:
         knew = 0;
-        trsapp(delta, d, crvmin);
+        {
+            GPD_NW_T0(tt_);
+            trsapp(delta, d, crvmin);
+            GPD_NW_T1(tt_, 0);
+        }
         dsq = 0.0;
 #pragma unroll
         for (int i = 0; i < N; ++i) dsq = dsq + d[i] * d[i];
@@ -1004,9 +1023,14 @@ struct Newuoa {
         }
     L120:
         if (dsq <= 1.0e-3 * xoptsq) shift_base(xoptsq, idz);
-        if (knew > 0) biglag(idz, knew, dstep, alpha);
+        if (knew > 0) {
+            GPD_NW_T0(tt_);
+            biglag(idz, knew, dstep, alpha);
+            GPD_NW_T1(tt_, 1);
+        }
         // VLAG and BETA for the current D; W(1..NPT) = Wcheck
         {
+            GPD_NW_T0(tvl_);
 #pragma unroll
             for (int k = 0; k < NPT; ++k) {
                 double suma = 0.0, sumb = 0.0, sum = 0.0;
@@ -1050,11 +1074,16 @@ struct Newuoa {
             }
             beta = dx * dx + dsq * (xoptsq + dx + dx + 0.5 * dsq) + beta - bsum;
             wr_(vlag, kopt - 1, rd_(vlag, kopt - 1) + 1.0);
+            GPD_NW_T1(tvl_, 5);
         }
         if (knew > 0) {
             const double vk = rd_(vlag, knew - 1);
             const double temp = 1.0 + alpha * beta / (vk * vk);
-            if (fabs(temp) <= 0.8) bigden(idz, kopt, knew, beta);
+            if (fabs(temp) <= 0.8) {
+                GPD_NW_T0(tt_);
+                bigden(idz, kopt, knew, beta);
+                GPD_NW_T1(tt_, 2);
+            }
         }
     L290:
 #pragma unroll
@@ -1149,9 +1178,14 @@ struct Newuoa {
                 if (knew == 0) goto L460;
             }
             // L410: move point knew to xnew and update the model
-            update(idz, beta, knew);
+            {
+                GPD_NW_T0(tt_);
+                update(idz, beta, knew);
+                GPD_NW_T1(tt_, 3);
+            }
             wr_(fval, knew - 1, f);
             {
+                GPD_NW_T0(tmu_);
                 const double pqk = rd_(pq, knew - 1);
                 int ih = 0;
 #pragma unroll
@@ -1221,6 +1255,7 @@ struct Newuoa {
                         }
                     }
                 }
+                GPD_NW_T1(tmu_, 6);
             }
             if (f < fsave) kopt = knew;
             if (f <= fsave + 0.1 * vquad) goto L100;

@@ -19,8 +19,8 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from ._lib import (GPD_FIT_OFFSETS, GPD_METHOD_EXACT, GPD_METHOD_HARMONIC, GPD_ONLY_HIGH,
-                   GPD_RECENTER, PARAM_DTYPE, check, load, ptr)
+from ._lib import (GPD_FIT_OFFSETS, GPD_FP32, GPD_METHOD_EXACT, GPD_METHOD_HARMONIC,
+                   GPD_ONLY_HIGH, GPD_RECENTER, PARAM_DTYPE, check, load, ptr)
 
 M_2PI = 6.283185  # src/Modulation.jl:11 (not 2π)
 
@@ -172,7 +172,9 @@ def _method_flags(method: str) -> int:
         return GPD_METHOD_EXACT
     if method == "harmonic":
         return GPD_METHOD_HARMONIC
-    raise ValueError(f"method must be auto|exact|harmonic, got {method!r}")
+    if method == "fp32":  # the exact evaluator in Float32 per-sample arithmetic (GPD_FP32)
+        return GPD_FP32
+    raise ValueError(f"method must be auto|exact|harmonic|fp32, got {method!r}")
 
 
 def _storage(d, fc):

@@ -56,6 +56,12 @@ typedef struct {
 #define GPD_ONLY_HIGH 0x4u        /* onlyhigh=true (faint mode only)                        */
 #define GPD_METHOD_EXACT 0x10u    /* force the per-sample (reference-arithmetic) evaluator  */
 #define GPD_METHOD_HARMONIC 0x20u /* force the one-pass harmonic-moment evaluator           */
+#define GPD_FP32 0x40u            /* Float32 per-sample arithmetic (BASELINE config 5's fp32
+                                     half, the build's own experiment): the exact evaluator
+                                     with θ, sin, sincos, phasor, model, products and
+                                     residual in Float32 on phases reduced modulo 2π once per
+                                     call in Float64; sums and NEWUOA stay Float64.  Not with
+                                     FIT_OFFSETS or METHOD_HARMONIC.                          */
 /* neither METHOD bit: automatic (harmonic when the timestamps allow it, else exact)          */
 
 /* per-series status bits (the reference ignores NEWUOA's status: check=false) */

@@ -1,0 +1,20 @@
+#!/usr/bin/env bash
+# A/B of the fit kernels (GPD_LIB variants, build.py --variant): C4 rank (12 500 series) and C3
+# bench steps, plus the harmonic parity tests with the release library.  → gpurun_out/ab_fit/
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$R/gpurun_out/ab_fit
+mkdir -p "$OUT"
+cd "$R"
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread \
+    tests/test_gpu_parity.py tests/test_gpu_windows.py tests/test_gpu_c4.py > "$OUT/tests.log" 2>&1 || { tail -30 "$OUT/tests.log"; exit 1; }
+tail -2 "$OUT/tests.log"
+for rep in 1 2; do
+  for lib in "" "$@"; do
+    GPD_LIB=$lib timeout -k 10 120 python bench.py --steps 10 --warmup 2 --no-cpu --no-f64 --pixels 12500 \
+        | python -c "import json,sys; j=json.loads(sys.stdin.read()); print(json.dumps({'lib':'$lib','shape':'c4rank','ms':round(j['ms_per_step'],3),'k':j['kernels_ms']}))" >> "$OUT/ab.jsonl" || exit 1
+    GPD_LIB=$lib timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu --no-f64 \
+        | python -c "import json,sys; j=json.loads(sys.stdin.read()); print(json.dumps({'lib':'$lib','shape':'c3','ms':round(j['ms_per_step'],3),'k':j['kernels_ms']}))" >> "$OUT/ab.jsonl" || exit 1
+  done
+done
+cat "$OUT/ab.jsonl"

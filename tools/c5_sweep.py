@@ -13,10 +13,13 @@ Precisions compared (the engine always computes in Float64; "fp32" is the data):
   c32      the same series rounded to ComplexF32 (the FITS VOLT precision) and kept in Float32 in
            HBM (gpd_fit_batch_c32_dev)
 for both evaluators (harmonic = default, exact = reference arithmetic), plus f64 harmonic vs f64
-exact as the scale of evaluator-level differences.  For each pair: per-series deviation of b
-(relative), ϕ and arg a (absolute, radians, mod 2π), |a| (relative), and the fraction of series
-within each tolerance 1e-3 … 1e-8.  A fully Float32 arithmetic path is not built (DESIGN.md
-§12): the reference's own Float32 path cannot run (binit is Float64, src/Modulation.jl:403).
+exact as the scale of evaluator-level differences.  Float32 *arithmetic* (GPD_FP32, "fp32"): the
+exact evaluator with θ, sin, sincos, FC phasor, model, products and residual in Float32 on phases
+reduced modulo 2π once per call in Float64 (the sums and NEWUOA stay Float64), on the Float64
+and on the ComplexF32 data — the build's own experiment (the reference's Float32 path cannot
+run: binit is Float64, src/Modulation.jl:403), measured against the Float64 exact
+path.  For each pair: per-series deviation of b (relative), ϕ and arg a (absolute, radians,
+mod 2π), |a| (relative), and the fraction of series within each tolerance 1e-3 … 1e-8.
 """
 from __future__ import annotations
 
@@ -122,7 +125,7 @@ def main():
 
     def run(c32, method):
         flags = gpd.GPD_RECENTER | {"harmonic": gpd.GPD_METHOD_HARMONIC,
-                                    "exact": gpd.GPD_METHOD_EXACT}[method]
+                                    "exact": gpd.GPD_METHOD_EXACT, "fp32": gpd.GPD_FP32}[method]
         fn = L.gpd_fit_batch_c32_dev if c32 else L.gpd_fit_batch_dev
         dd, ff = (d32, fc32) if c32 else (d, fc)
         best = None
@@ -144,7 +147,7 @@ def main():
     runs = {}
     res = {}
     for c32 in (False, True):
-        for method in ("harmonic", "exact"):
+        for method in ("harmonic", "exact", "fp32"):
             key = f"{'c32' if c32 else 'f64'}_{method}"
             res[key], runs[key] = run(c32, method)
     tr = truth.cpu().numpy().reshape(-1).view(rec)
@@ -156,6 +159,12 @@ def main():
         "c32_vs_f64": {m: summarise(res[f"c32_{m}"], res[f"f64_{m}"])
                        for m in ("harmonic", "exact")},
         "harmonic_vs_exact_f64": summarise(res["f64_harmonic"], res["f64_exact"]),
+        # Float32 arithmetic against the Float64 exact path: on the same (Float64) data, and the
+        # whole Float32 pipeline (ComplexF32 data + Float32 arithmetic)
+        "fp32_arith_vs_f64_exact": summarise(res["f64_fp32"], res["f64_exact"]),
+        "fp32_arith_c32_data_vs_f64_exact": summarise(res["c32_fp32"], res["f64_exact"]),
+        "fp32_arith_speedup_over_f64_exact": round(runs["f64_exact"]["wall_ms"]
+                                                   / runs["f64_fp32"]["wall_ms"], 2),
         "f64_exact_vs_truth_median_abs_b": float(np.median(np.abs(res["f64_exact"]["b"] - tr["b"]))),
         # whole faint harmonic step against the HBM roofline: algorithmic bytes = the series
         # (16 B, c32: 8) + its FC column shared by 4 (4 B, c32: 2) per sample, + t and the state
@@ -173,7 +182,10 @@ def main():
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     with open(args.out, "w") as f:
         json.dump(out, f, indent=1)
-    print(json.dumps({k: out[k] for k in ("c32_vs_f64", "harmonic_vs_exact_f64")}, indent=1))
+    print(json.dumps({k: out[k] for k in ("c32_vs_f64", "harmonic_vs_exact_f64",
+                                           "fp32_arith_vs_f64_exact",
+                                           "fp32_arith_c32_data_vs_f64_exact",
+                                           "fp32_arith_speedup_over_f64_exact")}, indent=1))
 
 
 if __name__ == "__main__":

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--samples", type=int, default=100_000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--c32", action="store_true")
+    ap.add_argument("--method", default="harmonic", choices=["harmonic", "exact", "fp32"])
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -54,11 +55,15 @@ def main():
     for _ in range(args.reps):
         gpd._lib.check(fn(N, P, t.data_ptr(), d.data_ptr(), N, fc.data_ptr(), G, N,
                           fcop.data_ptr(), std.data_ptr(), gpd.M_2PI, None,
-                          gpd.GPD_RECENTER | gpd.GPD_METHOD_HARMONIC, 60, params.data_ptr(),
+                          gpd.GPD_RECENTER | {"harmonic": gpd.GPD_METHOD_HARMONIC,
+                                              "exact": gpd.GPD_METHOD_EXACT,
+                                              "fp32": gpd.GPD_FP32}[args.method], 60,
+                          params.data_ptr(),
                           None, N, 0, sptr, err, len(err)), err)
         torch.cuda.synchronize(dev)
         out.append({k: round(v, 3) for k, v in gpd.timings(0).items()})
-    print(json.dumps({"series": P, "samples": N, "c32": args.c32, "kernels_ms": out[-1],
+    print(json.dumps({"series": P, "samples": N, "c32": args.c32, "method": args.method,
+                      "kernels_ms": out[-1],
                       "faint_stats_ms": [o.get("faint_stats") for o in out]}))
 
 
