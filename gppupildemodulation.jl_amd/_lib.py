@@ -158,10 +158,15 @@ def libm_eval(fn: str, x, y=None, device: int = 0):
 
 
 def timings(device: int = 0):
-    """Per-kernel HIP-event timings (ms) of the last gpd_fit_batch_dev call on `device`."""
+    """Per-kernel HIP-event timings (ms) of the last gpd_fit_batch_dev call on `device`; a stage
+    that ran once per series cohort (the pipelined harmonic path) is summed over its cohorts."""
     L = load()
-    cap = 16
+    cap = 40
     names = (ctypes.c_char_p * cap)()
     ms = (ctypes.c_double * cap)()
     n = L.gpd_last_timings(device, names, ms, cap)
-    return {names[i].decode(): ms[i] for i in range(n)}
+    out = {}
+    for i in range(n):
+        k = names[i].decode()
+        out[k] = out.get(k, 0.0) + ms[i]
+    return out

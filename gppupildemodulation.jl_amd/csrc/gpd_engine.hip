@@ -48,7 +48,9 @@ void set_err(char *buf, size_t len, const char *fmt, ...) {
         }                                                                                \
     } while (0)
 
-constexpr int kMaxTimers = 12;
+constexpr int kMaxTimers = 40;   // named kernel intervals of the last call
+constexpr int kMaxEv = 96;       // timing events of the last call (both streams)
+constexpr int kMaxCohorts = 16;  // series cohorts of the pipelined harmonic path
 
 struct DevCtx {
     int dev = -1;
@@ -56,9 +58,15 @@ struct DevCtx {
     char *ws = nullptr;
     size_t ws_cap = 0;
     hipEvent_t done = nullptr;  // orders successive calls that share the workspace
-    hipEvent_t ev[kMaxTimers + 1] = {};
+    hipEvent_t ev[kMaxEv] = {};
     const char *tname[kMaxTimers] = {};
+    int tbeg[kMaxTimers] = {}, tend[kMaxTimers] = {};  // event indices of each interval
     int ntimers = 0;
+    // pipelined harmonic path: the fits of cohort c run on `side` while the moment pass of
+    // cohort c+1 runs on the caller's stream (high priority: the latency-bound fit waves take
+    // CUs as soon as they free up)
+    hipStream_t side = nullptr;
+    hipEvent_t fork[kMaxCohorts] = {}, join = nullptr;
     bool have_timers = false;
     int n_cu = 0;  // compute units (wave-quantisation of the moment grid)
     // gpd_buildstates_dev: pinned staging of the timer lists, reused once its copy has run
@@ -101,26 +109,18 @@ struct Layout {
     int fs_mmax;        // samples per thread and part: ⌈N/2048⌉
 };
 
-Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic, bool phbuf,
-            bool mfma, int n_cu, bool harm_offs, bool windowed = false, int exact_g = 1,
-            bool fp32 = false) {
-    Layout L{};
-    size_t off = 0;
-    auto take = [&](size_t bytes) {
-        size_t o = off;
-        off += align_up(bytes);
-        return o;
-    };
-    // moment-pass grid: (series groups) × (sample chunks).  The samples are cut into U ≤ 26
-    // fixed units (whole 32-sample tiles, a function of N only) and every unit gets its own set
-    // of partial moments, reduced in unit order — so a series' moments do not depend on P, i.e.
-    // on the batch or the shard it is in (a sharded run gives the 1-GPU records bit for bit).
-    // A workgroup of the producer/consumer kernel (one per CU) streams `upw` consecutive units;
-    // upw is chosen to fill the last wave of workgroups: the smallest number of unit-times
-    // ceil(npg·ceil(U/upw) / n_cu)·upw, ties to the larger upw (fewer, longer workgroups).
-    // C3 (782 series groups, 256 CUs, U = 26): upw 1 or 2 → 79.4 / 39.7 waves; 12 500 series
-    // per GPU (C4 on 8 GPUs, 98 groups): upw 1 → 2548 workgroups = 9.95 waves (with 32 units:
-    // 12.25 waves, a 0.75-wave tail).
+// Moment-pass grid: (series groups) × (sample chunks).  The samples are cut into U ≤ 26 fixed
+// units (whole 32-sample tiles, a function of N only) and every unit gets its own set of partial
+// moments, reduced in unit order — so a series' moments do not depend on P, i.e. on the batch,
+// the shard or the cohort it is in (a sharded run gives the 1-GPU records bit for bit).  A
+// workgroup of the producer/consumer kernel (one per CU) streams `upw` consecutive units; upw is
+// chosen to fill the last wave of workgroups: the smallest number of unit-times
+// ceil(npg·ceil(U/upw) / n_cu)·upw, ties to the larger upw (fewer, longer workgroups).
+// C3 (782 series groups, 256 CUs, U = 26): upw 1 or 2 → 79.4 / 39.7 waves; 12 500 series per GPU
+// (C4 on 8 GPUs, 98 groups): upw 1 → 2548 workgroups = 9.95 waves (with 32 units: 12.25 waves,
+// a 0.75-wave tail).
+void moment_grid(long long N, long long P, int n_cu, bool harmonic, bool mfma, int &units,
+                 long long &unit_len, long long &chunk, int &nch) {
     const long long per = mfma ? MM_PIX : 64;
     const long long npg = (P + per - 1) / per;
     // at most 26 units: 26 (not 32) makes both the C3 batch (782 groups: 79.4 waves) and its
@@ -144,11 +144,25 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
         }
     }
     if (const char *e = getenv("GPD_UPW")) upw = std::min(U, std::max(1LL, atoll(e)));  // A/B only
-    L.units = (int)U;
-    L.unit_len = ulen;
-    L.chunk = mfma ? upw * ulen : ulen;
-    L.nch = (int)((U + (L.chunk / ulen) - 1) / (L.chunk / ulen));
-    const long long nch = U;  // partial-moment sets
+    units = (int)U;
+    unit_len = ulen;
+    chunk = mfma ? upw * ulen : ulen;
+    nch = (int)((U + (chunk / ulen) - 1) / (chunk / ulen));
+}
+
+Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic, bool phbuf,
+            bool mfma, int n_cu, bool harm_offs, bool windowed = false, int exact_g = 1,
+            bool fp32 = false) {
+    Layout L{};
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        size_t o = off;
+        off += align_up(bytes);
+        return o;
+    };
+    moment_grid(N, P, n_cu, harmonic, mfma, L.units, L.unit_len, L.chunk, L.nch);
+    const long long U = L.units;
+    const long long nch = U;  // partial-moment sets (units)
     L.info = take(sizeof(Info));
     L.prof = take(PROF_LEN * sizeof(unsigned long long));  // diagnostic counters
     // cos/sin table, padded to whole MM_TS-sample tiles (k_table_mix fills the padding)
@@ -159,7 +173,7 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     L.aux = take((size_t)P * 4 * sizeof(double));
     L.fstat = take(faint ? (size_t)P * 16 * sizeof(double) : 0);
     L.raw = take((size_t)P * 2 * sizeof(double));
-    L.list = take((size_t)(P + 64) * sizeof(int));
+    L.list = take((size_t)(P + 64 + kMaxCohorts) * sizeof(int));  // + per-cohort counters
     L.phbuf = take(phbuf ? (size_t)n_fc * N * sizeof(c64) : 0);
     // harmonic fitoffsets: G moments of the FC columns (same chunking), Σ d per series
     L.partG = take(harm_offs ? (size_t)nch * NMOM * n_fc * sizeof(double) : 0);
@@ -376,7 +390,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     }
     if (!cx->done) {
         HIP_TRY(hipEventCreateWithFlags(&cx->done, hipEventDisableTiming));
-        for (int i = 0; i <= kMaxTimers; ++i) HIP_TRY(hipEventCreate(&cx->ev[i]));
+        for (int i = 0; i < kMaxEv; ++i) HIP_TRY(hipEventCreate(&cx->ev[i]));
     } else {
         HIP_TRY(hipStreamWaitEvent(stream, cx->done, 0));
     }
@@ -419,21 +433,31 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     pb.xr32 = fp32 ? (const float *)(ws + L.xr32) : nullptr;
     Param *outp = (Param *)out_params;
 
-    int nt = 0;
+    int nt = 0, ne = 0;
     // GPD_SYNC_DEBUG=1: synchronise after every stage and name the stage that faulted
     static const bool sync_debug = getenv("GPD_SYNC_DEBUG") != nullptr;
-    auto mark = [&](const char *name) {
+    auto rec = [&](hipStream_t s) -> int {  // a timing event on stream s (index, or -1)
+        if (ne >= kMaxEv) return -1;
+        (void)hipEventRecord(cx->ev[ne], s);
+        return ne++;
+    };
+    // interval [beg, new event on s] named `name`; returns the new event's index
+    auto mark_on = [&](hipStream_t s, int beg, const char *name) -> int {
         if (sync_debug) {
-            const hipError_t e = hipStreamSynchronize(stream);
+            const hipError_t e = hipStreamSynchronize(s);
             if (e != hipSuccess) fprintf(stderr, "gpdemod: stage %s: %s\n", name, hipGetErrorString(e));
         }
-        if (nt < kMaxTimers) {
+        const int e = rec(s);
+        if (e >= 0 && beg >= 0 && nt < kMaxTimers) {
             cx->tname[nt] = name;
-            (void)hipEventRecord(cx->ev[nt + 1], stream);
+            cx->tbeg[nt] = beg;
+            cx->tend[nt] = e;
             ++nt;
         }
+        return e;
     };
-    HIP_TRY(hipEventRecord(cx->ev[0], stream));
+    int lastA = rec(stream);  // consecutive intervals on the caller's stream
+    auto mark = [&](const char *name) { lastA = mark_on(stream, lastA, name); };
     // diagnostic counters (GPD_FIT_PROF, GPD_MOMENTS=ws_prof): zeroed, read back after the kernel
     unsigned long long prof_h[PROF_LEN] = {};
     auto prof_reset = [&]() { return hipMemsetAsync(pb.prof, 0, sizeof prof_h, stream); };
@@ -445,7 +469,113 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     k_prepare<<<1, 1024, 0, stream>>>(pb, info);
     HIP_TRY(hipMemsetAsync(count, 0, sizeof(int), stream));
     mark("prepare");
-    if (faint) {
+    // Pipelined harmonic path (whole-exposure series, fits only, without fitoffsets): the
+    // series are cut into cohorts; cohort c's statistics, moment pass and reduction run on the
+    // caller's stream while cohort c−1's fit (latency-bound NEWUOA lanes, a few CUs) runs on the
+    // side stream.  Per-series results do not depend on the cohort (fixed sample units, §7 of
+    // DESIGN.md), so the records equal the one-cohort run's bit for bit.  Off by default
+    // (GPD_COHORTS=n opts in): the last cohort's fit is one round of waves whose latency
+    // (~1.1-1.4 ms) is exposed whatever the cohort size, so C3, C4 and C5 gained nothing
+    // (profiles/r3/cohorts.txt).
+    static const bool fit_prof_env = getenv("GPD_FIT_PROF") != nullptr;
+    int cohorts = 1;
+    if (harmonic && use_mfma && window == 0 && !bphi && !harm_offs && !fit_prof_env &&
+        !(mk && std::string(mk).rfind("ws_", 0) == 0)) {
+        cohorts = 1;  // measured: no gain by default, GPD_COHORTS opts in
+        if (const char *e = getenv("GPD_COHORTS")) cohorts = std::max(1, std::min(kMaxCohorts, atoi(e)));
+        cohorts = (int)std::min<long long>(cohorts, std::max<long long>(1, P / (2 * MM_PIX)));
+    }
+    if (cohorts > 1) {
+        if (!cx->side) {
+            int lo = 0, hi = 0;
+            HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            HIP_TRY(hipStreamCreateWithPriority(&cx->side, hipStreamNonBlocking, hi));
+            for (int c = 0; c < kMaxCohorts; ++c)
+                HIP_TRY(hipEventCreateWithFlags(&cx->fork[c], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&cx->join, hipEventDisableTiming));
+        }
+        hipStream_t side = cx->side;
+        const bool tm = mix;  // the producer/consumer kernel reads the k_table_mix layout
+        if (tm)
+            k_table_mix<<<(unsigned)((N + MM_TS - 1) / MM_TS * MM_TS / 256 + 1), 256, 0, stream>>>(
+                t, N, omega, tab);
+        else
+            k_table<<<(unsigned)((N + 255) / 256), 256, 0, stream>>>(t, N, omega, tab);
+        mark("table");
+        int *ccount = list + P + 64;  // one fallback counter per cohort
+        HIP_TRY(hipMemsetAsync(ccount, 0, kMaxCohorts * sizeof(int), stream));
+        const bool fs1 = L.fs1 && !(getenv("GPD_FAINT_STATS") &&
+                                    std::string(getenv("GPD_FAINT_STATS")) == "2");
+        const long long step = ((P + cohorts - 1) / cohorts + MM_PIX - 1) / MM_PIX * MM_PIX;
+        int c = 0;
+        for (long long k0 = 0; k0 < P; k0 += step, ++c) {
+            const long long n = std::min(step, P - k0);
+            Problem sp = pb;  // the cohort's series k0 .. k0 + n
+            sp.P = n;
+            sp.ncol = n;
+            if (is_c32)
+                sp.d32 = pb.d32 + k0 * ldd;
+            else
+                sp.d = pb.d + k0 * ldd;
+            sp.fcop = pb.fcop + k0;
+            double *fs_c = fstat + 16 * k0, *part_c = part + (size_t)L.units * NMOM * k0,
+                   *mom_c = mom + (size_t)NMOM * k0, *aux_c = aux + 4 * k0, *raw_c = raw + 2 * k0;
+            int *list_c = list + k0, *count_c = ccount + c;
+            Param *out_c = outp + k0;
+            if (faint) {
+                if (fs1)
+                    HIP_TRY(run_faint_onepass(sp, fs_c, (double *)(ws + L.fsx),
+                                              (double *)(ws + L.fsc), L.fs_pc, L.fs_mmax, is_c32,
+                                              stream));
+                else
+                    k_faint_stats<<<(unsigned)n, 256, 0, stream>>>(sp, fs_c);
+                mark("faint_stats");
+            }
+            int units, nch;
+            long long ulen, chunk;
+            moment_grid(N, n, cx->n_cu, true, true, units, ulen, chunk, nch);
+            dim3 g((unsigned)((n + MM_PIX - 1) / MM_PIX), (unsigned)nch);
+            if (faint && is_c32 && tm)
+                k_moments_ws<0, false, c32, 2, true, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, fs_c);
+            else if (faint && tm)
+                k_moments_ws<0, false, c64, 2, true, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, fs_c);
+            else if (faint && is_c32)
+                k_moments_ws<0, false, c32, 2, false, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, fs_c);
+            else if (faint)
+                k_moments_ws<0, false, c64, 2, false, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, fs_c);
+            else if (!tm && is_c32)
+                k_moments_ws<0, false, c32, 2, false><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c);
+            else if (!tm)
+                k_moments_ws<0, false, c64, 2, false><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c);
+            else if (is_c32)
+                k_moments_ws<0, false, c32, 2><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c);
+            else
+                k_moments_ws<0, false, c64, 2><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c);
+            mark("moments");
+            dim3 gr((unsigned)((n + 255) / 256), (unsigned)NMOM);
+            k_reduce_moments<<<gr, 256, 0, stream>>>(part_c, units, n, info, fs_c, faint ? 1 : 0,
+                                                     mom_c, aux_c);
+            mark("reduce");
+            // the cohort's fit on the side stream, after its moments
+            HIP_TRY(hipEventRecord(cx->fork[c], stream));
+            HIP_TRY(hipStreamWaitEvent(side, cx->fork[c], 0));
+            const int b0 = rec(side);
+            k_fit_harmonic<<<(unsigned)((n + 63) / 64), 64, 0, side>>>(
+                sp, info, mom_c, aux_c, nullptr, n_fc, nullptr, out_c, raw_c, list_c, count_c);
+            const int b1 = mark_on(side, b0, "fit_harmonic");
+            const unsigned xg = (unsigned)std::min<long long>(n, 1024);
+            if (faint)
+                k_fit_exact<true, false, false><<<xg, EXACT_WG, 0, side>>>(
+                    sp, info, nullptr, fs_c, list_c, count_c, out_c, raw_c, ST_FALLBACK);
+            else
+                k_fit_exact<false, false, false><<<xg, EXACT_WG, 0, side>>>(
+                    sp, info, nullptr, fs_c, list_c, count_c, out_c, raw_c, ST_FALLBACK);
+            mark_on(side, b1, "fit_fallback");
+        }
+        HIP_TRY(hipEventRecord(cx->join, side));
+        HIP_TRY(hipStreamWaitEvent(stream, cx->join, 0));
+        mark("fit_tail");  // the last cohort's fit, exposed
+    } else if (faint) {
         // whole-exposure series: one pass over the series, one hypot per sample (k_faint_p1/p2/
         // fin); windows: the two-pass kernel over each window's span (same bits);
         // GPD_FAINT_STATS=2 forces the two-pass kernel (tests of that identity)
@@ -461,7 +591,9 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     }
     const unsigned exact_grid = (unsigned)std::min<long long>(P, 1024);
     bool tmix = false;  // the table holds the k_table_mix layout
-    if (harmonic) {
+    if (harmonic && cohorts > 1) {
+        // fitted by the pipelined cohorts above
+    } else if (harmonic) {
         // the producer/consumer kernel (non-faint whole-exposure series, also the UNIT pass
         // of harmonic fitoffsets) reads the k_table_mix layout when mixing; every other
         // moment kernel the plain rows
@@ -597,6 +729,12 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                     "update %.3g init %.3g vlag/beta %.3g model-update %.3g cycles (lanes %d)\n",
                     (double)zn[0] / P, (double)zn[1] / P, (double)zn[2] / P, (double)zn[3] / P,
                     (double)zn[4] / P, (double)zn[5] / P, (double)zn[6] / P, pp.fit_lanes);
+            const double nw = (double)fit_wg;  // waves
+            fprintf(stderr, "fit_prof per wave: objective %.3g trsapp %.3g biglag %.3g update %.3g "
+                    "init %.3g vlag/beta %.3g model-update %.3g cycles, whole fit (max lane) "
+                    "n/a\n", (double)z[4] / nw, (double)zn[8] / nw, (double)zn[9] / nw,
+                    (double)zn[11] / nw, (double)zn[12] / nw, (double)zn[13] / nw,
+                    (double)zn[14] / nw);
 #endif
         } else {
             k_fit_harmonic<<<(unsigned)((P + 63) / 64), 64, 0, stream>>>(pb, info, mom, aux, momG,
@@ -642,11 +780,20 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         }
         const unsigned fit_grid =
             exact_g > 1 ? (unsigned)((P + 7) / 8 * 8 * exact_g) : exact_grid;
+        // two waves per SIMD (k_fit_exact MINB = 2) when the grid needs more than one round of
+        // one-wave-per-SIMD workgroups; GPD_EXACT_WAVES=1|2 forces it (A/B and tests)
+        bool two_waves = exact_g == 1 && (long long)fit_grid * (EXACT_WG / 64) > 4LL * cx->n_cu;
+        if (const char *e = getenv("GPD_EXACT_WAVES")) two_waves = atoi(e) == 2 && exact_g == 1;
 #define GPD_LAUNCH_EXACT(FA, OF, PH)                                                                 \
     do {                                                                                        \
         if (bphi)                                                                               \
             k_chi2_exact<FA, OF, PH><<<(unsigned)P, EXACT_WG, 0, stream>>>(pb, info, ph, fstat, \
                                                                            bphi, outp);         \
+        else if (two_waves)                                                                     \
+            k_fit_exact<FA, OF, PH, 2><<<fit_grid, EXACT_WG, 0, stream>>>(                    \
+                pb, info, ph, fstat, nullptr, nullptr, outp, raw, 0,                            \
+                L.mstride ? (c64 *)(ws + L.mcache) : nullptr, L.mstride, exact_g,               \
+                (double *)(ws + L.xtot), (unsigned *)(ws + L.xcnt));                            \
         else                                                                                    \
             k_fit_exact<FA, OF, PH><<<fit_grid, EXACT_WG, 0, stream>>>(                       \
                 pb, info, ph, fstat, nullptr, nullptr, outp, raw, 0,                            \
@@ -759,11 +906,12 @@ int gpd_last_timings(int device, const char **names, double *ms, int cap) {
     std::lock_guard<std::mutex> lk(cx->mu);
     if (!cx->have_timers) return 0;
     if (hipSetDevice(device) != hipSuccess) return 0;
-    if (hipEventSynchronize(cx->ev[cx->ntimers]) != hipSuccess) return 0;
     int n = std::min(cap, cx->ntimers);
+    for (int i = 0; i < n; ++i)
+        if (hipEventSynchronize(cx->ev[cx->tend[i]]) != hipSuccess) return 0;
     for (int i = 0; i < n; ++i) {
         float f = 0.f;
-        (void)hipEventElapsedTime(&f, cx->ev[i], cx->ev[i + 1]);
+        (void)hipEventElapsedTime(&f, cx->ev[cx->tbeg[i]], cx->ev[cx->tend[i]]);
         if (names) names[i] = cx->tname[i];
         if (ms) ms[i] = (double)f;
     }

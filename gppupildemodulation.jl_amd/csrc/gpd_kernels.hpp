@@ -30,7 +30,7 @@
 #define GPD_U_ENGINE 0x1  // unit 0: gpd_engine.hip
 #define GPD_U_FITH 0x2    // unit 1: k_fit_harmonic, k_chi2_harmonic
 #define GPD_U_MOM 0x44    // units 2, 6: k_moments_ws (Float64 / Float32 storage)
-#define GPD_U_EXACT 0x198  // units 3, 4, 7, 8: k_fit_exact (faint × offsets instances)
+#define GPD_U_EXACT 0xF198  // units 3, 4, 7, 8 / 12-15: k_fit_exact (faint × offsets, MINB 1 / 2)
 #define GPD_U_CHI2X 0xE20  // units 5, 9, 10, 11: k_chi2_exact, k_refine_exact
 
 namespace gpd {
@@ -59,8 +59,8 @@ constexpr uint32_t F_PROF = 0x80000000u;  // internal: k_fit_harmonic cycle spli
 constexpr uint32_t F_XSPIN_TEST = 0x40000000u;
 // Diagnostic cycle counters (GPD_FIT_PROF, GPD_MOMENTS=ws_prof) live in the workspace, reached
 // through Problem::prof: [0..3] fit split (objective, whole fit, evals, exact exchange),
-// [8..15] moment-kernel roles, [16..23] NEWUOA phases (diagnostics build)
-constexpr int PROF_FIT = 0, PROF_WS = 8, PROF_NW = 16, PROF_LEN = 32;
+// [8..15] moment-kernel roles, [16..31] NEWUOA phases (diagnostics build: lane- and wave-level)
+constexpr int PROF_FIT = 0, PROF_WS = 8, PROF_NW = 16, PROF_LEN = 40;
 
 struct Param {  // == gpd_param
     double c_re, c_im, a_re, a_im, b, phi, chi2;
@@ -1582,75 +1582,25 @@ struct HarmChi2 {
 
     // one out-of-line copy: NEWUOA calls the objective from several sites, and each inlined
     // copy of the Bessel recurrence + 24-harmonic sum adds its own live registers
-    unsigned long long prof_cycles;
+    unsigned long long prof_cycles, prof_wave;  // lane-level / wave-level (first active lane)
     bool prof;
 
     __device__ __attribute__((noinline)) double operator()(const double (&x)[2]) {
         // one inlined copy of eval (the cycle split only brackets it)
         const unsigned long long t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
         const double r = eval(x);
-        if (prof) prof_cycles += __builtin_amdgcn_s_memtime() - t0;
+        if (prof) {
+            const unsigned long long dt = __builtin_amdgcn_s_memtime() - t0;
+            prof_cycles += dt;
+            if ((int)threadIdx.x == __builtin_amdgcn_readfirstlane((int)threadIdx.x)) prof_wave += dt;
+        }
         return r;
-    }
-    // The series' moments in registers, loaded before the Bessel recurrence so that their
-    // L2/MALL latency hides under it (each evaluation reads the same 98 values).
-    // GPD_PRELOAD_MOM=0 (A/B builds): loads interleaved with the sum (combine).
-#ifndef GPD_PRELOAD_MOM
-#define GPD_PRELOAD_MOM 1
-#endif
-    struct Mom {
-        double f0r, f0i, a[KH], b[KH], c[KH], d[KH];
-    };
-    __device__ __forceinline__ void load_moments(const double *__restrict__ m_, long long ld,
-                                                 long long col, Mom &M) const {
-        gdouble *p = (gdouble *)m_ + col;
-        M.f0r = p[0];
-        M.f0i = p[ld];
-        p += 3 * ld;
-#pragma unroll
-        for (int n = 0; n < KH; ++n) {
-            M.a[n] = p[0];
-            M.b[n] = p[ld];
-            M.c[n] = p[2 * ld];
-            M.d[n] = p[3 * ld];
-            p += 4 * ld;
-        }
-    }
-    // combine() on preloaded moments: the same operations in the same order
-    __device__ __forceinline__ void combine_m(const Mom &M, const double (&J)[KH + 2], double cph,
-                                              double sph, double &Sr, double &Si) const {
-        Sr = J[0] * M.f0r;
-        Si = J[0] * M.f0i;
-        double cn = 1.0, sn = 0.0;
-#pragma unroll
-        for (int n = 1; n <= KH; ++n) {
-            const double c2 = cn * cph - sn * sph;
-            const double s2 = sn * cph + cn * sph;
-            cn = c2;
-            sn = s2;
-            const double A = M.a[n - 1], B = M.b[n - 1], C = M.c[n - 1], D = M.d[n - 1];
-            double tr, ti;
-            if ((n & 1) == 0) {
-                tr = fma(A, cn, -(D * sn));
-                ti = fma(C, cn, -(B * sn));
-            } else {
-                tr = fma(B, cn, C * sn);
-                ti = -fma(D, cn, A * sn);
-            }
-            const double j2 = 2.0 * J[n];
-            Sr = fma(j2, tr, Sr);
-            Si = fma(j2, ti, Si);
-        }
     }
     __device__ __forceinline__ double eval(const double (&x)[2]) {
         ++nfev;
         if (fallback) return 0.0;
         const double b = x[0];
         double phi = x[1];
-#if GPD_PRELOAD_MOM
-        Mom M;
-        load_moments(mom, P, k, M);
-#endif
         double J[KH + 2];
         bessel_j<KH + 1>(b, J);
         if (!(fabs(b) < 0.45 * KH) || fabs(J[KH + 1]) > tailref) {
@@ -1667,11 +1617,7 @@ struct HarmChi2 {
         double sph, cph;
         jl_sincos(phi, &sph, &cph);
         double Sr, Si;  // S = Σ w m̄ d
-#if GPD_PRELOAD_MOM
-        combine_m(M, J, cph, sph, Sr, Si);
-#else
         combine(mom, P, k, J, cph, sph, Sr, Si);
-#endif
         if (offs) {
             // [Σw  Σw m; Σw m̄  Σw|m|²] [c; a] = [Σw d; Σw m̄ d], StaticArrays 2×2 solve as in the
             // exact evaluator; Nχ² = Σw|d|² − Re(c̄ Σw d + ā S) at the solution
@@ -1762,13 +1708,13 @@ __global__ __launch_bounds__(64) void k_fit_harmonic(Problem pb, const Info *__r
     f.fallback = false;
     harm_offsets(f, pb, k, momG, PG, d0);
     f.prof = (pb.flags & F_PROF) != 0;
-    f.prof_cycles = 0;
+    f.prof_cycles = f.prof_wave = 0;
     const unsigned long long tfit = f.prof ? __builtin_amdgcn_s_memtime() : 0;
     double x[2];
     int status = 0;
 #ifdef GPD_DIAG
 #pragma unroll
-    for (int q = 0; q < 8; ++q) nwpool[threadIdx.x].prof_[q] = 0;
+    for (int q = 0; q < 16; ++q) nwpool[threadIdx.x].prof_[q] = 0;
 #endif
     drive_fit(f, pb, x, status, nwpool[threadIdx.x]);
     const double chi2 = f(x);  // likelihood[idx] = lkl(x) (src/Modulation.jl:416)
@@ -1778,7 +1724,8 @@ __global__ __launch_bounds__(64) void k_fit_harmonic(Problem pb, const Info *__r
         atomicAdd(&pb.prof[PROF_FIT + 2], (unsigned long long)f.nfev);
 #ifdef GPD_DIAG
 #pragma unroll
-        for (int q = 0; q < 8; ++q) atomicAdd(&pb.prof[PROF_NW + q], nwpool[threadIdx.x].prof_[q]);
+        for (int q = 0; q < 16; ++q) atomicAdd(&pb.prof[PROF_NW + q], nwpool[threadIdx.x].prof_[q]);
+        atomicAdd(&pb.prof[PROF_FIT + 4], f.prof_wave);
 #endif
     }
     if (f.fallback) {
@@ -2070,7 +2017,7 @@ struct ExactChi2 {
         if (PHBUF) {  // the phasor buffer holds the Float64 phasor
             ph = {fr, fi};
         } else {
-            const float inv = 1.0f / sqrtf(fr * fr + fi * fi);
+            const float inv = rsqrtf(fr * fr + fi * fi);
             ph = {fr * inv, fi * inv};
         }
         if (FAINT) {
@@ -2082,11 +2029,30 @@ struct ExactChi2 {
         }
         return ph;
     }
+    // Float32 sin and cos for the small arguments of this evaluator (|θ| ≲ 2π + |ϕ|, |β| ≤ |b|):
+    // Cody–Waite reduction by π/2 in three Float32 parts with fma, the classic minimax
+    // polynomials on [−π/4, π/4] (Cephes sinf/cosf coefficients), quadrant selected branch-free
+    static __device__ __forceinline__ void sincos32(float x, float &s, float &c) {
+        const float k = rintf(x * 0.636619772f);
+        float r = fmaf(-k, 1.57079637050628662109375f, x);
+        r = fmaf(-k, -4.37113882867379e-8f, r);
+        r = fmaf(-k, -1.7151245e-15f, r);
+        const float r2 = r * r;
+        float sp = fmaf(r2, -1.9515295891e-4f, 8.3321608736e-3f);
+        sp = fmaf(r2, sp, -1.6666654611e-1f);
+        sp = fmaf(r2 * r, sp, r);
+        float cp = fmaf(r2, 2.443315711809948e-5f, -1.388731625493765e-3f);
+        cp = fmaf(r2, cp, 4.166664568298827e-2f);
+        cp = fmaf(r2 * r2, cp, fmaf(-0.5f, r2, 1.0f));
+        const int q = (int)k & 3;
+        s = (q == 0) ? sp : (q == 1) ? cp : (q == 2) ? -sp : -cp;
+        c = (q == 0) ? cp : (q == 1) ? -sp : (q == 2) ? -cp : sp;
+    }
     __device__ __forceinline__ f2 model32(float x, const f2 &p, float b, float phi) const {
         const float th = x + phi;
-        const float be = b * sinf(th);
-        float sn, cs;
-        sincosf(be, &sn, &cs);
+        float st, ct, sn, cs;
+        sincos32(th, st, ct);
+        sincos32(b * st, sn, cs);
         return fmul2(p, f2{cs, sn});
     }
     template <int U>
@@ -2449,11 +2415,13 @@ __device__ __forceinline__ void setup_exact(F &f, const Problem &pb, long long k
 __device__ __forceinline__ long long xser(long long b, int G) { return ((b >> 3) / G) * 8 + (b & 7); }
 __device__ __forceinline__ int xpart(long long b, int G) { return (int)((b >> 3) % G); }
 
-template <bool FAINT, bool OFFS, bool PHBUF>
-#ifndef GPD_EXACT_MINB
-#define GPD_EXACT_MINB 1
-#endif
-__global__ __launch_bounds__(EXACT_WG, GPD_EXACT_MINB) void k_fit_exact(Problem pb, const Info *__restrict__ info,
+// MINB: minimum workgroups per CU the register allocation must allow.  1 (512 registers, one
+// wave per SIMD) for small grids — one exposure, G workgroups per series, a single round of
+// waves, where spills would only cost; 2 (256 registers, two waves per SIMD, spills to scratch)
+// for batches of several rounds, where the second wave hides the first one's latency (C5 exact:
+// 491 → 330 ms; C2 at G = 8: 3.40 → 3.71 ms, profiles/r3/ab_exact).
+template <bool FAINT, bool OFFS, bool PHBUF, int MINB = 1>
+__global__ __launch_bounds__(EXACT_WG, MINB) void k_fit_exact(Problem pb, const Info *__restrict__ info,
                                                         const c64 *__restrict__ phbuf,
                                                         const double *__restrict__ fstat,
                                                         const int *__restrict__ list,

@@ -110,7 +110,15 @@ constexpr double kAngSin[50] = {
 // (TRSAPP, BIGLAG, BIGDEN, UPDATE), summed over the fit's lanes by k_fit_harmonic.
 #if defined(GPD_DIAG) && defined(__HIP_DEVICE_COMPILE__)
 #define GPD_NW_T0(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#define GPD_NW_T1(v, slot) (prof_[slot] += __builtin_amdgcn_s_memtime() - (v))
+// lane-level cycles in prof_[slot], wave-level (counted by the first active lane of each
+// execution of the phase) in prof_[8 + slot]
+#define GPD_NW_T1(v, slot)                                                            \
+    do {                                                                             \
+        const unsigned long long dt_ = __builtin_amdgcn_s_memtime() - (v);           \
+        prof_[slot] += dt_;                                                          \
+        if ((int)threadIdx.x == __builtin_amdgcn_readfirstlane((int)threadIdx.x))     \
+            prof_[8 + (slot)] += dt_;                                                \
+    } while (0)
 #else
 #define GPD_NW_T0(v)
 #define GPD_NW_T1(v, slot)
@@ -119,7 +127,7 @@ constexpr double kAngSin[50] = {
 template <int N, int NPT, bool DIRECT = false>
 struct Newuoa {
 #ifdef GPD_DIAG
-    unsigned long long prof_[8];
+    unsigned long long prof_[16];
 #endif
     template <int L>
     GPD_HD static double rd_(const double (&a)[L], int k) {

@@ -114,3 +114,35 @@ def test_full_length_shard_invariance_device(gpu):
     whole = fit(0, P)
     _same(fit(1024, 1536), whole[1024:1536])
     assert not np.any(whole["status"] & gpu.GPD_ST_NAN)
+
+
+@pytest.mark.parametrize("faint", [False, True])
+@pytest.mark.parametrize("storage", ["c64", "c32"])
+def test_cohort_pipeline_records_bitwise(gpu, monkeypatch, faint, storage):
+    """The pipelined harmonic path (series cohorts: moments of cohort c on the caller's stream
+    while cohort c−1's fit runs on the side stream, gpd_engine.hip) gives the one-cohort records
+    bit for bit, for any cohort count — the fixed sample units make a series' moments
+    independent of the cohort it is in, including a ragged last cohort."""
+    import synth
+    from test_gpu_parity import faint_states
+    N, P = 12_000, 1000
+    B = synth.make_batch(N, P, seed=21)
+    st = None
+    if faint:
+        st = faint_states(N, seed=6)
+        B["d"] = B["d"] * np.where(st == 3, 1.1, np.where(st == 1, 0.05, 0.3))[None, :]
+    d, fc = B["d"], B["fc"]
+    if storage == "c32":
+        d, fc = d.astype(np.complex64), fc.astype(np.complex64)
+    args = (B["t"], d, fc, B["fc_of_pixel"])
+    recs = {}
+    for c in ("1", "2", "3", "5"):
+        monkeypatch.setenv("GPD_COHORTS", c)
+        recs[c] = gpu.fit_batch(*args, state=st, method="harmonic")
+    for c, r in recs.items():
+        _same(r, recs["1"])
+    assert not np.any(recs["1"]["status"] & gpu.GPD_ST_NAN)
+    monkeypatch.setenv("GPD_COHORTS", "2")
+    gpu.fit_batch(*args, state=st, method="harmonic")
+    t = gpu.timings(0)
+    assert "fit_tail" in t and t["moments"] > 0, t  # the cohort path ran

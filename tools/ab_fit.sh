@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$R/gpurun_out/ab_fit
 mkdir -p "$OUT"
 cd "$R"
-timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread \
+[ -n "$AB_NOTEST" ] || timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread \
     tests/test_gpu_parity.py tests/test_gpu_windows.py tests/test_gpu_c4.py > "$OUT/tests.log" 2>&1 || { tail -30 "$OUT/tests.log"; exit 1; }
 tail -2 "$OUT/tests.log"
 for rep in 1 2; do
@@ -18,3 +18,12 @@ for rep in 1 2; do
   done
 done
 cat "$OUT/ab.jsonl"
+# wave-level phase split of the fit (diagnostics build) on the C4 rank
+GPD_LIB=diag GPD_FIT_PROF=1 timeout -k 10 120 python bench.py --steps 1 --warmup 1 --no-cpu --no-f64 --pixels 12500 > "$OUT/fitprof_c4.json" 2> "$OUT/fitprof_c4.err" || exit 1
+grep fit_prof "$OUT/fitprof_c4.err" | tail -3
+# exact evaluator on the C5 batch: release vs a 2-waves/SIMD build (GPD_EXACT_MINB=2), + fp32
+for lib in "" minb2; do
+  GPD_LIB=$lib timeout -k 10 200 python tools/faint_time.py --method exact --reps 2 >> "$OUT/exact.jsonl" 2>/dev/null || exit 1
+done
+timeout -k 10 200 python tools/faint_time.py --method fp32 --reps 2 >> "$OUT/exact.jsonl" 2>/dev/null || exit 1
+cat "$OUT/exact.jsonl"
