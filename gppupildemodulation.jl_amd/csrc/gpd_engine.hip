@@ -560,7 +560,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             HIP_TRY(hipEventRecord(cx->fork[c], stream));
             HIP_TRY(hipStreamWaitEvent(side, cx->fork[c], 0));
             const int b0 = rec(side);
-            k_fit_harmonic<<<(unsigned)((n + 63) / 64), 64, 0, side>>>(
+            k_fit_harmonic<<<(unsigned)((n + GPD_FIT_WAVE_LANES - 1) / GPD_FIT_WAVE_LANES), 64, 0, side>>>(
                 sp, info, mom_c, aux_c, nullptr, n_fc, nullptr, out_c, raw_c, list_c, count_c);
             const int b1 = mark_on(side, b0, "fit_harmonic");
             const unsigned xg = (unsigned)std::min<long long>(n, 1024);
@@ -711,7 +711,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             HIP_TRY(prof_reset());
             Problem pp = pb;
             pp.flags |= F_PROF;
-            unsigned fit_wg = (unsigned)((P + 63) / 64);
+            unsigned fit_wg = (unsigned)((P + GPD_FIT_WAVE_LANES - 1) / GPD_FIT_WAVE_LANES);
 #ifdef GPD_DIAG
             pp.fit_lanes = getenv("GPD_FIT_LANES") ? std::max(1, std::min(64, atoi(getenv("GPD_FIT_LANES")))) : 64;
             fit_wg = (unsigned)((P + pp.fit_lanes - 1) / pp.fit_lanes);
@@ -737,7 +737,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                     (double)zn[14] / nw);
 #endif
         } else {
-            k_fit_harmonic<<<(unsigned)((P + 63) / 64), 64, 0, stream>>>(pb, info, mom, aux, momG,
+            k_fit_harmonic<<<(unsigned)((P + GPD_FIT_WAVE_LANES - 1) / GPD_FIT_WAVE_LANES), 64, 0, stream>>>(pb, info, mom, aux, momG,
                                                                        n_fc, d0, outp, raw, list,
                                                                        count);
         }

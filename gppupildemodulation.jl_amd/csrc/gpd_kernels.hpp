@@ -1585,7 +1585,10 @@ struct HarmChi2 {
     unsigned long long prof_cycles, prof_wave;  // lane-level / wave-level (first active lane)
     bool prof;
 
-    __device__ __attribute__((noinline)) double operator()(const double (&x)[2]) {
+#ifndef GPD_FIT_OBJ_ATTR
+#define GPD_FIT_OBJ_ATTR __attribute__((noinline))
+#endif
+    __device__ GPD_FIT_OBJ_ATTR double operator()(const double (&x)[2]) {
         // one inlined copy of eval (the cycle split only brackets it)
         const unsigned long long t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
         const double r = eval(x);
@@ -1663,7 +1666,15 @@ __device__ __forceinline__ void harm_offsets(HarmChi2 &f, const Problem &pb, lon
     f.D0i = d0[2 * k + 1];
 }
 
-__global__ __launch_bounds__(64) void k_fit_harmonic(Problem pb, const Info *__restrict__ info,
+// A/B builds: GPD_FIT_WAVE_LANES series per 64-thread workgroup (the other lanes idle; LDS and
+// the launch grid scale with it), GPD_FIT_MINB workgroups per CU the register allocation must allow
+#ifndef GPD_FIT_WAVE_LANES
+#define GPD_FIT_WAVE_LANES 64
+#endif
+#ifndef GPD_FIT_MINB
+#define GPD_FIT_MINB 1
+#endif
+__global__ __launch_bounds__(64, GPD_FIT_MINB) void k_fit_harmonic(Problem pb, const Info *__restrict__ info,
                                                      const double *__restrict__ mom,
                                                      const double *__restrict__ aux,
                                                      const double *__restrict__ momG, long long PG,
@@ -1674,14 +1685,15 @@ __global__ __launch_bounds__(64) void k_fit_harmonic(Problem pb, const Info *__r
 {
     // NEWUOA state of each lane in LDS (71 doubles, odd 8-byte stride): its ~1e3 dependent
     // accesses per iteration stay at LDS latency instead of spilling through the caches
-    __shared__ Newuoa<2, 5, true> nwpool[64];
+    __shared__ Newuoa<2, 5, true> nwpool[GPD_FIT_WAVE_LANES];
 #ifdef GPD_DIAG
     // GPD_FIT_LANES (diagnostics): only the first `lanes` lanes of each wave hold a series
-    const int lanes = pb.fit_lanes > 0 ? pb.fit_lanes : 64;
+    const int lanes = pb.fit_lanes > 0 ? pb.fit_lanes : GPD_FIT_WAVE_LANES;
     if ((int)threadIdx.x >= lanes) return;
     const long long k = (long long)blockIdx.x * lanes + threadIdx.x;
 #else
-    const long long k = (long long)blockIdx.x * 64 + threadIdx.x;
+    if ((int)threadIdx.x >= GPD_FIT_WAVE_LANES) return;
+    const long long k = (long long)blockIdx.x * GPD_FIT_WAVE_LANES + threadIdx.x;
 #endif
     if (k >= pb.P) return;
     const Info in = *info;
