@@ -1792,7 +1792,9 @@ struct Xchg {
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
 
-template <bool FAINT, bool OFFS, bool PHBUF>
+// UR: samples per prefetched batch of the residual pass (the model cache and the series);
+// 8 at two waves per SIMD (C5 exact 339 → 315-320 ms), 4 at one (r2: 2/6/8/16 no better there)
+template <bool FAINT, bool OFFS, bool PHBUF, int UR = CR_UR>
 struct ExactChi2 {
     static constexpr bool kOffs = OFFS;
     const Problem *pb;
@@ -2345,7 +2347,7 @@ struct ExactChi2 {
                 a[0] += (double)(w * (rr * rr + ri * ri));
             };
             if (mcg) {
-                cr_sum2<1, CR_UR>([&](long long i, Raw &r) { load_res(V, i, r); },
+                cr_sum2<1, UR>([&](long long i, Raw &r) { load_res(V, i, r); },
                                   [&](long long i, const Raw &r, double (&a)[1]) {
                                       if (!valid_st(V, r.st)) return;
                                       resid32(f2{(float)r.f.re, (float)r.f.im}, r.d,
@@ -2353,7 +2355,7 @@ struct ExactChi2 {
                                   },
                                   s);
             } else {
-                cr_sum2<1, CR_UR>([&](long long i, Raw &r) { load_raw(V, i, r); },
+                cr_sum2<1, UR>([&](long long i, Raw &r) { load_raw(V, i, r); },
                                   [&](long long i, const Raw &r, double (&a)[1]) {
                                       if (!valid_st(V, r.st)) return;
                                       const f2 m2 = model32((float)r.t, power_phasor32(r),
@@ -2363,7 +2365,7 @@ struct ExactChi2 {
                                   s);
             }
         } else if (mcg) {  // the model the same thread wrote for element i in the first pass
-            cr_sum2<1, CR_UR>([&](long long i, Raw &r) { load_res(V, i, r); },
+            cr_sum2<1, UR>([&](long long i, Raw &r) { load_res(V, i, r); },
                        [&](long long i, const Raw &r, double (&a)[1]) {
                            if (!valid_st(V, r.st)) return;
                            resid(r.f, r.d, weight_of(r.st), a);
@@ -2455,7 +2457,7 @@ __global__ __launch_bounds__(EXACT_WG, MINB) void k_fit_exact(Problem pb, const 
         const long long k = xser(blockIdx.x, G);
         if (k >= pb.P) return;  // uniform per series: all its parts leave together
         const int g = xpart(blockIdx.x, G);
-        ExactChi2<FAINT, OFFS, PHBUF> f;
+        ExactChi2<FAINT, OFFS, PHBUF, (MINB == 2 ? 8 : CR_UR)> f;
         setup_exact(f, pb, k, PHBUF ? phbuf : nullptr, lds, nvalid, G, g,
                     Xchg{xtot + k * (2 * CR_BLOCKS * CR_NV), xcnt + k});
         if (mcache) f.mc = mcache + k * mstride;
@@ -2487,7 +2489,7 @@ __global__ __launch_bounds__(EXACT_WG, MINB) void k_fit_exact(Problem pb, const 
     const long long total = list ? (long long)(*count) : pb.P;
     for (long long idx = blockIdx.x; idx < total; idx += gridDim.x) {
         const long long k = list ? (long long)list[idx] : idx;
-        ExactChi2<FAINT, OFFS, PHBUF> f;
+        ExactChi2<FAINT, OFFS, PHBUF, (MINB == 2 ? 8 : CR_UR)> f;
         setup_exact(f, pb, k, PHBUF ? phbuf : nullptr, lds, nvalid);
         if (mcache) f.mc = mcache + (long long)blockIdx.x * mstride;
         if (FAINT) {
