@@ -264,6 +264,37 @@ def main():
                    "note": "GPD_MIX=0: all 24 harmonics on v_mfma_f64_16x16x4 (not the headline)",
                    "records": par64}
 
+    # one C4 rank rehearsed on this GPU: the shard an 8-GPU node's rank fits (12 500 series of
+    # the resident batch, a view — its records equal the batch's bit for bit, tests/test_gpu_c4.py),
+    # timed the same way; the driver measures the 8-GPU run itself
+    c4 = None
+    if world == 1 and (P_total, N) == (100_000, 100_000) and args.scaling == "strong":
+        n8 = shard.shard_counts(P_total, 8)[0]
+        fo8 = fcop[:n8].contiguous()
+        p8 = torch.empty((n8, 64), dtype=torch.uint8, device=dev)
+
+        def step8():
+            r = fit_dev(N, n8, t.data_ptr(), d.data_ptr(), N, fc.data_ptr(), n8 // 4, N,
+                        fo8.data_ptr(), None, gpd.M_2PI, None, flags, 60, p8.data_ptr(), None, N,
+                        local, sptr, err, len(err))
+            gpd._lib.check(r, err)
+        for _ in range(2):
+            step8()
+        torch.cuda.synchronize(dev)
+        k8 = {}
+        t8 = time.perf_counter()
+        for _ in range(args.steps):
+            step8()
+            for name, ms in gpd.timings(local).items():
+                k8.setdefault(name, []).append(ms)
+        torch.cuda.synchronize(dev)
+        ms8 = 1e3 * (time.perf_counter() - t8) / args.steps
+        c4 = {"series": n8, "ms_per_step": round(ms8, 3),
+              "kernels_ms": {k: round(float(np.mean(v)), 3) for k, v in k8.items()},
+              "projected_speedup_at_8_gpus": round(1e3 * elapsed / args.steps / ms8, 2),
+              "note": "rank 0's shard of the C4 split fitted alone on this GPU (no gather); "
+                      "not the measured 8-GPU scaling"}
+
     cpu = None
     if not args.no_cpu and args.cpu_pixels > 0 and world == 1:  # rank 0 at N=1 only
         cpu = cpu_baseline(gpd, t, d, fc, fcop, par, args, N,
@@ -284,7 +315,7 @@ def main():
                    "gather": ("none" if not use_dist else "RCCL gather of 64-B records to rank 0"
                               if backend == "nccl" else f"{backend} gather (multi-rank rehearsal)")},
         "roofline": roofline, "cpu_baseline": cpu, "kernels_ms": kernels, "fits": fits,
-        "all_f64_moments": f64_all,
+        "all_f64_moments": f64_all, "c4_rank_rehearsal": c4,
     }
     print(json.dumps(out))
     if dist:
