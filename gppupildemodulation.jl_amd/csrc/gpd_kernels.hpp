@@ -559,8 +559,11 @@ __device__ __forceinline__ void fs_accum3(int q, double a, double b, int (&cnt)[
     }
 }
 
+#ifndef GPD_FS_MINW
+#define GPD_FS_MINW 1  // A/B builds: minimum waves per SIMD the register allocation must allow
+#endif
 template <class TS>
-__global__ __launch_bounds__(256) void k_faint_p1(Problem pb, long long k0, int Mmax,
+__global__ __launch_bounds__(256, GPD_FS_MINW) void k_faint_p1(Problem pb, long long k0, int Mmax,
                                                   double *__restrict__ scr,
                                                   double *__restrict__ xt)
 #if GPD_OWNS(GPD_U_ENGINE)
