@@ -21,7 +21,8 @@ cat "$OUT/ab.jsonl"
 # wave-level phase split of the fit (diagnostics build) on the C4 rank
 GPD_LIB=diag GPD_FIT_PROF=1 timeout -k 10 120 python bench.py --steps 1 --warmup 1 --no-cpu --no-f64 --pixels 12500 > "$OUT/fitprof_c4.json" 2> "$OUT/fitprof_c4.err" || exit 1
 grep fit_prof "$OUT/fitprof_c4.err" | tail -3
-# exact evaluator on the C5 batch: release vs a 2-waves/SIMD build (GPD_EXACT_MINB=2), + fp32
+# exact evaluator on the C5 batch (AB_EXACT=1): release vs a 2-waves/SIMD build, + fp32
+[ -n "$AB_EXACT" ] || exit 0
 for lib in "" minb2; do
   GPD_LIB=$lib timeout -k 10 200 python tools/faint_time.py --method exact --reps 2 >> "$OUT/exact.jsonl" 2>/dev/null || exit 1
 done
