@@ -1,0 +1,129 @@
+#!/usr/bin/env python3
+"""Randomised parity soak (GPU box): random shapes, FC layouts, faint states, flags and
+timestamp offsets through gpd_fit_batch with the exact evaluator, every record compared with the
+oracle bit for bit (tests/test_gpu_parity.assert_exact_bitwise); the auto method on the same
+inputs is checked against the oracle under the harmonic tie rule when it fits harmonically.
+Runs cases until --seconds have passed; one line per case; exits non-zero on the first failure.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+    sys.path.insert(0, p)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=150.0)
+    ap.add_argument("--seed", type=int, default=2026)
+    args = ap.parse_args()
+    import numpy as np
+
+    import gpdemod_loader
+    import oracle
+    import synth
+    from test_gpu_parity import HARM_ULPS, _dev, assert_exact_bitwise, assert_fit_parity
+
+    def parity(auto, ref, pert):
+        """The tie rule; where the oracle's own outcomes under χ² noise already spread beyond
+        NEWUOA's rhoend (a chaotic landscape, e.g. the MJD-quantised staircase in ϕ started from a
+        far xinit), landing anywhere inside 1.5× that spread is admissible too."""
+        keys = ("b", "phi", "a", "chi2")
+        env = max(float(np.max([_dev(p, ref, k) for k in keys])) for p in pert)
+        return assert_fit_parity(auto, ref, pert, label="auto", min_match=0.0,
+                                 max_dev=max(1e-3, 1.5 * env + 1e-10)), env > 1e-3
+
+    gpd = gpdemod_loader.load()
+    gpd.load()
+    oracle.build()
+    rng = np.random.default_rng(args.seed)
+    t_end = time.time() + args.seconds
+    case = 0
+    escalated = 0  # cases whose tie series needed the 48-run envelope
+    chaotic_cases = 0  # cases where the oracle's own outcomes spread beyond rhoend
+    while time.time() < t_end:
+        case += 1
+        N = int(rng.choice([2, 3, 17, 255, 256, 257, 1000, 2047, 2048, 2049, 5000, 12345, 20000]))
+        P = int(rng.integers(1, 41))
+        group = int(rng.choice([1, 2, 4]))
+        t0 = float(rng.choice([0.0, 0.0, 86400.0 * 60000.5]))
+        B = synth.make_batch(N, P, seed=int(rng.integers(1, 1 << 30)), t0=t0, group=group,
+                             offsets=bool(rng.random() < 0.3))
+        if rng.random() < 0.3:  # a general FC assignment
+            B["fc_of_pixel"] = rng.integers(0, B["fc"].shape[0], P).astype(np.int32)
+        kw = {"recenter": bool(rng.random() < 0.8), "fitoffsets": bool(rng.random() < 0.3)}
+        state = None
+        if rng.random() < 0.35 and N >= 8:
+            # runs of HIGH (3) / NORMAL (2) / LOW (1) / TRANSIENT (-1)
+            state = np.empty(N, np.int8)
+            i = 0
+            while i < N:
+                L = int(rng.integers(1, max(2, N // 4)))
+                state[i:i + L] = rng.choice([3, 2, 1, -1], p=[0.3, 0.3, 0.3, 0.1])
+                i += L
+            kw["onlyhigh"] = bool(rng.random() < 0.4)
+        xinit = None
+        if rng.random() < 0.2:
+            xinit = (float(rng.uniform(0.2, 2.0)), float(rng.uniform(-3, 3)))
+        okw = dict(kw)
+        if state is not None:
+            okw["state"] = state
+        if xinit is not None:
+            okw["xinit"] = xinit
+        t1 = time.time()
+        ref = (oracle.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], state=state,
+                                xinit=xinit,
+                                flags=(oracle.RECENTER if kw["recenter"] else 0)
+                                | (oracle.FIT_OFFSETS if kw["fitoffsets"] else 0)
+                                | (oracle.ONLY_HIGH if kw.get("onlyhigh") else 0)))
+        got = gpd.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], method="exact", **okw)
+        desc = {"case": case, "N": N, "P": P, "group": group, "t0": t0, "faint": state is not None,
+                **kw, "xinit": xinit}
+        try:
+            assert_exact_bitwise(got, ref, label=json.dumps(desc))
+        except AssertionError as e:
+            print("FAIL exact", e, flush=True)
+            return 1
+        auto = gpd.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], **okw)
+        harm = int(((auto["status"] & gpd.GPD_ST_EXACT) == 0).sum())
+        verdict, wild = "exact-only", False
+        if harm and N >= 2000 and not kw["fitoffsets"]:
+            pert = [oracle.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], state=state,
+                                     xinit=xinit, perturb_seed=s, perturb_ulps=HARM_ULPS,
+                                     flags=(oracle.RECENTER if kw["recenter"] else 0)
+                                     | (oracle.ONLY_HIGH if kw.get("onlyhigh") else 0))
+                    for s in range(1, 13)]
+            try:
+                verdict, wild = parity(auto, ref, pert)
+            except AssertionError as e12:
+                # the bench's escalation: 36 more oracle runs at 512 ulp
+                pert += [oracle.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], state=state,
+                                          xinit=xinit, perturb_seed=s, perturb_ulps=4 * HARM_ULPS,
+                                          flags=(oracle.RECENTER if kw["recenter"] else 0)
+                                          | (oracle.ONLY_HIGH if kw.get("onlyhigh") else 0))
+                         for s in range(13, 49)]
+                try:
+                    verdict, wild = parity(auto, ref, pert)
+                    verdict = "after 48 oracle runs: " + verdict
+                    escalated += 1
+                except AssertionError as e:
+                    print("FAIL auto", json.dumps(desc), e12, "|", e, flush=True)
+                    return 1
+        chaotic_cases += wild
+        print(json.dumps({**desc, "exact": "bitwise", "auto_harmonic_series": harm,
+                          "auto": verdict, "oracle_spread_beyond_rhoend": wild,
+                          "s": round(time.time() - t1, 2)}), flush=True)
+    print(f"soak: {case} cases, all exact records bit-identical to the oracle; harmonic ties "
+          f"explained by 12 oracle runs except {escalated} case(s) that needed 48; "
+          f"{chaotic_cases} case(s) where the oracle itself spread beyond rhoend", flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
