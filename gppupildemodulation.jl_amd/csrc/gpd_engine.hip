@@ -119,6 +119,21 @@ struct Layout {
 // C3 (782 series groups, 256 CUs, U = 26): upw 1 or 2 → 79.4 / 39.7 waves; 12 500 series per GPU
 // (C4 on 8 GPUs, 98 groups): upw 1 → 2548 workgroups = 9.95 waves (with 32 units: 12.25 waves,
 // a 0.75-wave tail).
+// Series per wave of the lane-per-series fit (k_fit_harmonic).  A wave lasts as long as its
+// slowest lane, and lanes diverging through NEWUOA's branches serialise its phases,
+// so fewer series per wave finish sooner — as long as the waves do not crowd the CUs: the fewest
+// lanes (a power of two, ≤ 64) that keep the fit at one wave per CU.  Measured on one MI355X
+// (tools/fit_lanes_sweep.py, profiles/r3/fit_lanes_sweep.jsonl): one exposure (32 series) 0.71 →
+// 0.42 ms, 512 series 0.95 → 0.58 ms, 2048 series 0.96 → 0.82 ms; 4096 and more unchanged (the
+// rule gives 16 and 64 lanes).  Every lane runs the same arithmetic whatever the wave holds: the
+// records are the same bits for any setting.  GPD_FIT_LANES overrides (A/B).
+int fit_lanes_for(long long P, int n_cu) {
+    int lanes = 1;
+    while (lanes < GPD_FIT_WAVE_LANES && (P + lanes - 1) / lanes > std::max(1, n_cu)) lanes *= 2;
+    if (const char *e = getenv("GPD_FIT_LANES")) lanes = std::max(1, std::min(GPD_FIT_WAVE_LANES, atoi(e)));
+    return lanes;
+}
+
 void moment_grid(long long N, long long P, int n_cu, bool harmonic, bool mfma, int &units,
                  long long &unit_len, long long &chunk, int &nch) {
     const long long per = mfma ? MM_PIX : 64;
@@ -560,7 +575,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             HIP_TRY(hipEventRecord(cx->fork[c], stream));
             HIP_TRY(hipStreamWaitEvent(side, cx->fork[c], 0));
             const int b0 = rec(side);
-            k_fit_harmonic<<<(unsigned)((n + GPD_FIT_WAVE_LANES - 1) / GPD_FIT_WAVE_LANES), 64, 0, side>>>(
+            sp.fit_lanes = fit_lanes_for(n, cx->n_cu);
+            k_fit_harmonic<<<(unsigned)((n + sp.fit_lanes - 1) / sp.fit_lanes), 64, 0, side>>>(
                 sp, info, mom_c, aux_c, nullptr, n_fc, nullptr, out_c, raw_c, list_c, count_c);
             const int b1 = mark_on(side, b0, "fit_harmonic");
             const unsigned xg = (unsigned)std::min<long long>(n, 1024);
@@ -711,11 +727,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             HIP_TRY(prof_reset());
             Problem pp = pb;
             pp.flags |= F_PROF;
-            unsigned fit_wg = (unsigned)((P + GPD_FIT_WAVE_LANES - 1) / GPD_FIT_WAVE_LANES);
-#ifdef GPD_DIAG
-            pp.fit_lanes = getenv("GPD_FIT_LANES") ? std::max(1, std::min(64, atoi(getenv("GPD_FIT_LANES")))) : 64;
-            fit_wg = (unsigned)((P + pp.fit_lanes - 1) / pp.fit_lanes);
-#endif
+            pp.fit_lanes = fit_lanes_for(P, cx->n_cu);
+            const unsigned fit_wg = (unsigned)((P + pp.fit_lanes - 1) / pp.fit_lanes);
             k_fit_harmonic<<<fit_wg, 64, 0, stream>>>(pp, info, mom, aux, momG,
                                                                        n_fc, d0, outp, raw, list,
                                                                        count);
@@ -737,9 +750,10 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                     (double)zn[14] / nw);
 #endif
         } else {
-            k_fit_harmonic<<<(unsigned)((P + GPD_FIT_WAVE_LANES - 1) / GPD_FIT_WAVE_LANES), 64, 0, stream>>>(pb, info, mom, aux, momG,
-                                                                       n_fc, d0, outp, raw, list,
-                                                                       count);
+            Problem pf = pb;
+            pf.fit_lanes = fit_lanes_for(P, cx->n_cu);
+            k_fit_harmonic<<<(unsigned)((P + pf.fit_lanes - 1) / pf.fit_lanes), 64, 0, stream>>>(
+                pf, info, mom, aux, momG, n_fc, d0, outp, raw, list, count);
         }
         mark("fit_harmonic");
         // fallback: series whose fit left the expansion's safe range, re-fitted exactly

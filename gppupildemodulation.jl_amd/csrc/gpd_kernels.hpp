@@ -107,7 +107,7 @@ struct Problem {
     // GPD_HARM_MIN_SPAN overrides it for the window-length sweep, tools/window_sweep.py)
     long long harm_min;
     unsigned long long *prof;  // PROF_LEN diagnostic counters (workspace), or nullptr
-    int fit_lanes;             // diagnostics build: series per k_fit_harmonic wave (0 = 64)
+    int fit_lanes;             // series per k_fit_harmonic wave (0 = GPD_FIT_WAVE_LANES)
     const float *xr32;         // F_FP32: rem(fl(ω t_i), 2π) per sample (k_phase32), or nullptr
 };
 
@@ -1689,15 +1689,11 @@ __global__ __launch_bounds__(64, GPD_FIT_MINB) void k_fit_harmonic(Problem pb, c
     // NEWUOA state of each lane in LDS (71 doubles, odd 8-byte stride): its ~1e3 dependent
     // accesses per iteration stay at LDS latency instead of spilling through the caches
     __shared__ Newuoa<2, 5, true> nwpool[GPD_FIT_WAVE_LANES];
-#ifdef GPD_DIAG
-    // GPD_FIT_LANES (diagnostics): only the first `lanes` lanes of each wave hold a series
+    // series per wave (pb.fit_lanes, fit_lanes_for() in gpd_engine.hip): only the first `lanes`
+    // lanes of each wave hold a series
     const int lanes = pb.fit_lanes > 0 ? pb.fit_lanes : GPD_FIT_WAVE_LANES;
     if ((int)threadIdx.x >= lanes) return;
     const long long k = (long long)blockIdx.x * lanes + threadIdx.x;
-#else
-    if ((int)threadIdx.x >= GPD_FIT_WAVE_LANES) return;
-    const long long k = (long long)blockIdx.x * GPD_FIT_WAVE_LANES + threadIdx.x;
-#endif
     if (k >= pb.P) return;
     const Info in = *info;
     const Span sp = span_of(pb, k);
