@@ -37,17 +37,19 @@ def _stale(out: str) -> bool:
 
 
 def build(force: bool = False, verbose: bool = False, diag: bool = False, jobs: int = 0,
-          variant: str | None = None, defines: tuple = (), only: tuple = ()) -> str:
-    """variant: an A/B build libgpdemod_<variant>.so with extra -D `defines` (loaded with
-    GPD_LIB=<variant>, tools/ab_*.sh); `only`: compile just these units for the variant and
-    link the other units' objects of the release build; diag: the diagnostics build."""
+          variant: str | None = None, defines: tuple = (), only: tuple = (),
+          flags: tuple = ()) -> str:
+    """variant: an A/B build libgpdemod_<variant>.so with extra -D `defines` and compiler
+    `flags` (loaded with GPD_LIB=<variant>, tools/ab_*.sh); `only`: compile just these units for
+    the variant and link the other units' objects of the release build; diag: the diagnostics
+    build."""
     out = (os.path.join(HERE, f"libgpdemod_{variant}.so") if variant
            else OUT_DIAG if diag else OUT)
     if not force and not _stale(out):
         return out
     objdir = os.path.join(HERE, "build", variant or ("diag" if diag else "release"))
     os.makedirs(objdir, exist_ok=True)
-    extra = (["-DGPD_DIAG"] if diag else []) + [f"-D{d}" for d in defines]
+    extra = (["-DGPD_DIAG"] if diag else []) + [f"-D{d}" for d in defines] + list(flags)
     jobs = jobs or max(1, min(len(SOURCES), os.cpu_count() or 1))
     procs, objs, errs = [], [], []
     pending = [u for u in SOURCES if not only or u in only]
@@ -83,10 +85,11 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, jobs: 
 if __name__ == "__main__":
     import sys
 
-    # build.py [--diag] [--variant NAME -DDEF ...]
+    # build.py [--diag] [--variant NAME -DDEF ... --flag=-mllvm --flag=-opt ...]
     argv = sys.argv[1:]
     var = argv[argv.index("--variant") + 1] if "--variant" in argv else None
     defs = tuple(a[2:] for a in argv if a.startswith("-D"))
     only = tuple(argv[argv.index("--only") + 1].split(",")) if "--only" in argv else ()
+    flg = tuple(a[len("--flag="):] for a in argv if a.startswith("--flag="))
     print(build(force=True, verbose=True, diag="--diag" in argv, variant=var, defines=defs,
-                only=only))
+                only=only, flags=flg))

@@ -62,9 +62,11 @@ def main():
                           None, N, 0, sptr, err, len(err)), err)
         torch.cuda.synchronize(dev)
         out.append({k: round(v, 3) for k, v in gpd.timings(0).items()})
+    rec = params.cpu().numpy().reshape(-1).view(gpd.PARAM_DTYPE)
     print(json.dumps({"series": P, "samples": N, "c32": args.c32, "method": args.method,
                       "kernels_ms": out[-1],
-                      "faint_stats_ms": [o.get("faint_stats") for o in out]}))
+                      "faint_stats_ms": [o.get("faint_stats") for o in out],
+                      "mean_nfev": round(float(rec["nfev"].mean()), 3)}))
 
 
 if __name__ == "__main__":

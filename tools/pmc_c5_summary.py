@@ -11,7 +11,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KEEP = ("k_faint_p1", "k_faint_p2", "k_faint_fin", "k_moments_ws", "k_reduce_moments",
+KEEP = ("k_faint_p1", "k_faint_p2", "k_faint_fin", "k_moments_ws", "k_reduce_moments", "k_fit_exact",
         "k_fit_harmonic", "k_prepare", "k_table")
 
 
