@@ -122,16 +122,16 @@ struct Layout {
 // Series per wave of the lane-per-series fit (k_fit_harmonic).  A wave lasts as long as its
 // slowest lane, and lanes diverging through NEWUOA's branches serialise its phases,
 // so fewer series per wave finish sooner — as long as the waves do not crowd the CUs: the fewest
-// lanes (a power of two, ≤ 64) that keep the fit at one wave per CU.  Measured on one MI355X
-// (tools/fit_lanes_sweep.py, profiles/r3/fit_lanes_sweep.jsonl): one exposure (32 series) 0.71 →
-// 0.42 ms, 512 series 0.95 → 0.58 ms, 2048 series 0.96 → 0.82 ms; 4096 and more unchanged (the
-// rule gives 16 and 64 lanes).  Every lane runs the same arithmetic whatever the wave holds: the
-// records are the same bits for any setting.  GPD_FIT_LANES overrides (A/B).
+// lanes (≤ 64) that keep the fit at one wave per CU, ⌈P / n_cu⌉.  Measured on one MI355X
+// (tools/fit_lanes_sweep.py, profiles/r3/fit_lanes_*.jsonl): one exposure (32 series) 0.71 →
+// 0.42 ms, 512 series 0.95 → 0.58 ms, 2048 series 0.96 → 0.82 ms, a C4 rank (12 500 series, 49
+// lanes) 1.05 → 1.01 ms; 1e5 series stay at 64.  Every lane runs the same arithmetic whatever the
+// wave holds: the records are the same bits for any setting.  GPD_FIT_LANES overrides (A/B).
 int fit_lanes_for(long long P, int n_cu) {
-    int lanes = 1;
-    while (lanes < GPD_FIT_WAVE_LANES && (P + lanes - 1) / lanes > std::max(1, n_cu)) lanes *= 2;
+    long long lanes = (P + std::max(1, n_cu) - 1) / std::max(1, n_cu);
+    lanes = std::max<long long>(1, std::min<long long>(GPD_FIT_WAVE_LANES, lanes));
     if (const char *e = getenv("GPD_FIT_LANES")) lanes = std::max(1, std::min(GPD_FIT_WAVE_LANES, atoi(e)));
-    return lanes;
+    return (int)lanes;
 }
 
 void moment_grid(long long N, long long P, int n_cu, bool harmonic, bool mfma, int &units,
