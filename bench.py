@@ -58,6 +58,8 @@ def parse():
                     help="0: the CPUs this process may run on (sched_getaffinity), capped by "
                          "OMP_NUM_THREADS when the pool sets it (the box's CPU share)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="skip the C4-rank rehearsal block (profiling runs: one kernel shape)")
     ap.add_argument("--dist-always", action="store_true",
                     help="initialise torch.distributed even at world size 1 (launch with "
                          "torch.distributed.run --nproc-per-node 1) and send the records through "
@@ -268,7 +270,8 @@ def main():
     # the resident batch, a view — its records equal the batch's bit for bit, tests/test_gpu_c4.py),
     # timed the same way; the driver measures the 8-GPU run itself
     c4 = None
-    if world == 1 and (P_total, N) == (100_000, 100_000) and args.scaling == "strong":
+    if (world == 1 and (P_total, N) == (100_000, 100_000) and args.scaling == "strong"
+            and not args.no_c4):
         n8 = shard.shard_counts(P_total, 8)[0]
         fo8 = fcop[:n8].contiguous()
         p8 = torch.empty((n8, 64), dtype=torch.uint8, device=dev)
