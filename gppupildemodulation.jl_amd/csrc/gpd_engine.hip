@@ -378,8 +378,10 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     int exact_g = 1;
     if (want_exact && !bphi && window == 0) {
         const long long p8 = (P + 7) / 8 * 8;
+        // no more parts than canonical blocks that hold samples (N ≤ 1792 leaves some empty)
+        const long long filled = std::min<long long>(8, (N + 255) / 256);
         for (int gg = 8; gg >= 2 && exact_g == 1; gg >>= 1)
-            if (p8 * gg <= cx->n_cu) exact_g = gg;
+            if (p8 * gg <= cx->n_cu && gg <= filled) exact_g = gg;
         if (const char *e = getenv("GPD_EXACT_G")) {
             const int f = atoi(e);
             if ((f == 1 || f == 2 || f == 4 || f == 8) && p8 * f <= (long long)cx->n_cu) exact_g = f;

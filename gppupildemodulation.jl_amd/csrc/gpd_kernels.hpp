@@ -2139,6 +2139,15 @@ struct ExactChi2 {
         }
         const int nb = CR_BLOCKS / G, b0 = g * nb;
         for (int blk = b0; blk < b0 + nb; ++blk) {
+            if (G == 1 && blk > 0 && s0 + (long long)blk * EXACT_WG >= s1) {
+                // a span of at most blk·256 samples: this block and every later one hold no
+                // sample, so their totals are +0.0; adding +0.0 once does what adding all of
+                // them would (x + 0.0 == x, except −0.0 → +0.0) — the same bits, without the
+                // block reductions of empty blocks (short windows)
+#pragma unroll
+                for (int k = 0; k < NV; ++k) tot[k] = tot[k] + 0.0;
+                break;
+            }
             double acc[NV];
 #pragma unroll
             for (int k = 0; k < NV; ++k) acc[k] = 0.0;
