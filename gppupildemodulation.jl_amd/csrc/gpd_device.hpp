@@ -128,15 +128,51 @@ __host__ __device__ __forceinline__ void bessel_j(double b, double (&J)[KP + 1])
 // lds must hold (WG/64)*NV doubles.  On return every thread holds the same totals.
 // PT: double* or an LDS-qualified pointer (out-of-line callers pass the latter so that the
 // partials go through ds_ instructions, not flat ones)
+// The value of lane (this lane xor OFF) — exactly __shfl_xor(v, OFF, 64), through the cheapest
+// cross-lane path: DPP quad permutes for 1 and 2, ds_swizzle's xor mode within 32-lane halves
+// for 4, 8 and 16, ds_bpermute for 32.  GPD_BS_DPP=0 (A/B builds) keeps __shfl_xor throughout.
+#ifndef GPD_BS_DPP
+#define GPD_BS_DPP 1
+#endif
+template <int OFF>
+__device__ __forceinline__ double lane_xor(double v) {
+#if GPD_BS_DPP
+    if constexpr (OFF <= 16) {
+        const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+        int lo = (int)(unsigned)u, hi = (int)(unsigned)(u >> 32);
+        if constexpr (OFF == 1) {  // quad_perm [1,0,3,2]
+            lo = __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xF, 0xF, false);
+            hi = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xF, 0xF, false);
+        } else if constexpr (OFF == 2) {  // quad_perm [2,3,0,1]
+            lo = __builtin_amdgcn_mov_dpp(lo, 0x4E, 0xF, 0xF, false);
+            hi = __builtin_amdgcn_mov_dpp(hi, 0x4E, 0xF, 0xF, false);
+        } else {  // bit mode: and_mask 0x1F, xor_mask OFF
+            lo = __builtin_amdgcn_ds_swizzle(lo, 0x1F | (OFF << 10));
+            hi = __builtin_amdgcn_ds_swizzle(hi, 0x1F | (OFF << 10));
+        }
+        return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+    }
+#endif
+    return __shfl_xor(v, OFF, 64);
+}
+
 template <int WG, int NV, class PT = double *>
 __device__ __forceinline__ void block_sum(double (&v)[NV], PT lds) {
     constexpr int NW = WG / 64;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // xor butterfly, partners 32, 16, …, 1 (each step adds the partner's value)
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
+    for (int k = 0; k < NV; ++k) v[k] = v[k] + lane_xor<32>(v[k]);
 #pragma unroll
-        for (int k = 0; k < NV; ++k) v[k] = v[k] + __shfl_xor(v[k], off, 64);
-    }
+    for (int k = 0; k < NV; ++k) v[k] = v[k] + lane_xor<16>(v[k]);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = v[k] + lane_xor<8>(v[k]);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = v[k] + lane_xor<4>(v[k]);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = v[k] + lane_xor<2>(v[k]);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = v[k] + lane_xor<1>(v[k]);
     if (NW == 1) return;
     if (lane == 0) {
 #pragma unroll
