@@ -146,3 +146,20 @@ def test_cohort_pipeline_records_bitwise(gpu, monkeypatch, faint, storage):
     gpu.fit_batch(*args, state=st, method="harmonic")
     t = gpu.timings(0)
     assert "fit_tail" in t and t["moments"] > 0, t  # the cohort path ran
+
+
+def test_series_per_fit_wave_does_not_change_records(gpu, monkeypatch):
+    """The harmonic fit packs ⌈P / CUs⌉ series per wave (fit_lanes_for, gpd_engine.hip); every
+    lane runs the same arithmetic whatever its wave holds, so the records are the same bytes for
+    1, 7, 49 and 64 series per wave and for the automatic choice (C2-sized batch and a batch
+    that fills several waves per CU), the exact fallback and the π-flip re-fits included."""
+    for N, P in ((20_000, 32), (8_000, 700)):
+        B = synth.make_batch(N, P, seed=N + P, b_range=(0.3, 5.5))  # b > 4.5: exact fallback
+        args = (B["t"], B["d"], B["fc"], B["fc_of_pixel"])
+        monkeypatch.delenv("GPD_FIT_LANES", raising=False)
+        ref = gpu.fit_batch(*args, method="auto")
+        for lanes in ("1", "7", "49", "64"):
+            monkeypatch.setenv("GPD_FIT_LANES", lanes)
+            _same(gpu.fit_batch(*args, method="auto"), ref)
+        assert np.any(ref["status"] & gpu.GPD_ST_FALLBACK)
+        assert np.mean((ref["status"] & gpu.GPD_ST_EXACT) == 0) > 0.5  # mostly harmonic
