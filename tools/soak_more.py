@@ -8,7 +8,9 @@ bit for bit:
   * faint    — gpd_mean_var_power (m, w per series and state) vs the oracle's
                compute_mean_var_power restatement, random state runs, onlyhigh;
   * shards   — gpd_fit_batch(n_gpus = 2..5) with GPD_FAKE_GPUS=1 (shard g on device g mod 1)
-               vs n_gpus = 1, automatic method, demodulated output included.
+               vs n_gpus = 1, automatic method, demodulated output included;
+  * mixed    — windows × ComplexF32 × faint × fitoffsets × MJD-scale t0 × device shards, exact
+               evaluator, against the oracle per window slice.
 Runs until --seconds have passed; one JSON line per case; exits non-zero on the first failure.
 """
 from __future__ import annotations
@@ -55,12 +57,12 @@ def main():
         return ((oracle.RECENTER if recenter else 0) | (oracle.FIT_OFFSETS if fitoffsets else 0)
                 | (oracle.ONLY_HIGH if onlyhigh else 0))
 
-    counts = {"windows": 0, "c32": 0, "faint": 0, "shards": 0}
+    counts = {"windows": 0, "c32": 0, "faint": 0, "shards": 0, "mixed": 0}
     t_end = time.time() + args.seconds
     case = 0
     while time.time() < t_end:
         case += 1
-        kind = ["windows", "c32", "faint", "shards"][case % 4]
+        kind = ["windows", "c32", "faint", "shards", "mixed"][case % 5]
         t1 = time.time()
         desc = {"case": case, "kind": kind}
         try:
@@ -115,6 +117,32 @@ def main():
                     same = ((m5[k] == rm) | (np.isnan(m5[k]) & np.isnan(rm))) & \
                         ((w5[k] == rw) | (np.isnan(w5[k]) & np.isnan(rw)))
                     assert same.all(), f"{desc}: series {k}: m {m5[k]} vs {rm}, w {w5[k]} vs {rw}"
+            elif kind == "mixed":
+                # windows × ComplexF32 × faint × fitoffsets × MJD-scale t0 × device shards,
+                # exact evaluator, against the oracle per window slice on the widened values
+                N = int(rng.integers(2, 6000))
+                w = int(rng.choice([2, 100, 300, int(rng.integers(2, N + 1))]))
+                C = int(rng.integers(1, 13))
+                t0 = float(rng.choice([0.0, 86400.0 * 60000.5]))
+                B = synth.make_batch(N, C, seed=int(rng.integers(1, 1 << 30)), t0=t0,
+                                     offsets=bool(rng.random() < 0.4))
+                c32 = bool(rng.random() < 0.5)
+                d, fc = B["d"], B["fc"]
+                if c32:
+                    d, fc = d.astype(np.complex64), fc.astype(np.complex64)
+                rec, off = bool(rng.random() < 0.8), bool(rng.random() < 0.4)
+                st, oh = (states(N), bool(rng.random() < 0.4)) if rng.random() < 0.4 else (None, False)
+                ng = int(rng.integers(1, 4))
+                desc.update(N=N, window=w, C=C, t0=t0, c32=c32, faint=st is not None,
+                            fitoffsets=off, n_gpus=ng)
+                got = gpd.fit_windows(B["t"], d, fc, B["fc_of_pixel"], w, state=st, recenter=rec,
+                                      fitoffsets=off, onlyhigh=oh, method="exact", n_gpus=ng)
+                d64, f64 = d.astype(np.complex128), fc.astype(np.complex128)
+                ref = np.stack([oracle.fit_batch(B["t"][I], d64[:, I], f64[:, I], B["fc_of_pixel"],
+                                                 state=None if st is None else st[I],
+                                                 flags=flags(rec, off, oh))
+                                for I in (slice(s0, min(N, s0 + w)) for s0 in range(0, N, w))])
+                assert_exact_bitwise(got.reshape(-1), ref.reshape(-1), label=json.dumps(desc))
             else:
                 N = int(rng.integers(2, 20000))
                 P = int(rng.integers(1, 60))
