@@ -399,8 +399,8 @@ def window_tables(params, n_samples, nwindow, *, fitoffsets=False):
     counts = np.full(nwin, nwindow)
     counts[-1] = n_samples - nwindow * (nwin - 1)
 
-    def per_sample(v):  # (nwin, C) per-window values → (C, N) Float32 rows
-        return np.repeat(v.astype(np.float32), counts, axis=0).T.copy()
+    def per_sample(v):  # (nwin, C) per-window values → (C, N) Float32 rows, one pass
+        return np.repeat(np.ascontiguousarray(v.T, dtype=np.float32), counts, axis=1)
 
     tables = {"ABSA": per_sample(np.abs(params["a"])),
               "ARGA": per_sample(np.angle(params["a"])),
