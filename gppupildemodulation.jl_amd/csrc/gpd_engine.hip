@@ -1194,25 +1194,6 @@ int gpd_process_volt(int64_t n_samples, const double *t, const float *volt, int6
     }
     HIP_TRY(hipSetDevice(device));
     const int64_t nrec = 32 * (window > 0 ? (N + window - 1) / window : 1);
-    double *dt = nullptr;
-    float *dv = nullptr, *dov = nullptr;
-    c64 *dcen = nullptr, *dcplx = nullptr, *dout = nullptr;
-    int8_t *dst = nullptr;
-    int32_t *dfcop = nullptr;
-    Param *dpar = nullptr;
-    hipStream_t s = nullptr;
-    auto cleanup = [&]() {
-        if (s) (void)hipStreamDestroy(s);
-        (void)hipFree(dt);
-        (void)hipFree(dv);
-        (void)hipFree(dov);
-        (void)hipFree(dcen);
-        (void)hipFree(dcplx);
-        (void)hipFree(dout);
-        (void)hipFree(dst);
-        (void)hipFree(dfcop);
-        (void)hipFree(dpar);
-    };
     auto chk = [&](hipError_t e, const char *what) {
         if (e != hipSuccess) {
             set_err(errbuf, errlen, "gpd_process_volt: %s: %s", what, hipGetErrorString(e));
@@ -1222,50 +1203,78 @@ int gpd_process_volt(int64_t n_samples, const double *t, const float *volt, int6
     };
     int32_t fcop[32];
     for (int c = 0; c < 32; ++c) fcop[c] = c / 4;  // idx(side, tel, FC) - 33 for diode column c
-    bool ok = chk(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "stream") &&
-              chk(hipMalloc(&dt, N * sizeof(double)), "malloc t") &&
-              chk(hipMalloc(&dv, (size_t)N * 80 * sizeof(float)), "malloc volt") &&
-              chk(hipMalloc(&dcplx, (size_t)40 * N * sizeof(c64)), "malloc columns") &&
-              chk(hipMalloc(&dfcop, 32 * sizeof(int32_t)), "malloc fcop") &&
-              chk(hipMalloc(&dpar, nrec * sizeof(Param)), "malloc params") &&
-              (!centers || chk(hipMalloc(&dcen, 40 * sizeof(c64)), "malloc centres")) &&
-              (!state || chk(hipMalloc(&dst, N), "malloc state")) &&
-              (!out_volt || (chk(hipMalloc(&dout, (size_t)32 * N * sizeof(c64)), "malloc out") &&
-                             chk(hipMalloc(&dov, (size_t)N * 80 * sizeof(float)), "malloc out volt")));
-    if (!ok) {
-        cleanup();
-        (void)hipGetLastError();
-        return GPD_E_OOM;
-    }
-    ok = chk(hipMemcpyAsync(dt, t, N * sizeof(double), hipMemcpyHostToDevice, s), "H2D t") &&
-         chk(hipMemcpy2DAsync(dv, 80 * sizeof(float), volt, ldv * sizeof(float), 80 * sizeof(float),
-                              N, hipMemcpyHostToDevice, s), "H2D volt") &&
-         chk(hipMemcpyAsync(dfcop, fcop, sizeof fcop, hipMemcpyHostToDevice, s), "H2D fcop") &&
-         (!centers || chk(hipMemcpyAsync(dcen, centers, 40 * sizeof(c64), hipMemcpyHostToDevice, s),
-                          "H2D centres")) &&
-         (!state || chk(hipMemcpyAsync(dst, state, N, hipMemcpyHostToDevice, s), "H2D state"));
-    if (!ok) {
-        cleanup();
+    // the device's grow-only arena and stream of the host-buffer entry points (no hipMalloc /
+    // hipFree / stream creation per exposure); hmu serialises host calls on this device
+    DevCtx *cx = ctx_for(device);
+    std::lock_guard<std::mutex> hlk(cx->hmu);
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off += align_up(bytes);
+        return o;
+    };
+    const size_t o_t = take(N * sizeof(double)), o_v = take((size_t)N * 80 * sizeof(float)),
+                 o_cplx = take((size_t)40 * N * sizeof(c64)), o_fcop = take(32 * sizeof(int32_t)),
+                 o_par = take(nrec * sizeof(Param)), o_cen = take(centers ? 40 * sizeof(c64) : 0),
+                 o_st = take(state ? N : 0),
+                 o_out = take(out_volt ? (size_t)32 * N * sizeof(c64) : 0),
+                 o_ov = take(out_volt ? (size_t)N * 80 * sizeof(float) : 0);
+    if (!cx->hstream && !chk(hipStreamCreateWithFlags(&cx->hstream, hipStreamNonBlocking), "stream"))
         return GPD_E_HIP;
+    hipStream_t s = cx->hstream;
+    if (cx->harena_cap < off) {
+        if (cx->harena) {
+            (void)hipStreamSynchronize(s);
+            (void)hipFree(cx->harena);
+            cx->harena = nullptr;
+            cx->harena_cap = 0;
+        }
+        if (hipMalloc(&cx->harena, off) != hipSuccess) {
+            (void)hipGetLastError();
+            set_err(errbuf, errlen, "gpd_process_volt: device arena of %zu bytes: out of device memory", off);
+            return GPD_E_OOM;
+        }
+        cx->harena_cap = off;
     }
+    char *A = cx->harena;
+    double *dt = (double *)(A + o_t);
+    float *dv = (float *)(A + o_v), *dov = out_volt ? (float *)(A + o_ov) : nullptr;
+    c64 *dcplx = (c64 *)(A + o_cplx), *dcen = centers ? (c64 *)(A + o_cen) : nullptr;
+    c64 *dout = out_volt ? (c64 *)(A + o_out) : nullptr;
+    int32_t *dfcop = (int32_t *)(A + o_fcop);
+    Param *dpar = (Param *)(A + o_par);
+    int8_t *dst = state ? (int8_t *)(A + o_st) : nullptr;
+    // rows of 80 Float32: one linear copy when the caller's rows are contiguous
+    auto copy_rows = [&](void *dst_, size_t dpitch, const void *src, size_t spitch, hipMemcpyKind k) {
+        if (dpitch == spitch)
+            return hipMemcpyAsync(dst_, src, (size_t)N * dpitch, k, s);
+        return hipMemcpy2DAsync(dst_, dpitch, src, spitch, 80 * sizeof(float), N, k, s);
+    };
+    bool ok = chk(hipMemcpyAsync(dt, t, N * sizeof(double), hipMemcpyHostToDevice, s), "H2D t") &&
+              chk(copy_rows(dv, 80 * sizeof(float), volt, ldv * sizeof(float), hipMemcpyHostToDevice),
+                  "H2D volt") &&
+              chk(hipMemcpyAsync(dfcop, fcop, sizeof fcop, hipMemcpyHostToDevice, s), "H2D fcop") &&
+              (!centers || chk(hipMemcpyAsync(dcen, centers, 40 * sizeof(c64), hipMemcpyHostToDevice, s),
+                               "H2D centres")) &&
+              (!state || chk(hipMemcpyAsync(dst, state, N, hipMemcpyHostToDevice, s), "H2D state"));
+    if (!ok) return GPD_E_HIP;
     const unsigned tiles = (unsigned)((N + VT_ROWS - 1) / VT_ROWS);
     k_volt_ingest<<<tiles, 256, 0, s>>>(N, dv, 80, dcen, dcplx, N);
     int r = pipeline_dev(N, 32, dt, (const gpd_c64 *)dcplx, N, (const gpd_c64 *)(dcplx + 32 * N), 8,
                          N, dfcop, dst, omega, xinit, flags, maxfun, (gpd_param *)dpar,
                          (gpd_c64 *)dout, N, nullptr, device, s, errbuf, errlen, window);
     if (r != GPD_OK) {
-        cleanup();
+        (void)hipStreamSynchronize(s);
         return r;
     }
     if (out_volt) k_volt_egress<<<tiles, 256, 0, s>>>(N, dout, dcplx, N, dov, 80);
     ok = chk(hipGetLastError(), "launch") &&
          chk(hipMemcpyAsync(out_params, dpar, nrec * sizeof(Param), hipMemcpyDeviceToHost, s),
              "D2H params") &&
-         (!out_volt || chk(hipMemcpy2DAsync(out_volt, ldov * sizeof(float), dov, 80 * sizeof(float),
-                                            80 * sizeof(float), N, hipMemcpyDeviceToHost, s),
+         (!out_volt || chk(copy_rows(out_volt, ldov * sizeof(float), dov, 80 * sizeof(float),
+                                     hipMemcpyDeviceToHost),
                            "D2H volt")) &&
          chk(hipStreamSynchronize(s), "synchronize");
-    cleanup();
     return ok ? GPD_OK : GPD_E_HIP;
 }
 
