@@ -156,11 +156,10 @@ __device__ __forceinline__ double lane_xor(double v) {
     return __shfl_xor(v, OFF, 64);
 }
 
-template <int WG, int NV, class PT = double *>
-__device__ __forceinline__ void block_sum(double (&v)[NV], PT lds) {
-    constexpr int NW = WG / 64;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // xor butterfly, partners 32, 16, …, 1 (each step adds the partner's value)
+// The wave stage of block_sum: xor butterfly over the 64 lanes, partners 32, 16, …, 1 (each
+// step adds the partner's value); every lane ends with the same total.
+template <int NV>
+__device__ __forceinline__ void wave_sum(double (&v)[NV]) {
 #pragma unroll
     for (int k = 0; k < NV; ++k) v[k] = v[k] + lane_xor<32>(v[k]);
 #pragma unroll
@@ -173,6 +172,13 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], PT lds) {
     for (int k = 0; k < NV; ++k) v[k] = v[k] + lane_xor<2>(v[k]);
 #pragma unroll
     for (int k = 0; k < NV; ++k) v[k] = v[k] + lane_xor<1>(v[k]);
+}
+
+template <int WG, int NV, class PT = double *>
+__device__ __forceinline__ void block_sum(double (&v)[NV], PT lds) {
+    constexpr int NW = WG / 64;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    wave_sum<NV>(v);
     if (NW == 1) return;
     if (lane == 0) {
 #pragma unroll

@@ -51,6 +51,10 @@ void set_err(char *buf, size_t len, const char *fmt, ...) {
 constexpr int kMaxTimers = 40;   // named kernel intervals of the last call
 constexpr int kMaxEv = 96;       // timing events of the last call (both streams)
 constexpr int kMaxCohorts = 16;  // series cohorts of the pipelined harmonic path
+// exact fits of short spans take one wave per series once the series outnumber two 256-thread
+// workgroups per CU (one round of those); below, the 256-thread workgroup's lower latency per
+// evaluation wins (r3: 32 series 0.98 vs 1.56 ms; 16 000 windows 41.6 vs 17.0 ms)
+constexpr long long kOneWaveMinSeriesPerCU = 2;
 
 struct DevCtx {
     int dev = -1;
@@ -800,11 +804,23 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         // one-wave-per-SIMD workgroups; GPD_EXACT_WAVES=1|2 forces it (A/B and tests)
         bool two_waves = exact_g == 1 && (long long)fit_grid * (EXACT_WG / 64) > 4LL * cx->n_cu;
         if (const char *e = getenv("GPD_EXACT_WAVES")) two_waves = atoi(e) == 2 && exact_g == 1;
+        // short spans (every series or window ≤ 256 samples, e.g. windows of < 0.5 s at 500 Hz):
+        // one wave per series (k_fit_exact WGT = 64; the same records), no model cache, a
+        // persistent grid of two waves per SIMD.  GPD_EXACT_WGT=64|256 forces it (A/B, tests).
+        const long long span = window > 0 ? std::min<long long>(window, N) : N;
+        bool one_wave = exact_g == 1 && span <= EXACT_WG &&
+                        P > kOneWaveMinSeriesPerCU * std::max(1, cx->n_cu);
+        if (const char *e = getenv("GPD_EXACT_WGT")) one_wave = exact_g == 1 && atoi(e) == 64;
+        const unsigned grid64 = (unsigned)std::min<long long>(P, 8LL * std::max(1, cx->n_cu));
 #define GPD_LAUNCH_EXACT(FA, OF, PH)                                                                 \
     do {                                                                                        \
         if (bphi)                                                                               \
             k_chi2_exact<FA, OF, PH><<<(unsigned)P, EXACT_WG, 0, stream>>>(pb, info, ph, fstat, \
                                                                            bphi, outp);         \
+        else if (one_wave)                                                                      \
+            k_fit_exact<FA, OF, PH, 2, 64><<<grid64, 64, 0, stream>>>(                         \
+                pb, info, ph, fstat, nullptr, nullptr, outp, raw, 0, nullptr, 0, 1, nullptr,    \
+                nullptr);                                                                       \
         else if (two_waves)                                                                     \
             k_fit_exact<FA, OF, PH, 2><<<fit_grid, EXACT_WG, 0, stream>>>(                    \
                 pb, info, ph, fstat, nullptr, nullptr, outp, raw, 0,                            \

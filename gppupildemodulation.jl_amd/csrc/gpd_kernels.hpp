@@ -31,6 +31,7 @@
 #define GPD_U_FITH 0x2    // unit 1: k_fit_harmonic, k_chi2_harmonic
 #define GPD_U_MOM 0x44    // units 2, 6: k_moments_ws (Float64 / Float32 storage)
 #define GPD_U_EXACT 0xF198  // units 3, 4, 7, 8 / 12-15: k_fit_exact (faint × offsets, MINB 1 / 2)
+#define GPD_U_EXACT64 0xF0000  // units 16-19: k_fit_exact one wave per series (faint × offsets)
 #define GPD_U_CHI2X 0xE20  // units 5, 9, 10, 11: k_chi2_exact, k_refine_exact
 
 namespace gpd {
@@ -1792,8 +1793,11 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
 
 // UR: samples per prefetched batch of the residual pass (the model cache and the series);
-// 8 at two waves per SIMD (C5 exact 339 → 315-320 ms), 4 at one (r2: 2/6/8/16 no better there)
-template <bool FAINT, bool OFFS, bool PHBUF, int UR = CR_UR>
+// 8 at two waves per SIMD (C5 exact 339 → 315-320 ms), 4 at one (r2: 2/6/8/16 no better there).
+// WGT: threads per series — EXACT_WG (256: thread t owns slot t of each canonical block), or 64
+// for short spans (k_fit_exact with WGT = 64: lane l owns the block's slots l, l+64, l+128,
+// l+192 and reduces them as block_sum's four waves would — the same sums, one wave per series).
+template <bool FAINT, bool OFFS, bool PHBUF, int UR = CR_UR, int WGT = EXACT_WG>
 struct ExactChi2 {
     static constexpr bool kOffs = OFFS;
     const Problem *pb;
@@ -2137,6 +2141,33 @@ struct ExactChi2 {
             for (int k = 0; k < NV; ++k) tot[k] = __builtin_nan("");
             return;
         }
+        if constexpr (WGT == 64) {
+            // one wave per series (G = 1): block blk's 256 slots in four quarters of 64 lanes,
+            // each quarter butterflied as block_sum's wave stage, the quarter totals added left
+            // to right as its LDS stage — block_sum<256>'s tree, bit for bit
+            const int lane = (int)threadIdx.x;
+            for (int blk = 0; blk < CR_BLOCKS; ++blk) {
+                if (blk > 0 && s0 + (long long)blk * EXACT_WG >= s1) {  // empty blocks: as below
+#pragma unroll
+                    for (int k = 0; k < NV; ++k) tot[k] = tot[k] + 0.0;
+                    break;
+                }
+                double part[NV];
+#pragma unroll
+                for (int q = 0; q < EXACT_WG / 64; ++q) {
+                    double acc[NV];
+#pragma unroll
+                    for (int k = 0; k < NV; ++k) acc[k] = 0.0;
+                    chain(s0 + blk * EXACT_WG + q * 64 + lane, acc);
+                    wave_sum<NV>(acc);
+#pragma unroll
+                    for (int k = 0; k < NV; ++k) part[k] = (q == 0) ? acc[k] : part[k] + acc[k];
+                }
+#pragma unroll
+                for (int k = 0; k < NV; ++k) tot[k] = (blk == 0) ? part[k] : tot[k] + part[k];
+            }
+            return;
+        }
         const int nb = CR_BLOCKS / G, b0 = g * nb;
         for (int blk = b0; blk < b0 + nb; ++blk) {
             if (G == 1 && blk > 0 && s0 + (long long)blk * EXACT_WG >= s1) {
@@ -2442,8 +2473,11 @@ __device__ __forceinline__ int xpart(long long b, int G) { return (int)((b >> 3)
 // waves, where spills would only cost; 2 (256 registers, two waves per SIMD, spills to scratch)
 // for batches of several rounds, where the second wave hides the first one's latency (C5 exact:
 // 491 → 330 ms; C2 at G = 8: 3.40 → 3.71 ms, profiles/r3/ab_exact).
-template <bool FAINT, bool OFFS, bool PHBUF, int MINB = 1>
-__global__ __launch_bounds__(EXACT_WG, MINB) void k_fit_exact(Problem pb, const Info *__restrict__ info,
+// WGT = 64 (units 16-19): one wave per series for short spans (windows of < 256 samples, where a
+// 256-thread workgroup leaves most threads without a sample): four times the series in flight,
+// NEWUOA run once per series instead of once per wave; the same records (ExactChi2 WGT).
+template <bool FAINT, bool OFFS, bool PHBUF, int MINB = 1, int WGT = EXACT_WG>
+__global__ __launch_bounds__(WGT, MINB) void k_fit_exact(Problem pb, const Info *__restrict__ info,
                                                         const c64 *__restrict__ phbuf,
                                                         const double *__restrict__ fstat,
                                                         const int *__restrict__ list,
@@ -2454,18 +2488,18 @@ __global__ __launch_bounds__(EXACT_WG, MINB) void k_fit_exact(Problem pb, const 
                                                         long long mstride = 0, int G = 1,
                                                         double *__restrict__ xtot = nullptr,
                                                         unsigned *__restrict__ xcnt = nullptr)
-#if GPD_OWNS(GPD_U_EXACT)
+#if GPD_OWNS(GPD_U_EXACT | GPD_U_EXACT64)
 {
     __shared__ double lds[EXACT_LDS];
     // NEWUOA state: one copy per wave in LDS (all lanes of a wave run the same iteration and
     // read/write the same addresses), instead of replicated in every thread's registers
-    __shared__ Newuoa<2, 5, true> nwx[EXACT_WG / 64];
+    __shared__ Newuoa<2, 5, true> nwx[WGT / 64];
     const double nvalid = (double)info->nvalid;
-    if (G > 1) {  // one series per G workgroups (whole exposures, no list)
+    if (WGT == EXACT_WG && G > 1) {  // one series per G workgroups (whole exposures, no list)
         const long long k = xser(blockIdx.x, G);
         if (k >= pb.P) return;  // uniform per series: all its parts leave together
         const int g = xpart(blockIdx.x, G);
-        ExactChi2<FAINT, OFFS, PHBUF, (MINB == 2 ? 8 : CR_UR)> f;
+        ExactChi2<FAINT, OFFS, PHBUF, (MINB == 2 ? 8 : CR_UR), WGT> f;
         setup_exact(f, pb, k, PHBUF ? phbuf : nullptr, lds, nvalid, G, g,
                     Xchg{xtot + k * (2 * CR_BLOCKS * CR_NV), xcnt + k});
         if (mcache) f.mc = mcache + k * mstride;
@@ -2497,7 +2531,7 @@ __global__ __launch_bounds__(EXACT_WG, MINB) void k_fit_exact(Problem pb, const 
     const long long total = list ? (long long)(*count) : pb.P;
     for (long long idx = blockIdx.x; idx < total; idx += gridDim.x) {
         const long long k = list ? (long long)list[idx] : idx;
-        ExactChi2<FAINT, OFFS, PHBUF, (MINB == 2 ? 8 : CR_UR)> f;
+        ExactChi2<FAINT, OFFS, PHBUF, (MINB == 2 ? 8 : CR_UR), WGT> f;
         setup_exact(f, pb, k, PHBUF ? phbuf : nullptr, lds, nvalid);
         if (mcache) f.mc = mcache + (long long)blockIdx.x * mstride;
         if (FAINT) {

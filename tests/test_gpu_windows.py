@@ -137,3 +137,29 @@ def test_demodulate_windows_api(gpu, oracle):
     ref0 = oracle.fit_batch(B["t"][:nw], data[:nw, :32].T, data[:nw].T, fop)
     ok = np.abs(params["b"][0] - ref0["b"]) <= 1e-10 * ref0["b"]
     assert ok.mean() >= 0.7
+
+
+@pytest.mark.parametrize("faint,fitoffsets", [(False, False), (True, False), (False, True)])
+def test_short_windows_one_wave_per_series(gpu, oracle, monkeypatch, faint, fitoffsets):
+    """Windows of < 256 samples are fitted exactly; past two 256-thread workgroups per CU of them
+    the library takes one wave per series (k_fit_exact WGT = 64, which reduces a canonical block
+    as block_sum's four waves would).  Its records equal the 256-thread kernel's byte for byte
+    and the oracle's on every window slice bit for bit (1 200 series of 40 samples, with a
+    ragged last window)."""
+    N, w = 3013, 40
+    B = synth.make_batch(N, 16, seed=77, offsets=fitoffsets)
+    st = faint_states(N, seed=3) if faint else None
+    args = (B["t"], B["d"], B["fc"], B["fc_of_pixel"], w)
+    kw = dict(state=st, fitoffsets=fitoffsets, method="exact")
+    monkeypatch.delenv("GPD_EXACT_WGT", raising=False)
+    auto = gpu.fit_windows(*args, **kw)
+    assert auto.size > 2 * 256  # the one-wave kernel's range on a 256-CU part
+    monkeypatch.setenv("GPD_EXACT_WGT", "256")
+    wg256 = gpu.fit_windows(*args, **kw)
+    assert auto.tobytes() == wg256.tobytes()
+    flags = oracle.RECENTER | (oracle.FIT_OFFSETS if fitoffsets else 0)
+    ref = np.stack([oracle.fit_batch(B["t"][I], B["d"][:, I], B["fc"][:, I], B["fc_of_pixel"],
+                                     state=None if st is None else st[I], flags=flags)
+                    for I in (slice(s0, min(N, s0 + w)) for s0 in range(0, N, w))])
+    print(assert_exact_bitwise(auto.reshape(-1), ref.reshape(-1),
+                               label=f"one wave per series, faint={faint} offsets={fitoffsets}"))
