@@ -804,11 +804,13 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         // one-wave-per-SIMD workgroups; GPD_EXACT_WAVES=1|2 forces it (A/B and tests)
         bool two_waves = exact_g == 1 && (long long)fit_grid * (EXACT_WG / 64) > 4LL * cx->n_cu;
         if (const char *e = getenv("GPD_EXACT_WAVES")) two_waves = atoi(e) == 2 && exact_g == 1;
-        // short spans (every series or window ≤ 256 samples, e.g. windows of < 0.5 s at 500 Hz):
-        // one wave per series (k_fit_exact WGT = 64; the same records), no model cache, a
-        // persistent grid of two waves per SIMD.  GPD_EXACT_WGT=64|256 forces it (A/B, tests).
+        // short spans (every series or window ≤ 2048 samples = one sample per canonical slot,
+        // e.g. windows of ≤ 4 s at 500 Hz): one wave per series (k_fit_exact WGT = 64; the same
+        // records), no model cache, a persistent grid of two waves per SIMD — measured faster
+        // from 100- to 2000-sample windows, slower on 5000 and on whole 1e5-sample series
+        // (DESIGN.md §9).  GPD_EXACT_WGT=64|256 forces it (A/B, tests).
         const long long span = window > 0 ? std::min<long long>(window, N) : N;
-        bool one_wave = exact_g == 1 && span <= EXACT_WG &&
+        bool one_wave = exact_g == 1 && span <= CR_SLOTS &&
                         P > kOneWaveMinSeriesPerCU * std::max(1, cx->n_cu);
         if (const char *e = getenv("GPD_EXACT_WGT")) one_wave = exact_g == 1 && atoi(e) == 64;
         const unsigned grid64 = (unsigned)std::min<long long>(P, 8LL * std::max(1, cx->n_cu));
