@@ -108,6 +108,7 @@ struct Layout {
     long long chunk;    // samples per chunk (a whole number of units)
     int units;          // sample units = partial-moment sets
     long long unit_len; // samples per unit
+    size_t smask, dlist, fixp;  // faint state-split moments (k_moments_ws<FAINT>)
     bool fs1;           // faint statistics in one pass (k_faint_p1/p2/fin), cohorts of fs_pc
     long long fs_pc;    // series per cohort
     int fs_mmax;        // samples per thread and part: ⌈N/2048⌉
@@ -139,12 +140,15 @@ int fit_lanes_for(long long P, int n_cu) {
 }
 
 void moment_grid(long long N, long long P, int n_cu, bool harmonic, bool mfma, int &units,
-                 long long &unit_len, long long &chunk, int &nch) {
+                 long long &unit_len, long long &chunk, int &nch, bool faint = false) {
     const long long per = mfma ? MM_PIX : 64;
     const long long npg = (P + per - 1) / per;
     // at most 26 units: 26 (not 32) makes both the C3 batch (782 groups: 79.4 waves) and its
-    // 8-way shard of 12 500 series (98 groups: 9.95 waves) fill their last wave of workgroups
-    long long umax = 26;
+    // 8-way shard of 12 500 series (98 groups: 9.95 waves) fill their last wave of workgroups.
+    // Faint series (state-split partials, their own records): 32 units, which fill the C5 batch
+    // (32 groups: 4 waves; with 26, 3.25 → a quarter-filled last wave: moments 2.1 → 1.65 ms,
+    // GPD_UNITS A/B, r3) and a faint 1e5 batch (97.75 waves).
+    long long umax = faint ? 32 : 26;
     if (const char *e = getenv("GPD_UNITS")) umax = std::max(1LL, atoll(e));  // A/B only
     long long U = std::min<long long>(umax, std::max<long long>(1, (N + 255) / 256));
     long long ulen = (N + U - 1) / U;
@@ -179,7 +183,7 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
         off += align_up(bytes);
         return o;
     };
-    moment_grid(N, P, n_cu, harmonic, mfma, L.units, L.unit_len, L.chunk, L.nch);
+    moment_grid(N, P, n_cu, harmonic, mfma, L.units, L.unit_len, L.chunk, L.nch, faint);
     const long long U = L.units;
     const long long nch = U;  // partial-moment sets (units)
     L.info = take(sizeof(Info));
@@ -187,7 +191,14 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     // cos/sin table, padded to whole MM_TS-sample tiles (k_table_mix fills the padding)
     L.tab = take(harmonic ? (size_t)((N + MM_TS - 1) / MM_TS * MM_TS) * 2 * KH * sizeof(double) : 0);
     // windowed series: k_moments_win writes mom directly (no partial moments)
-    L.part = take(harmonic && !windowed ? (size_t)nch * NMOM * P * sizeof(double) : 0);
+    // (faint: one slot per unit and state, FST_SLOTS; state masks of the units; the deferred
+    // samples' list and their per-state moments, k_faint_defer / k_moments_fix)
+    const bool fsplit = harmonic && !windowed && faint;
+    L.part = take(harmonic && !windowed
+                      ? (size_t)nch * (fsplit ? FST_SLOTS : 1) * NMOM * P * sizeof(double) : 0);
+    L.smask = take(fsplit ? (size_t)U * sizeof(unsigned) : 0);
+    L.dlist = take(fsplit ? (size_t)(2 * ((N + MM_TS - 1) / MM_TS) + 2) * sizeof(int) : 0);
+    L.fixp = take(fsplit ? (size_t)FST_SLOTS * NMOM * P * sizeof(double) : 0);
     L.mom = take(harmonic ? (size_t)NMOM * P * sizeof(double) : 0);
     L.aux = take((size_t)P * 4 * sizeof(double));
     L.fstat = take(faint ? (size_t)P * 16 * sizeof(double) : 0);
@@ -506,15 +517,28 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         if (const char *e = getenv("GPD_COHORTS")) cohorts = std::max(1, std::min(kMaxCohorts, atoi(e)));
         cohorts = (int)std::min<long long>(cohorts, std::max<long long>(1, P / (2 * MM_PIX)));
     }
+    auto ensure_side = [&]() -> hipError_t {  // the high-priority side stream and its events
+        if (cx->side) return hipSuccess;
+        int lo = 0, hi = 0;
+        hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&cx->side, hipStreamNonBlocking, hi);
+        for (int c = 0; c < kMaxCohorts && e == hipSuccess; ++c)
+            e = hipEventCreateWithFlags(&cx->fork[c], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&cx->join, hipEventDisableTiming);
+        return e;
+    };
+    // faint whole-exposure series on the MFMA kernel: state-split moments (k_moments_ws<FAINT>,
+    // weighted in k_reduce_moments).  GPD_FAINT_SIDE=1 runs the statistics beside the moment
+    // pass on the side stream — measured on C5 (r3): no gain, both passes stream HBM (statistics
+    // 2.57 → 4.5 ms, moments 1.8 → 3.5 ms when overlapped); off by default.
+    const bool fsplit_on = faint && harmonic && use_mfma && window == 0;
+    const bool faint_side = getenv("GPD_FAINT_SIDE") && std::string(getenv("GPD_FAINT_SIDE")) == "1";
+    unsigned *smask = (unsigned *)(ws + L.smask);
+    int *dlist = (int *)(ws + L.dlist);
+    int *dhdr = dlist + 2 * ((N + MM_TS - 1) / MM_TS);
+    double *fixp = (double *)(ws + L.fixp);
     if (cohorts > 1) {
-        if (!cx->side) {
-            int lo = 0, hi = 0;
-            HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-            HIP_TRY(hipStreamCreateWithPriority(&cx->side, hipStreamNonBlocking, hi));
-            for (int c = 0; c < kMaxCohorts; ++c)
-                HIP_TRY(hipEventCreateWithFlags(&cx->fork[c], hipEventDisableTiming));
-            HIP_TRY(hipEventCreateWithFlags(&cx->join, hipEventDisableTiming));
-        }
+        HIP_TRY(ensure_side());
         hipStream_t side = cx->side;
         const bool tm = mix;  // the producer/consumer kernel reads the k_table_mix layout
         if (tm)
@@ -539,7 +563,9 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             else
                 sp.d = pb.d + k0 * ldd;
             sp.fcop = pb.fcop + k0;
-            double *fs_c = fstat + 16 * k0, *part_c = part + (size_t)L.units * NMOM * k0,
+            double *fs_c = fstat + 16 * k0,
+                   *part_c = part + (size_t)L.units * (faint ? FST_SLOTS : 1) * NMOM * k0,
+                   *fix_c = fixp + (size_t)FST_SLOTS * NMOM * k0,
                    *mom_c = mom + (size_t)NMOM * k0, *aux_c = aux + 4 * k0, *raw_c = raw + 2 * k0;
             int *list_c = list + k0, *count_c = ccount + c;
             Param *out_c = outp + k0;
@@ -554,16 +580,20 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             }
             int units, nch;
             long long ulen, chunk;
-            moment_grid(N, n, cx->n_cu, true, true, units, ulen, chunk, nch);
+            moment_grid(N, n, cx->n_cu, true, true, units, ulen, chunk, nch, faint);
             dim3 g((unsigned)((n + MM_PIX - 1) / MM_PIX), (unsigned)nch);
+            if (faint && c == 0) {
+                k_faint_defer<<<1, 1024, 0, stream>>>(pb, dlist, dhdr);
+                mark("faint_defer");
+            }
             if (faint && is_c32 && tm)
-                k_moments_ws<0, false, c32, 2, true, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, fs_c);
+                k_moments_ws<0, false, c32, 2, true, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, smask);
             else if (faint && tm)
-                k_moments_ws<0, false, c64, 2, true, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, fs_c);
+                k_moments_ws<0, false, c64, 2, true, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, smask);
             else if (faint && is_c32)
-                k_moments_ws<0, false, c32, 2, false, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, fs_c);
+                k_moments_ws<0, false, c32, 2, false, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, smask);
             else if (faint)
-                k_moments_ws<0, false, c64, 2, false, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, fs_c);
+                k_moments_ws<0, false, c64, 2, false, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, smask);
             else if (!tm && is_c32)
                 k_moments_ws<0, false, c32, 2, false><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c);
             else if (!tm)
@@ -573,9 +603,13 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             else
                 k_moments_ws<0, false, c64, 2><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c);
             mark("moments");
+            if (faint) {
+                k_moments_fix<<<(unsigned)std::min<long long>(n, 1024), 256, 0, stream>>>(sp, dlist, dhdr, fix_c);
+                mark("moments_fix");
+            }
             dim3 gr((unsigned)((n + 255) / 256), (unsigned)NMOM);
-            k_reduce_moments<<<gr, 256, 0, stream>>>(part_c, units, n, info, fs_c, faint ? 1 : 0,
-                                                     mom_c, aux_c);
+            k_reduce_moments<<<gr, 256, 0, stream>>>(part_c, units, n, info, fs_c, faint ? 2 : 0,
+                                                     mom_c, aux_c, smask, fix_c, dhdr);
             mark("reduce");
             // the cohort's fit on the side stream, after its moments
             HIP_TRY(hipEventRecord(cx->fork[c], stream));
@@ -603,13 +637,27 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         // GPD_FAINT_STATS=2 forces the two-pass kernel (tests of that identity)
         const bool fs1 = L.fs1 && !(getenv("GPD_FAINT_STATS") &&
                                     std::string(getenv("GPD_FAINT_STATS")) == "2");
-        if (fs1) {
-            HIP_TRY(run_faint_onepass(pb, fstat, (double *)(ws + L.fsx), (double *)(ws + L.fsc),
-                                      L.fs_pc, L.fs_mmax, is_c32, stream));
+        auto run_stats = [&](hipStream_t s) -> hipError_t {
+            if (fs1)
+                return run_faint_onepass(pb, fstat, (double *)(ws + L.fsx),
+                                         (double *)(ws + L.fsc), L.fs_pc, L.fs_mmax, is_c32, s);
+            k_faint_stats<<<(unsigned)P, 256, 0, s>>>(pb, fstat);
+            return hipGetLastError();
+        };
+        if (fsplit_on && faint_side) {
+            // the state-split moment pass does not read the statistics: they run beside it
+            // on the side stream and join before the reduction
+            HIP_TRY(ensure_side());
+            HIP_TRY(hipEventRecord(cx->fork[0], stream));
+            HIP_TRY(hipStreamWaitEvent(cx->side, cx->fork[0], 0));
+            const int b0 = rec(cx->side);
+            HIP_TRY(run_stats(cx->side));
+            mark_on(cx->side, b0, "faint_stats");
+            HIP_TRY(hipEventRecord(cx->join, cx->side));
         } else {
-            k_faint_stats<<<(unsigned)P, 256, 0, stream>>>(pb, fstat);
+            HIP_TRY(run_stats(stream));
+            mark("faint_stats");
         }
-        mark("faint_stats");
     }
     const unsigned exact_grid = (unsigned)std::min<long long>(P, 1024);
     bool tmix = false;  // the table holds the k_table_mix layout
@@ -635,14 +683,18 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             mark("moments_win");
         } else if (use_mfma) {
             dim3 g((unsigned)((P + MM_PIX - 1) / MM_PIX), (unsigned)L.nch);
-            if (faint && is_c32 && tmix)  // faint series: the producer/consumer kernel, weighted
-                k_moments_ws<0, false, c32, 2, true, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, fstat);
+            if (faint) {  // the deferred samples of the state-split pass (usually none)
+                k_faint_defer<<<1, 1024, 0, stream>>>(pb, dlist, dhdr);
+                mark("faint_defer");
+            }
+            if (faint && is_c32 && tmix)  // faint series: the producer/consumer kernel, state-split
+                k_moments_ws<0, false, c32, 2, true, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, smask);
             else if (faint && tmix)
-                k_moments_ws<0, false, c64, 2, true, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, fstat);
+                k_moments_ws<0, false, c64, 2, true, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, smask);
             else if (faint && is_c32)
-                k_moments_ws<0, false, c32, 2, false, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, fstat);
+                k_moments_ws<0, false, c32, 2, false, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, smask);
             else if (faint)
-                k_moments_ws<0, false, c64, 2, false, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, fstat);
+                k_moments_ws<0, false, c64, 2, false, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, smask);
             else if (!tmix && is_c32)  // all-f64 MFMA variants (GPD_MIX=0)
                 k_moments_ws<0, false, c32, 2, false><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
             else if (!tmix)
@@ -684,9 +736,15 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         }
         if (window == 0) {
             mark("moments");
+            if (fsplit_on) {
+                k_moments_fix<<<(unsigned)std::min<long long>(P, 1024), 256, 0, stream>>>(pb, dlist, dhdr, fixp);
+                mark("moments_fix");
+                if (faint_side) HIP_TRY(hipStreamWaitEvent(stream, cx->join, 0));  // statistics
+            }
             dim3 gr((unsigned)((P + 255) / 256), (unsigned)NMOM);
-            k_reduce_moments<<<gr, 256, 0, stream>>>(part, L.units, P, info, fstat, faint ? 1 : 0,
-                                                     mom, aux);
+            k_reduce_moments<<<gr, 256, 0, stream>>>(part, L.units, P, info, fstat,
+                                                     fsplit_on ? 2 : (faint ? 1 : 0), mom, aux,
+                                                     smask, fixp, dhdr);
             mark("reduce");
         }
         double *momG = (double *)(ws + L.momG), *d0 = (double *)(ws + L.d0);

@@ -950,6 +950,13 @@ constexpr int MM_GRP = MM_PIX / 4; // FC groups per workgroup
 
 __device__ __forceinline__ int mm_phys(int p, int s) { return s * MM_ROW + (p ^ ((s & 1) << 3)); }
 
+// State-split faint moments: one partial slot per valid MetState code (OFF, LOW, NORMAL, HIGH =
+// 0..3, src/Faint.jl:1); TRANSIENT (-1) and onlyhigh's excluded states contribute nothing.
+constexpr int FST_SLOTS = 4;
+__device__ __forceinline__ bool fst_valid(unsigned flags, int st) {
+    return st >= 0 && st < FST_SLOTS && (!(flags & F_ONLY_HIGH) || st == 3 || st == 2);
+}
+
 // One complex element of storage type TS (c64: 16 B, c32: 8 B) through a buffer descriptor;
 // kept in its storage type until staged (widening at the load would wait on it there).
 // POL: cache policy bits of the load (0 default, 2 = nt: streamed once, no MALL allocation).
@@ -1015,10 +1022,18 @@ __device__ __forceinline__ void split_bf16x2(float f0, float f1, unsigned &h, un
     l = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf16x2));
 }
 
-// FAINT: q = w·m p̄ d with the per-series, per-state weight w and power m of
-// compute_mean_var_power (fstat, src/Faint.jl:89-100; src/Modulation.jl:392-396); samples
-// outside the valid mask (TRANSIENT, or not HIGH/NORMAL with onlyhigh: src/Modulation.jl:373-382)
-// contribute 0.  The state byte of each sample is loaded with the tile.
+// FAINT (state-split moments, r3): the weighted moments Σ w_s m_s p̄ d e^{-jnx} of a faint
+// series (compute_mean_var_power's per-state weight w and power m, src/Faint.jl:89-100;
+// src/Modulation.jl:392-396) are linear in the per-state constant w_s·m_s, so the kernel sums
+// the unweighted q = p̄ d per (unit, state) and k_reduce_moments applies w_s·m_s — the moment
+// pass does not wait for the faint statistics, which run beside it on a second stream.  Each
+// 32-sample tile is given one state: that of its first valid sample (samples outside the valid
+// mask — TRANSIENT, or not HIGH/NORMAL with onlyhigh, src/Modulation.jl:373-382 — contribute
+// 0); the accumulators are flushed into part[unit][state] whenever the tile state changes and
+// at the unit end (adding to the slot when a state recurs within a unit), smask[unit] records
+// the slots written.  A valid sample whose state differs from its tile's (two valid states
+// within 32 samples, which buildstates' TRANSIENT margins never produce) is left to
+// k_moments_fix.  Tiles with no valid sample skip the MFMAs.
 // Sample units: the samples are cut into fixed units of unit_len samples (a function of N only,
 // plan() in gpd_engine.hip) and the consumers write one set of partial moments per unit,
 // part[unit][moment][series], restarting their accumulators at each unit boundary; a workgroup
@@ -1030,13 +1045,13 @@ template <int DBG = 0, bool UNIT = false, class TS = c64, int POL = 0, bool MIX 
 __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double *__restrict__ tab,
                                                        long long chunk_len, long long unit_len,
                                                        double *__restrict__ part,
-                                                       const double *__restrict__ fstat = nullptr)
+                                                       unsigned *__restrict__ smask = nullptr)
 #if GPD_OWNS(GPD_U_MOM)
 {
     __shared__ c64 qs[2][MM_TS * MM_ROW];
     __shared__ __attribute__((aligned(16))) double ts[2][MM_TS * 2 * KH];
     __shared__ int fcl[MM_PIX];
-    __shared__ double wml[FAINT ? MM_PIX * 5 : 1];  // FAINT: w·m per series and state
+    __shared__ int tds[2];  // FAINT: the state of the staged tile (-1: no valid sample)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const long long p0 = (long long)blockIdx.x * MM_PIX;
     const long long s_begin = (long long)blockIdx.y * chunk_len;
@@ -1046,11 +1061,6 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
     if (tid < MM_PIX) {
         const long long p = p0 + tid;
         fcl[tid] = p < pb.P ? pb.fcop[p] : 0;
-        if constexpr (FAINT) {
-#pragma unroll
-            for (int q = 0; q < 5; ++q)
-                wml[tid * 5 + q] = p < pb.P ? fstat[p * 16 + 5 + q] * fstat[p * 16 + q] : 0.0;
-        }
     }
     __syncthreads();
     // general layout: some series of the workgroup does not use its 4-group's FC column
@@ -1141,11 +1151,14 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             bool sok = s < s_end;
             const long long sl = s < Nm1 ? s : Nm1;
             c64 *q_out = qs[it & 1];
-            int stc = 0;  // FAINT: index of the sample's state in wml (code + 1)
             if constexpr (FAINT) {
                 const int st = R.st;
-                sok = sok && st != -1 && (!(pb.flags & F_ONLY_HIGH) || st == 3 || st == 2);
-                stc = st + 1;
+                const bool v = sok && fst_valid(pb.flags, st);
+                // lanes l and l + 32 hold the same sample: bits 0..31 are the tile's samples
+                const unsigned b32 = (unsigned)__builtin_amdgcn_ballot_w64(v);
+                const int ds = b32 ? __builtin_amdgcn_readlane(st, __builtin_ctz(b32)) : -1;
+                sok = v && st == ds;
+                if (ptid == 0) tds[it & 1] = ds;
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -1164,11 +1177,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
                         q.re = fma(pj.re, dv.re, pj.im * dv.im);
                         q.im = fma(pj.re, dv.im, -(pj.im * dv.re));
                     }
-                    if constexpr (FAINT) {
-                        const double f = wml[pl * 5 + stc];
-                        q.re = sok ? q.re * f : 0.0;
-                        q.im = sok ? q.im * f : 0.0;
-                    } else if (decltype(partial)::value) {  // rows beyond P read as 0 already
+                    if (FAINT || decltype(partial)::value) {  // rows beyond P read as 0 already
                         q.re = sok ? q.re : 0.0;
                         q.im = sok ? q.im : 0.0;
                     }
@@ -1273,17 +1282,28 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
         const int code = cq == 0 ? (trig == 0 ? 0 : 3) : (trig == 1 ? 1 : 2);
         if (pix < pb.P) base[(long long)(3 + 4 * h + code) * pb.P + pix] = v;
     };
-    auto flush = [&](long long u) {
-        double *base = part + u * NMOM * pb.P;
+    // slot: the unit (FAINT: unit · FST_SLOTS + state); add: the slot already holds a partial
+    // of this unit (FAINT, a state recurring within the unit) — same thread, same element
+    auto flush = [&](long long slot, bool add) {
+        double *base = part + slot * NMOM * pb.P;
+        auto putv = [&](int m, int n, int row, int col, double v) {
+            if (add) {
+                const long long pix = p0 + wave * 32 + m * 8 + (row >> 1);
+                const int cq = row & 1, trig = col & 1, h = n * 8 + (col >> 1);
+                const int code = cq == 0 ? (trig == 0 ? 0 : 3) : (trig == 1 ? 1 : 2);
+                if (pix < pb.P) v += base[(long long)(3 + 4 * h + code) * pb.P + pix];
+            }
+            put(base, m, n, row, col, v);
+        };
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
 #pragma unroll
             for (int n = 0; n < NC; ++n)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) put(base, m, n, fk + 4 * r, fi, acc[m][n][r]);  // f64 D map
+                for (int r = 0; r < 4; ++r) putv(m, n, fk + 4 * r, fi, acc[m][n][r]);  // f64 D map
             if constexpr (MIX) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) put(base, m, 2, 4 * fk + r, fi, (double)acc32[m][r]);  // bf16 D map
+                for (int r = 0; r < 4; ++r) putv(m, 2, 4 * fk + r, fi, (double)acc32[m][r]);  // bf16 D map
             }
         }
 #pragma unroll
@@ -1296,8 +1316,9 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             const double qo = __shfl_xor(q, 1, 64);
             const long long pix = p0 + wave * 32 + m * 8 + ppair;
             if (fk == 0 && pix < pb.P) {
-                base[(long long)comp * pb.P + pix] = f;
-                if (comp == 0) base[2 * pb.P + pix] = q + qo;
+                double *bf = base + (long long)comp * pb.P + pix;
+                *bf = add ? *bf + f : f;
+                if (comp == 0) base[2 * pb.P + pix] = add ? base[2 * pb.P + pix] + (q + qo) : q + qo;
             }
             f0[m] = q2[m] = 0.0;
 #pragma unroll
@@ -1308,11 +1329,25 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
     const long long u_first = s_begin / unit_len;
     __syncthreads();  // tile 0 staged
     unsigned long long cmf = 0, cbar = 0;  // DBG == 6 only
+    int cs = -1;      // FAINT: state of the accumulators (-1: empty)
+    unsigned um = 0;  // FAINT: state slots of the current unit written so far
     // fragments of K-step ks+1 are read from LDS while the MFMAs of K-step ks run
     // (register double buffer; only the first read of each tile waits on LDS latency)
     for (int i = 0; i < ntiles; ++i) {
         const double *qd = (const double *)qs[i & 1];
         const double *tb = ts[i & 1];
+        bool live = true;  // FAINT: the tile holds a valid sample
+        if constexpr (FAINT) {
+            const int ds = __builtin_amdgcn_readfirstlane(tds[i & 1]);
+            live = ds >= 0;
+            if (live && ds != cs) {
+                if (cs >= 0) {
+                    flush((u_first + i / tpu) * FST_SLOTS + cs, (um >> cs) & 1u);
+                    um |= 1u << cs;
+                }
+                cs = ds;
+            }
+        }
         auto ldfrag = [&](int ks, double (&a)[4], double (&b)[NC]) {
             const int k = ks * 4 + fk;
 #pragma unroll
@@ -1336,7 +1371,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
         };
         unsigned long long c0 = 0;
         if constexpr (DBG == 6) c0 = __builtin_amdgcn_s_memtime();
-        if constexpr (DBG != 1) {
+        if (DBG != 1 && live) {
             // MIX: the bf16 B fragments of this tile (hi, lo), and the A fragments gathered
             // over the 8 K-steps — element j of lane l is sample fk + 4j, as in the table
             v4u bh, bl, ah[4], al[4];
@@ -1388,7 +1423,20 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
         }
         __syncthreads();
         if constexpr (DBG == 6) cbar += __builtin_amdgcn_s_memtime() - c1;
-        if ((i + 1) % tpu == 0 || i + 1 == ntiles) flush(u_first + i / tpu);  // uniform
+        if ((i + 1) % tpu == 0 || i + 1 == ntiles) {  // uniform
+            const long long u = u_first + i / tpu;
+            if constexpr (FAINT) {
+                if (cs >= 0) {
+                    flush(u * FST_SLOTS + cs, (um >> cs) & 1u);
+                    um |= 1u << cs;
+                }
+                if (tid == 0) smask[u] = um;  // the same value from every series group
+                cs = -1;
+                um = 0;
+            } else {
+                flush(u, false);
+            }
+        }
     }
     if constexpr (DBG == 6) {
         if (lane == 0) {
@@ -1403,19 +1451,47 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
 
 
 // k_reduce_moments: mom[m][k] = Σ_chunk part[chunk][m][k] (fixed order), plus per-series
-// aux[k] = {W2, DEN, Q2, 0}.
+// aux[k] = {W2, DEN, Q2, 0}.  faint = 2 (state-split moments of k_moments_ws<FAINT>): the
+// partial of unit c and state s is part[c·FST_SLOTS + s] (written where smask[c] has bit s),
+// weighted here by f_s = w_s·m_s of compute_mean_var_power (f_s² for Σ|q|², row 2), units in
+// order, states in order, then k_moments_fix's slots of the deferred samples (fixp, when dhdr
+// counts any; dhdr[1] = their states).  faint = 1: the partials are weighted already.
 __global__ __launch_bounds__(256) void k_reduce_moments(const double *__restrict__ part, int nch,
                                                         long long P, const Info *__restrict__ info,
                                                         const double *__restrict__ fstat, int faint,
                                                         double *__restrict__ mom,
-                                                        double *__restrict__ aux)
+                                                        double *__restrict__ aux,
+                                                        const unsigned *__restrict__ smask = nullptr,
+                                                        const double *__restrict__ fixp = nullptr,
+                                                        const int *__restrict__ dhdr = nullptr)
 #if GPD_OWNS(GPD_U_ENGINE)
 {
     const long long k = (long long)blockIdx.x * 256 + threadIdx.x;
     const int m = blockIdx.y;
     if (k >= P) return;
     double s = 0.0;
-    for (int c = 0; c < nch; ++c) s += part[((long long)c * NMOM + m) * P + k];
+    if (faint == 2) {
+        double f[FST_SLOTS];
+#pragma unroll
+        for (int q = 0; q < FST_SLOTS; ++q) {
+            f[q] = fstat[k * 16 + 6 + q] * fstat[k * 16 + 1 + q];  // w·m of state code q
+            if (m == 2) f[q] *= f[q];
+        }
+        for (int c = 0; c < nch; ++c) {
+            const unsigned um = smask[c];
+#pragma unroll
+            for (int q = 0; q < FST_SLOTS; ++q)
+                if ((um >> q) & 1u) s += f[q] * part[(((long long)c * FST_SLOTS + q) * NMOM + m) * P + k];
+        }
+        if (dhdr[0] > 0) {
+            const unsigned dm = (unsigned)dhdr[1];
+#pragma unroll
+            for (int q = 0; q < FST_SLOTS; ++q)
+                if ((dm >> q) & 1u) s += f[q] * fixp[((long long)q * NMOM + m) * P + k];
+        }
+    } else {
+        for (int c = 0; c < nch; ++c) s += part[((long long)c * NMOM + m) * P + k];
+    }
     mom[(long long)m * P + k] = s;
     if (m == 2) {
         if (faint) {
@@ -1428,6 +1504,169 @@ __global__ __launch_bounds__(256) void k_reduce_moments(const double *__restrict
             aux[4 * k + 2] = s;                    // Σ|q|² = Σ|d|²
         }
         aux[4 * k + 3] = (double)info->nvalid;  // N of the χ² (per series: windows)
+    }
+}
+#else
+;
+#endif
+
+
+// k_faint_defer: the samples the state-split moment pass leaves out — valid samples whose state
+// differs from their 32-sample tile's (the state of its first valid sample) — as a list of
+// (tile, sample bits) pairs in tile order: dlist[2e], dlist[2e + 1], e < dhdr[0]; dhdr[1] = the
+// OR of 1 << state over them.  States depend on the sample only, so the list serves every series
+// (and every shard: the order is that of the tiles).  One workgroup; prefix sums per round of
+// 1024 tiles.
+__global__ __launch_bounds__(1024) void k_faint_defer(Problem pb, int *__restrict__ dlist,
+                                                      int *__restrict__ dhdr)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
+    __shared__ int wcnt[16];
+    __shared__ int sbase;
+    __shared__ unsigned smk;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const long long N = pb.N, nt = (N + MM_TS - 1) / MM_TS;
+    if (tid == 0) {
+        sbase = 0;
+        smk = 0;
+    }
+    __syncthreads();
+    for (long long j0 = 0; j0 < nt; j0 += 1024) {
+        const long long j = j0 + tid;
+        unsigned dm = 0, sm = 0;
+        if (j < nt) {
+            // the tile's 32 state bytes in two 16-B loads when the array is 16-B aligned
+            unsigned w[8];
+            const long long nb = N - j * MM_TS;
+            if (nb >= MM_TS && (((unsigned long long)pb.state) & 15) == 0) {
+                const uint4 *src = (const uint4 *)(pb.state + j * MM_TS);
+                const uint4 a = src[0], b = src[1];
+                w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+                w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+            } else {
+                for (int q = 0; q < 8; ++q) w[q] = 0;
+                for (int s = 0; s < nb; ++s)
+                    w[s >> 2] |= (unsigned)(unsigned char)pb.state[j * MM_TS + s] << (8 * (s & 3));
+            }
+            int ds = -1;
+            for (int s = 0; s < MM_TS; ++s) {
+                if (s >= nb) break;
+                const int st = (int)(signed char)(w[s >> 2] >> (8 * (s & 3)));
+                if (!fst_valid(pb.flags, st)) continue;
+                if (ds < 0) {
+                    ds = st;
+                } else if (st != ds) {
+                    dm |= 1u << s;
+                    sm |= 1u << st;
+                }
+            }
+        }
+        const unsigned long long b = __builtin_amdgcn_ballot_w64(dm != 0);
+        const int before = __builtin_popcountll(b & ((1ull << lane) - 1ull));
+        if (lane == 0) wcnt[wave] = __builtin_popcountll(b);
+        if (sm) atomicOr(&smk, sm);
+        __syncthreads();
+        int off = sbase;
+        for (int w = 0; w < wave; ++w) off += wcnt[w];
+        if (dm) {
+            dlist[2 * (off + before)] = (int)j;
+            dlist[2 * (off + before) + 1] = (int)dm;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int tot = 0;
+            for (int w = 0; w < 16; ++w) tot += wcnt[w];
+            sbase += tot;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        dhdr[0] = sbase;
+        dhdr[1] = (int)smk;
+    }
+}
+#else
+;
+#endif
+
+
+// k_moments_fix: the unweighted moments q = p̄ d of the samples k_faint_defer lists, per state:
+// fixp[(q·NMOM + row)·P + k], the rows of k_moments_ws (Σq, Σ|q|², then A, B, C, D per
+// harmonic; every state of dhdr[1] written, nothing when the list is empty).  One workgroup
+// per series (≤ 1024 workgroups, each looping over series; with an empty list they return at
+// once); thread = (harmonic group hg of 3 harmonics, sample lane sl of 32); lane sl takes
+// sample sl of each listed tile in list order (cos/sin n x by k_table's recurrence), the lanes
+// are reduced by a fixed xor tree.
+__global__ __launch_bounds__(256) void k_moments_fix(Problem pb, const int *__restrict__ dlist,
+                                                     const int *__restrict__ dhdr,
+                                                     double *__restrict__ fixp)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
+    const int cnt = dhdr[0];
+    if (cnt == 0) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int hg = wave * 2 + (lane >> 5), sl = lane & 31;
+    const unsigned smk = (unsigned)dhdr[1];
+    for (long long k = blockIdx.x; k < pb.P; k += gridDim.x)
+    for (int q = 0; q < FST_SLOTS; ++q) {
+        const long long doff = k * pb.ldd, foff = (long long)pb.fcop[k] * pb.ldfc;
+        if (!((smk >> q) & 1u)) continue;
+        double acc[12], f0r = 0.0, f0i = 0.0, w2 = 0.0;
+#pragma unroll
+        for (int c = 0; c < 12; ++c) acc[c] = 0.0;
+        for (int e = 0; e < cnt; ++e) {
+            const unsigned dm = (unsigned)dlist[2 * e + 1];
+            if (!((dm >> sl) & 1u)) continue;
+            const long long i = (long long)dlist[2 * e] * MM_TS + sl;
+            if (gld(pb.state + i) != q) continue;
+            const c64 ph = unit_phasor(fc_at(pb, foff + i));
+            const c64 dv = d_at(pb, doff + i);
+            const double qr = fma(ph.re, dv.re, ph.im * dv.im);
+            const double qi = fma(ph.re, dv.im, -(ph.im * dv.re));
+            double s1, c1;
+            jl_sincos(pb.omega * gld(pb.t + i), &s1, &c1);
+            double cn = c1, sn = s1;
+            for (int n = 1; n <= 3 * hg; ++n) {
+                const double cn1 = cn * c1 - sn * s1;
+                const double sn1 = sn * c1 + cn * s1;
+                cn = cn1;
+                sn = sn1;
+            }
+#pragma unroll
+            for (int h = 0; h < 3; ++h) {
+                acc[4 * h + 0] = fma(qr, cn, acc[4 * h + 0]);
+                acc[4 * h + 1] = fma(qi, sn, acc[4 * h + 1]);
+                acc[4 * h + 2] = fma(qi, cn, acc[4 * h + 2]);
+                acc[4 * h + 3] = fma(qr, sn, acc[4 * h + 3]);
+                const double cn1 = cn * c1 - sn * s1;
+                const double sn1 = sn * c1 + cn * s1;
+                cn = cn1;
+                sn = sn1;
+            }
+            f0r += qr;
+            f0i += qi;
+            w2 = fma(qr, qr, fma(qi, qi, w2));
+        }
+#pragma unroll
+        for (int off = 1; off < 32; off <<= 1) {
+#pragma unroll
+            for (int c = 0; c < 12; ++c) acc[c] += __shfl_xor(acc[c], off, 64);
+            f0r += __shfl_xor(f0r, off, 64);
+            f0i += __shfl_xor(f0i, off, 64);
+            w2 += __shfl_xor(w2, off, 64);
+        }
+        if (sl == 0) {
+            double *o = fixp + (long long)q * NMOM * pb.P + k;
+#pragma unroll
+            for (int h = 0; h < 3; ++h)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) o[(long long)(3 + 4 * (3 * hg + h) + c) * pb.P] = acc[4 * h + c];
+            if (hg == 0) {
+                o[0] = f0r;
+                o[pb.P] = f0i;
+                o[2 * pb.P] = w2;
+            }
+        }
     }
 }
 #else

@@ -264,6 +264,34 @@ def test_faint_single_sample_state_gives_nan(gpu, oracle):
         assert np.all(got["status"] & gpu.GPD_ST_NAN)
 
 
+@pytest.mark.parametrize("onlyhigh", [False, True])
+def test_faint_interleaved_states_harmonic(gpu, oracle, monkeypatch, onlyhigh):
+    """State-split moments (k_moments_ws<FAINT>): valid states that change within a 32-sample
+    tile, with no TRANSIENT margin, leave samples to k_faint_defer / k_moments_fix; runs of
+    1..40 samples put several states in most tiles.  Harmonic fits against the oracle under the
+    tie envelope; the statistics on the side stream or serially give the same records."""
+    N, P = 6000, 32
+    rng = np.random.default_rng(5)
+    st = np.empty(N, np.int8)
+    i = 0
+    while i < N:
+        n = int(rng.integers(1, 41))
+        st[i:i + n] = rng.choice([1, 2, 3, 0], p=[0.3, 0.3, 0.3, 0.1])
+        i += n
+    st[rng.integers(0, N, 60)] = -1
+    B = synth.make_batch(N, P, seed=23)
+    power = np.where(st == 3, 1.1, np.where(st == 1, 0.3, 0.6))
+    B["d"] = B["d"] * power[None, :]
+    ref = oracle_fit(oracle, B, state=st, onlyhigh=onlyhigh)
+    got = fit(gpu, B, state=st, method="harmonic", onlyhigh=onlyhigh)
+    pert = perturbed_runs(oracle, B, ulps=HARM_ULPS, state=st, onlyhigh=onlyhigh)
+    print(assert_fit_parity(got, ref, pert, label=f"faint/interleaved/onlyhigh={onlyhigh}"))
+    monkeypatch.setenv("GPD_FAINT_SIDE", "0")
+    got2 = fit(gpu, B, state=st, method="harmonic", onlyhigh=onlyhigh)
+    for k in ("b", "phi", "chi2"):
+        assert np.array_equal(got[k], got2[k], equal_nan=True), k
+
+
 def test_mjd_timestamps_quantised_harmonic(gpu, oracle):
     """Real exposures use t ≈ 86400·MJD ≈ 5.2e9 s (src/GPPupilDemodulation.jl:139): θ = fl(fl(ωt)+ϕ)
     is quantised at ~3.8e-6 rad; the harmonic path reproduces it by quantising ϕ."""

@@ -51,8 +51,11 @@ def main():
     params = torch.empty((P, 64), dtype=torch.uint8, device=dev)
     err = ctypes.create_string_buffer(512)
     fn = L.gpd_fit_batch_c32_dev if args.c32 else L.gpd_fit_batch_dev
-    out = []
+    out, wall = [], []
+    import time
     for _ in range(args.reps):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
         gpd._lib.check(fn(N, P, t.data_ptr(), d.data_ptr(), N, fc.data_ptr(), G, N,
                           fcop.data_ptr(), std.data_ptr(), gpd.M_2PI, None,
                           gpd.GPD_RECENTER | {"harmonic": gpd.GPD_METHOD_HARMONIC,
@@ -61,10 +64,11 @@ def main():
                           params.data_ptr(),
                           None, N, 0, sptr, err, len(err)), err)
         torch.cuda.synchronize(dev)
+        wall.append(round((time.perf_counter() - t0) * 1e3, 3))
         out.append({k: round(v, 3) for k, v in gpd.timings(0).items()})
     rec = params.cpu().numpy().reshape(-1).view(gpd.PARAM_DTYPE)
     print(json.dumps({"series": P, "samples": N, "c32": args.c32, "method": args.method,
-                      "kernels_ms": out[-1],
+                      "kernels_ms": out[-1], "wall_ms": wall,
                       "faint_stats_ms": [o.get("faint_stats") for o in out],
                       "mean_nfev": round(float(rec["nfev"].mean()), 3)}))
 
