@@ -586,6 +586,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                 k_faint_defer<<<1, 1024, 0, stream>>>(pb, dlist, dhdr);
                 mark("faint_defer");
             }
+            if (faint) k_moments_fix<<<(unsigned)std::min<long long>(n, 1024), 256, 0, stream>>>(sp, dlist, dhdr, fix_c);
             if (faint && is_c32 && tm)
                 k_moments_ws<0, false, c32, 2, true, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, smask);
             else if (faint && tm)
@@ -603,10 +604,6 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             else
                 k_moments_ws<0, false, c64, 2><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c);
             mark("moments");
-            if (faint) {
-                k_moments_fix<<<(unsigned)std::min<long long>(n, 1024), 256, 0, stream>>>(sp, dlist, dhdr, fix_c);
-                mark("moments_fix");
-            }
             dim3 gr((unsigned)((n + 255) / 256), (unsigned)NMOM);
             k_reduce_moments<<<gr, 256, 0, stream>>>(part_c, units, n, info, fs_c, faint ? 2 : 0,
                                                      mom_c, aux_c, smask, fix_c, dhdr);
@@ -685,6 +682,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             dim3 g((unsigned)((P + MM_PIX - 1) / MM_PIX), (unsigned)L.nch);
             if (faint) {  // the deferred samples of the state-split pass (usually none)
                 k_faint_defer<<<1, 1024, 0, stream>>>(pb, dlist, dhdr);
+                k_moments_fix<<<(unsigned)std::min<long long>(P, 1024), 256, 0, stream>>>(pb, dlist, dhdr, fixp);
                 mark("faint_defer");
             }
             if (faint && is_c32 && tmix)  // faint series: the producer/consumer kernel, state-split
@@ -736,11 +734,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         }
         if (window == 0) {
             mark("moments");
-            if (fsplit_on) {
-                k_moments_fix<<<(unsigned)std::min<long long>(P, 1024), 256, 0, stream>>>(pb, dlist, dhdr, fixp);
-                mark("moments_fix");
-                if (faint_side) HIP_TRY(hipStreamWaitEvent(stream, cx->join, 0));  // statistics
-            }
+            if (fsplit_on && faint_side) HIP_TRY(hipStreamWaitEvent(stream, cx->join, 0));  // statistics
             dim3 gr((unsigned)((P + 255) / 256), (unsigned)NMOM);
             k_reduce_moments<<<gr, 256, 0, stream>>>(part, L.units, P, info, fstat,
                                                      fsplit_on ? 2 : (faint ? 1 : 0), mom, aux,
