@@ -1595,8 +1595,8 @@ __global__ __launch_bounds__(1024) void k_faint_defer(Problem pb, int *__restric
 // harmonic; every state of dhdr[1] written, nothing when the list is empty).  One workgroup
 // per series (≤ 1024 workgroups, each looping over series; with an empty list they return at
 // once); thread = (harmonic group hg of 3 harmonics, sample lane sl of 32); lane sl takes
-// sample sl of each listed tile in list order (cos/sin n x by k_table's recurrence), the lanes
-// are reduced by a fixed xor tree.
+// sample sl of each listed tile in list order (cos/sin n x by k_table's recurrence; entries in
+// batches of 4), the lanes are reduced by a fixed xor tree.
 __global__ __launch_bounds__(256) void k_moments_fix(Problem pb, const int *__restrict__ dlist,
                                                      const int *__restrict__ dhdr,
                                                      double *__restrict__ fixp)
@@ -1614,38 +1614,59 @@ __global__ __launch_bounds__(256) void k_moments_fix(Problem pb, const int *__re
         double acc[12], f0r = 0.0, f0i = 0.0, w2 = 0.0;
 #pragma unroll
         for (int c = 0; c < 12; ++c) acc[c] = 0.0;
-        for (int e = 0; e < cnt; ++e) {
-            const unsigned dm = (unsigned)dlist[2 * e + 1];
-            if (!((dm >> sl) & 1u)) continue;
-            const long long i = (long long)dlist[2 * e] * MM_TS + sl;
-            if (gld(pb.state + i) != q) continue;
-            const c64 ph = unit_phasor(fc_at(pb, foff + i));
-            const c64 dv = d_at(pb, doff + i);
-            const double qr = fma(ph.re, dv.re, ph.im * dv.im);
-            const double qi = fma(ph.re, dv.im, -(ph.im * dv.re));
-            double s1, c1;
-            jl_sincos(pb.omega * gld(pb.t + i), &s1, &c1);
-            double cn = c1, sn = s1;
-            for (int n = 1; n <= 3 * hg; ++n) {
-                const double cn1 = cn * c1 - sn * s1;
-                const double sn1 = sn * c1 + cn * s1;
-                cn = cn1;
-                sn = sn1;
+        // entries in batches of 4 with every load issued up front (a list walk one entry at a
+        // time is a chain of dependent loads per entry); the same order of the sums
+        constexpr int EB = 4;
+        for (int e0 = 0; e0 < cnt; e0 += EB) {
+            long long ii[EB];
+            bool ok[EB];
+#pragma unroll
+            for (int u = 0; u < EB; ++u) {
+                const int e = e0 + u;
+                const unsigned dm = e < cnt ? (unsigned)dlist[2 * e + 1] : 0u;
+                ok[u] = (dm >> sl) & 1u;
+                ii[u] = ok[u] ? (long long)dlist[2 * e] * MM_TS + sl : 0;
+            }
+            c64 fv[EB], dvv[EB];
+            double tv[EB];
+#pragma unroll
+            for (int u = 0; u < EB; ++u) {
+                ok[u] = ok[u] && gld(pb.state + ii[u]) == q;
+                fv[u] = fc_at(pb, foff + ii[u]);
+                dvv[u] = d_at(pb, doff + ii[u]);
+                tv[u] = gld(pb.t + ii[u]);
             }
 #pragma unroll
-            for (int h = 0; h < 3; ++h) {
-                acc[4 * h + 0] = fma(qr, cn, acc[4 * h + 0]);
-                acc[4 * h + 1] = fma(qi, sn, acc[4 * h + 1]);
-                acc[4 * h + 2] = fma(qi, cn, acc[4 * h + 2]);
-                acc[4 * h + 3] = fma(qr, sn, acc[4 * h + 3]);
-                const double cn1 = cn * c1 - sn * s1;
-                const double sn1 = sn * c1 + cn * s1;
-                cn = cn1;
-                sn = sn1;
+            for (int u = 0; u < EB; ++u) {
+                if (!ok[u]) continue;
+                const c64 ph = unit_phasor(fv[u]);
+                const c64 dv = dvv[u];
+                const double qr = fma(ph.re, dv.re, ph.im * dv.im);
+                const double qi = fma(ph.re, dv.im, -(ph.im * dv.re));
+                double s1, c1;
+                jl_sincos(pb.omega * tv[u], &s1, &c1);
+                double cn = c1, sn = s1;
+                for (int n = 1; n <= 3 * hg; ++n) {
+                    const double cn1 = cn * c1 - sn * s1;
+                    const double sn1 = sn * c1 + cn * s1;
+                    cn = cn1;
+                    sn = sn1;
+                }
+#pragma unroll
+                for (int h = 0; h < 3; ++h) {
+                    acc[4 * h + 0] = fma(qr, cn, acc[4 * h + 0]);
+                    acc[4 * h + 1] = fma(qi, sn, acc[4 * h + 1]);
+                    acc[4 * h + 2] = fma(qi, cn, acc[4 * h + 2]);
+                    acc[4 * h + 3] = fma(qr, sn, acc[4 * h + 3]);
+                    const double cn1 = cn * c1 - sn * s1;
+                    const double sn1 = sn * c1 + cn * s1;
+                    cn = cn1;
+                    sn = sn1;
+                }
+                f0r += qr;
+                f0i += qi;
+                w2 = fma(qr, qr, fma(qi, qi, w2));
             }
-            f0r += qr;
-            f0i += qi;
-            w2 = fma(qr, qr, fma(qi, qi, w2));
         }
 #pragma unroll
         for (int off = 1; off < 32; off <<= 1) {
