@@ -108,7 +108,7 @@ struct Layout {
     long long chunk;    // samples per chunk (a whole number of units)
     int units;          // sample units = partial-moment sets
     long long unit_len; // samples per unit
-    size_t smask, dlist, fixp;  // faint state-split moments (k_moments_ws<FAINT>)
+    size_t smask, dlist, fixp, ftab;  // faint state-split moments (k_moments_ws<FAINT>)
     bool fs1;           // faint statistics in one pass (k_faint_p1/p2/fin), cohorts of fs_pc
     long long fs_pc;    // series per cohort
     int fs_mmax;        // samples per thread and part: ⌈N/2048⌉
@@ -199,6 +199,7 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     L.smask = take(fsplit ? (size_t)U * sizeof(unsigned) : 0);
     L.dlist = take(fsplit ? (size_t)(2 * ((N + MM_TS - 1) / MM_TS) + 2) * sizeof(int) : 0);
     L.fixp = take(fsplit ? (size_t)FST_SLOTS * NMOM * P * sizeof(double) : 0);
+    L.ftab = take(fsplit ? (size_t)((N + MM_TS - 1) / MM_TS) * MM_TS * 2 * KH * sizeof(double) : 0);
     L.mom = take(harmonic ? (size_t)NMOM * P * sizeof(double) : 0);
     L.aux = take((size_t)P * 4 * sizeof(double));
     L.fstat = take(faint ? (size_t)P * 16 * sizeof(double) : 0);
@@ -536,7 +537,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     unsigned *smask = (unsigned *)(ws + L.smask);
     int *dlist = (int *)(ws + L.dlist);
     int *dhdr = dlist + 2 * ((N + MM_TS - 1) / MM_TS);
-    double *fixp = (double *)(ws + L.fixp);
+    double *fixp = (double *)(ws + L.fixp), *ftab = (double *)(ws + L.ftab);
+    const unsigned ftab_grid = (unsigned)((N + MM_TS - 1) / MM_TS * MM_TS / 256 + 1);
     if (cohorts > 1) {
         HIP_TRY(ensure_side());
         hipStream_t side = cx->side;
@@ -584,9 +586,10 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             dim3 g((unsigned)((n + MM_PIX - 1) / MM_PIX), (unsigned)nch);
             if (faint && c == 0) {
                 k_faint_defer<<<1, 1024, 0, stream>>>(pb, dlist, dhdr);
+                k_fix_table<<<ftab_grid, 256, 0, stream>>>(pb, dlist, dhdr, ftab);
                 mark("faint_defer");
             }
-            if (faint) k_moments_fix<<<(unsigned)std::min<long long>(n, 1024), 256, 0, stream>>>(sp, dlist, dhdr, fix_c);
+            if (faint) k_moments_fix<<<(unsigned)std::min<long long>(n, 1024), 256, 0, stream>>>(sp, dlist, dhdr, ftab, fix_c);
             if (faint && is_c32 && tm)
                 k_moments_ws<0, false, c32, 2, true, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, smask);
             else if (faint && tm)
@@ -682,7 +685,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             dim3 g((unsigned)((P + MM_PIX - 1) / MM_PIX), (unsigned)L.nch);
             if (faint) {  // the deferred samples of the state-split pass (usually none)
                 k_faint_defer<<<1, 1024, 0, stream>>>(pb, dlist, dhdr);
-                k_moments_fix<<<(unsigned)std::min<long long>(P, 1024), 256, 0, stream>>>(pb, dlist, dhdr, fixp);
+                k_fix_table<<<ftab_grid, 256, 0, stream>>>(pb, dlist, dhdr, ftab);
+                k_moments_fix<<<(unsigned)std::min<long long>(P, 1024), 256, 0, stream>>>(pb, dlist, dhdr, ftab, fixp);
                 mark("faint_defer");
             }
             if (faint && is_c32 && tmix)  // faint series: the producer/consumer kernel, state-split

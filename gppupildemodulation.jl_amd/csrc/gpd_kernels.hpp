@@ -1590,15 +1590,48 @@ __global__ __launch_bounds__(1024) void k_faint_defer(Problem pb, int *__restric
 #endif
 
 
+// k_fix_table: cos/sin n x (n = 1..KH, k_table's recurrence) of every sample k_faint_defer
+// lists, once for all series: ftab[(e·32 + sl)·2KH + …] for entry e, sample bit sl.  Launched over
+// every possible entry (⌈N/32⌉·32 threads); threads beyond the list return.
+__global__ __launch_bounds__(256) void k_fix_table(Problem pb, const int *__restrict__ dlist,
+                                                   const int *__restrict__ dhdr,
+                                                   double *__restrict__ ftab)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
+    const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long e = g / MM_TS;
+    const int sl = (int)(g % MM_TS);
+    if (e >= dhdr[0]) return;
+    if (!(((unsigned)dlist[2 * e + 1] >> sl) & 1u)) return;
+    const long long i = (long long)dlist[2 * e] * MM_TS + sl;
+    double s1, c1;
+    jl_sincos(pb.omega * gld(pb.t + i), &s1, &c1);
+    double cn = c1, sn = s1;
+    double *row = ftab + g * (2 * KH);
+    for (int n = 1; n <= KH; ++n) {
+        row[2 * (n - 1)] = cn;
+        row[2 * (n - 1) + 1] = sn;
+        const double cn1 = cn * c1 - sn * s1;
+        const double sn1 = sn * c1 + cn * s1;
+        cn = cn1;
+        sn = sn1;
+    }
+}
+#else
+;
+#endif
+
+
 // k_moments_fix: the unweighted moments q = p̄ d of the samples k_faint_defer lists, per state:
 // fixp[(q·NMOM + row)·P + k], the rows of k_moments_ws (Σq, Σ|q|², then A, B, C, D per
 // harmonic; every state of dhdr[1] written, nothing when the list is empty).  One workgroup
 // per series (≤ 1024 workgroups, each looping over series; with an empty list they return at
 // once); thread = (harmonic group hg of 3 harmonics, sample lane sl of 32); lane sl takes
-// sample sl of each listed tile in list order (cos/sin n x by k_table's recurrence; entries in
-// batches of 4), the lanes are reduced by a fixed xor tree.
+// sample sl of each listed tile in list order (cos/sin n x from k_fix_table; entries in batches
+// of 4), the lanes are reduced by a fixed xor tree.
 __global__ __launch_bounds__(256) void k_moments_fix(Problem pb, const int *__restrict__ dlist,
                                                      const int *__restrict__ dhdr,
+                                                     const double *__restrict__ ftab,
                                                      double *__restrict__ fixp)
 #if GPD_OWNS(GPD_U_ENGINE)
 {
@@ -1628,13 +1661,11 @@ __global__ __launch_bounds__(256) void k_moments_fix(Problem pb, const int *__re
                 ii[u] = ok[u] ? (long long)dlist[2 * e] * MM_TS + sl : 0;
             }
             c64 fv[EB], dvv[EB];
-            double tv[EB];
 #pragma unroll
             for (int u = 0; u < EB; ++u) {
                 ok[u] = ok[u] && gld(pb.state + ii[u]) == q;
                 fv[u] = fc_at(pb, foff + ii[u]);
                 dvv[u] = d_at(pb, doff + ii[u]);
-                tv[u] = gld(pb.t + ii[u]);
             }
 #pragma unroll
             for (int u = 0; u < EB; ++u) {
@@ -1643,25 +1674,14 @@ __global__ __launch_bounds__(256) void k_moments_fix(Problem pb, const int *__re
                 const c64 dv = dvv[u];
                 const double qr = fma(ph.re, dv.re, ph.im * dv.im);
                 const double qi = fma(ph.re, dv.im, -(ph.im * dv.re));
-                double s1, c1;
-                jl_sincos(pb.omega * tv[u], &s1, &c1);
-                double cn = c1, sn = s1;
-                for (int n = 1; n <= 3 * hg; ++n) {
-                    const double cn1 = cn * c1 - sn * s1;
-                    const double sn1 = sn * c1 + cn * s1;
-                    cn = cn1;
-                    sn = sn1;
-                }
+                const double *row = ftab + ((long long)(e0 + u) * MM_TS + sl) * (2 * KH) + 6 * hg;
 #pragma unroll
                 for (int h = 0; h < 3; ++h) {
+                    const double cn = row[2 * h], sn = row[2 * h + 1];
                     acc[4 * h + 0] = fma(qr, cn, acc[4 * h + 0]);
                     acc[4 * h + 1] = fma(qi, sn, acc[4 * h + 1]);
                     acc[4 * h + 2] = fma(qi, cn, acc[4 * h + 2]);
                     acc[4 * h + 3] = fma(qr, sn, acc[4 * h + 3]);
-                    const double cn1 = cn * c1 - sn * s1;
-                    const double sn1 = sn * c1 + cn * s1;
-                    cn = cn1;
-                    sn = sn1;
                 }
                 f0r += qr;
                 f0i += qi;
