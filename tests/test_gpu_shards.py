@@ -163,3 +163,48 @@ def test_series_per_fit_wave_does_not_change_records(gpu, monkeypatch):
             _same(gpu.fit_batch(*args, method="auto"), ref)
         assert np.any(ref["status"] & gpu.GPD_ST_FALLBACK)
         assert np.mean((ref["status"] & gpu.GPD_ST_EXACT) == 0) > 0.5  # mostly harmonic
+
+
+def test_faint_state_pointer_alignment(gpu):
+    """The state-split faint moments read each tile's 32 state bytes in 16-B loads only when the
+    caller's state array is 16-B aligned (k_faint_defer); a state view at an odd byte offset
+    takes the byte path and must give the same records, bit for bit (device buffers)."""
+    import ctypes
+    import torch
+    L = gpu.load()
+    dev = torch.device("cuda", 0)
+    sptr = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    N, P = 20_000, 64
+    t = torch.empty(N, dtype=torch.float64, device=dev)
+    d = torch.empty((P, N, 2), dtype=torch.float64, device=dev)
+    fc = torch.empty((P // 4, N, 2), dtype=torch.float64, device=dev)
+    fcop = torch.empty(P, dtype=torch.int32, device=dev)
+    gpu._lib.check(L.gpd_synth_fill_dev(N, P, 0, 9, 0.0, 0.002, 0.1, 0, gpu.M_2PI, t.data_ptr(),
+                                        d.data_ptr(), N, fc.data_ptr(), N, fcop.data_ptr(), None,
+                                        0, sptr))
+    rng = np.random.default_rng(3)
+    st = np.empty(N, np.int8)
+    i = 0
+    while i < N:  # runs of 1..60 samples: most tiles hold several valid states
+        n = int(rng.integers(1, 61))
+        st[i:i + n] = rng.choice([-1, 1, 2, 3], p=[0.1, 0.3, 0.3, 0.3])
+        i += n
+    err = ctypes.create_string_buffer(512)
+
+    def fit(state_dev):
+        out = torch.empty((P, 64), dtype=torch.uint8, device=dev)
+        gpu._lib.check(L.gpd_fit_batch_dev(N, P, t.data_ptr(), d.data_ptr(), N, fc.data_ptr(),
+                                           P // 4, N, fcop.data_ptr(), state_dev.data_ptr(),
+                                           gpu.M_2PI, None, gpu.GPD_RECENTER, 60, out.data_ptr(),
+                                           None, N, 0, sptr, err, len(err)), err)
+        torch.cuda.synchronize(dev)
+        return out.cpu().numpy().reshape(-1).view(gpu.PARAM_DTYPE)
+
+    aligned = torch.from_numpy(st).to(dev)
+    buf = torch.zeros(N + 16, dtype=torch.int8, device=dev)
+    odd = buf[3:3 + N]
+    odd.copy_(aligned)
+    assert odd.data_ptr() % 16 == 3
+    a, b = fit(aligned), fit(odd)
+    _same(b, a)
+    assert not np.all(a["status"] & gpu.GPD_ST_NAN)
