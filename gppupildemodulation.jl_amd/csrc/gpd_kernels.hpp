@@ -249,30 +249,13 @@ __global__ __launch_bounds__(1024) void k_prepare(Problem pb, Info *info)
 {
     __shared__ double red[16 * 3];
     double cnt = 0.0, xmn = 1.0e308, xmx = 0.0;
-    // 8 samples per thread and round with every load issued first (a sample at a time left the
-    // scan latency-bound); the count is exact and min / max do not depend on the order
-    constexpr int PU = 8;
-    for (long long i0 = threadIdx.x; i0 < pb.N; i0 += 1024LL * PU) {
-        double tv[PU];
-        int sv[PU];
-#pragma unroll
-        for (int u = 0; u < PU; ++u) {
-            const long long i = i0 + 1024LL * u;
-            const long long ic = i < pb.N ? i : 0;
-            tv[u] = gld(pb.t + ic);
-            sv[u] = pb.state ? (int)gld(pb.state + ic) : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < PU; ++u) {
-            const int st = sv[u];
-            bool ok = i0 + 1024LL * u < pb.N;
-            if (pb.state) ok = ok && st != -1 && (!(pb.flags & F_ONLY_HIGH) || st == 3 || st == 2);
-            if (!ok) continue;
-            const double x = fabs(pb.omega * tv[u]);
-            cnt += 1.0;
-            xmn = fmin(xmn, x);
-            xmx = fmax(xmx, x);
-        }
+    for (long long i = threadIdx.x; i < pb.N; i += 1024) {
+        int st;
+        if (!sample_valid(pb, i, st)) continue;
+        const double x = fabs(pb.omega * gld(pb.t + i));
+        cnt += 1.0;
+        xmn = fmin(xmn, x);
+        xmx = fmax(xmx, x);
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
