@@ -49,7 +49,7 @@ EXPORTS = ("gpd_version", "gpd_strerror", "gpd_device_count", "gpd_fit_batch",
            "gpd_synth_fill_dev", "gpd_last_timings", "gpd_fit_windows", "gpd_fit_windows_dev",
            "gpd_process_volt", "gpd_fit_batch_c32", "gpd_fit_batch_c32_dev", "gpd_fit_windows_c32",
            "gpd_fit_windows_c32_dev", "gpd_buildstates_dev", "gpd_release", "gpd_libm_eval",
-           "gpd_mean_var_power")
+           "gpd_mean_var_power", "gpd_build_id", "gpd_last_faint_stats")
 
 
 class GpdError(RuntimeError):
@@ -117,6 +117,10 @@ def load():
                                      ctypes.c_size_t]
     L.gpd_libm_eval.restype = ctypes.c_int
     L.gpd_libm_eval.argtypes = [ctypes.c_int, I64, V, V, V, ctypes.c_int]
+    L.gpd_build_id.restype = ctypes.c_char_p
+    L.gpd_build_id.argtypes = []
+    L.gpd_last_faint_stats.restype = ctypes.c_int
+    L.gpd_last_faint_stats.argtypes = [ctypes.c_int, V, I64]
     L.gpd_last_timings.restype = ctypes.c_int
     L.gpd_last_timings.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                    ctypes.POINTER(ctypes.c_double), ctypes.c_int]
@@ -155,6 +159,19 @@ def libm_eval(fn: str, x, y=None, device: int = 0):
     out = np.empty(x.size * width)
     check(load().gpd_libm_eval(code, x.size, ptr(x), ptr(yy), ptr(out), device))
     return out.reshape(-1, width) if width > 1 else out
+
+
+def build_id() -> str:
+    """Id of the sources the loaded library was built from (build.tree_id at build time)."""
+    return load().gpd_build_id().decode()
+
+
+def last_faint_stats(n_series: int, device: int = 0):
+    """The faint statistics the last fit call on `device` used (gpd_last_faint_stats): m and w
+    as (n, 5) arrays indexed by MetState code + 1, and (n, 3) [Σw|d|², Σw m² n, Σ(w m)²|d|²]."""
+    out = np.empty((n_series, 16))
+    check(load().gpd_last_faint_stats(device, ptr(out), n_series))
+    return out[:, :5], out[:, 5:10], out[:, 10:13]
 
 
 def timings(device: int = 0):

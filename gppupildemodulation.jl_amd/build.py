@@ -27,14 +27,42 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          "-ffp-contract=off", "-Wall", "-Wno-unused-function"]
 
 
+def tree_id() -> str:
+    """Build id of the sources in this tree: sha256 (first 16 hex digits) over the contents of
+    every translation unit and header, include/gpdemod.h, and the compiler flags — compiled into
+    the library (gpd_build_id) so that a run can show which sources its .so was built from."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in sorted(SOURCES + HEADERS):
+        h.update(f.encode() + b"\0")
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    with open(os.path.join(HERE, "..", "include", "gpdemod.h"), "rb") as fh:
+        h.update(fh.read())
+    h.update(" ".join(FLAGS).encode())
+    return h.hexdigest()[:16]
+
+
+ID_MARKER = b"GPD_BUILD_ID="
+
+
+def lib_id(path: str) -> str | None:
+    """The build id embedded in a built library (read from its bytes, without loading it)."""
+    try:
+        with open(path, "rb") as fh:
+            data = fh.read()
+    except OSError:
+        return None
+    i = data.find(ID_MARKER)
+    if i < 0:
+        return None
+    return data[i + len(ID_MARKER):i + len(ID_MARKER) + 16].decode(errors="replace")
+
+
 def _stale(out: str) -> bool:
-    if not os.path.exists(out):
-        return True
-    t = os.path.getmtime(out)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
-    deps.append(os.path.join(HERE, "..", "include", "gpdemod.h"))
-    deps.append(os.path.abspath(__file__))
-    return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
+    # content, not mtimes: a library whose embedded id differs from the tree's is rebuilt
+    return not os.path.exists(out) or lib_id(out) != tree_id()
 
 
 def build(force: bool = False, verbose: bool = False, diag: bool = False, jobs: int = 0,
@@ -51,6 +79,7 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, jobs: 
     objdir = os.path.join(HERE, "build", variant or ("diag" if diag else "release"))
     os.makedirs(objdir, exist_ok=True)
     extra = (["-DGPD_DIAG"] if diag else []) + [f"-D{d}" for d in defines] + list(flags)
+    extra.append(f'-DGPD_BUILD_ID="{tree_id()}"')
     jobs = jobs or max(1, min(len(SOURCES), os.cpu_count() or 1))
     procs, objs, errs = [], [], []
     pending = [u for u in SOURCES if not only or u in only]

@@ -83,6 +83,9 @@ struct DevCtx {
     char *harena = nullptr;
     size_t harena_cap = 0;
     hipStream_t hstream = nullptr;
+    // the last fit call's faint statistics in the workspace (gpd_last_faint_stats; tests)
+    const double *last_fstat = nullptr;
+    long long last_fstat_P = 0;
 };
 
 std::mutex g_mu;
@@ -109,6 +112,7 @@ struct Layout {
     int units;          // sample units = partial-moment sets
     long long unit_len; // samples per unit
     size_t smask, dlist, fixp, ftab;  // faint state-split moments (k_moments_ws<FAINT>)
+    size_t fsp, fcnt, fixs;           // fused faint statistics (k_moments_ws<FAINT> producers)
     bool fs1;           // faint statistics in one pass (k_faint_p1/p2/fin), cohorts of fs_pc
     long long fs_pc;    // series per cohort
     int fs_mmax;        // samples per thread and part: ⌈N/2048⌉
@@ -197,9 +201,14 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     L.part = take(harmonic && !windowed
                       ? (size_t)nch * (fsplit ? FST_SLOTS : 1) * NMOM * P * sizeof(double) : 0);
     L.smask = take(fsplit ? (size_t)U * sizeof(unsigned) : 0);
-    L.dlist = take(fsplit ? (size_t)(2 * ((N + MM_TS - 1) / MM_TS) + 2) * sizeof(int) : 0);
+    L.dlist = take(fsplit ? (size_t)(2 * ((N + MM_TS - 1) / MM_TS) + 6) * sizeof(int) : 0);
     L.fixp = take(fsplit ? (size_t)FST_SLOTS * NMOM * P * sizeof(double) : 0);
     L.ftab = take(fsplit ? (size_t)((N + MM_TS - 1) / MM_TS) * MM_TS * 2 * KH * sizeof(double) : 0);
+    // fused faint statistics: per (unit, state) slot, S1/S2 of the two sample halves per series,
+    // the counts per slot, the deferred samples' (n, S1, S2) per state
+    L.fsp = take(fsplit ? (size_t)nch * FST_SLOTS * 4 * P * sizeof(double) : 0);
+    L.fcnt = take(fsplit ? (size_t)nch * FST_SLOTS * sizeof(int) : 0);
+    L.fixs = take(fsplit ? (size_t)FST_SLOTS * 3 * P * sizeof(double) : 0);
     L.mom = take(harmonic ? (size_t)NMOM * P * sizeof(double) : 0);
     L.aux = take((size_t)P * 4 * sizeof(double));
     L.fstat = take(faint ? (size_t)P * 16 * sizeof(double) : 0);
@@ -265,6 +274,14 @@ const char *kErrStr[] = {"ok", "invalid argument", "HIP runtime error", "no HIP 
 extern "C" {
 
 int gpd_version(void) { return GPD_ABI_VERSION; }
+
+// build provenance: the tree id build.py computes over the sources and flags (build.tree_id),
+// also kept as a marker string that build.py reads from the library's bytes
+#ifndef GPD_BUILD_ID
+#define GPD_BUILD_ID "unknown"
+#endif
+__attribute__((used)) static const char kBuildIdMarker[] = "GPD_BUILD_ID=" GPD_BUILD_ID;
+const char *gpd_build_id(void) { return kBuildIdMarker + 13; }
 
 const char *gpd_strerror(int code) {
     if (code > 0 || code < -5) return "unknown error";
@@ -434,6 +451,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     double *mom = (double *)(ws + L.mom);
     double *aux = (double *)(ws + L.aux);
     double *fstat = (double *)(ws + L.fstat);
+    cx->last_fstat = faint ? fstat : nullptr;
+    cx->last_fstat_P = faint ? P : 0;
     double *raw = (double *)(ws + L.raw);
     int *list = (int *)(ws + L.list);
     int *count = list + P;
@@ -534,6 +553,15 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     // 2.57 → 4.5 ms, moments 1.8 → 3.5 ms when overlapped); off by default.
     const bool fsplit_on = faint && harmonic && use_mfma && window == 0;
     const bool faint_side = getenv("GPD_FAINT_SIDE") && std::string(getenv("GPD_FAINT_SIDE")) == "1";
+    // the state-split moment pass also forms compute_mean_var_power's sums (k_moments_ws<FAINT>
+    // producers, k_faint_fused_fin): one HBM pass for the faint series (r4).  GPD_FAINT_STATS=1
+    // (one-pass kernels k_faint_p1/p2/fin) or 2 (two-pass kernel) computes the statistics
+    // separately instead — the exact evaluator's statistics, bit for bit the oracle's (A/B and
+    // tests).
+    const char *fse = getenv("GPD_FAINT_STATS");
+    const bool fused = fsplit_on && !(fse && (std::string(fse) == "1" || std::string(fse) == "2"));
+    double *fsp = (double *)(ws + L.fsp), *fixs = (double *)(ws + L.fixs);
+    int *fcnt = (int *)(ws + L.fcnt);
     unsigned *smask = (unsigned *)(ws + L.smask);
     int *dlist = (int *)(ws + L.dlist);
     int *dhdr = dlist + 2 * ((N + MM_TS - 1) / MM_TS);
@@ -568,10 +596,12 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             double *fs_c = fstat + 16 * k0,
                    *part_c = part + (size_t)L.units * (faint ? FST_SLOTS : 1) * NMOM * k0,
                    *fix_c = fixp + (size_t)FST_SLOTS * NMOM * k0,
+                   *fsp_c = fsp + (size_t)L.units * FST_SLOTS * 4 * k0,
+                   *fixs_c = fixs + (size_t)FST_SLOTS * 3 * k0,
                    *mom_c = mom + (size_t)NMOM * k0, *aux_c = aux + 4 * k0, *raw_c = raw + 2 * k0;
             int *list_c = list + k0, *count_c = ccount + c;
             Param *out_c = outp + k0;
-            if (faint) {
+            if (faint && !fused) {
                 if (fs1)
                     HIP_TRY(run_faint_onepass(sp, fs_c, (double *)(ws + L.fsx),
                                               (double *)(ws + L.fsc), L.fs_pc, L.fs_mmax, is_c32,
@@ -589,15 +619,15 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                 k_fix_table<<<ftab_grid, 256, 0, stream>>>(pb, dlist, dhdr, ftab);
                 mark("faint_defer");
             }
-            if (faint) k_moments_fix<<<(unsigned)std::min<long long>(n, 1024), 256, 0, stream>>>(sp, dlist, dhdr, ftab, fix_c);
+            if (faint) k_moments_fix<<<(unsigned)std::min<long long>(n, 1024), 256, 0, stream>>>(sp, dlist, dhdr, ftab, fix_c, fixs_c);
             if (faint && is_c32 && tm)
-                k_moments_ws<0, false, c32, 2, true, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, smask);
+                k_moments_ws<0, false, c32, 2, true, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, smask, fsp_c, fcnt, dhdr);
             else if (faint && tm)
-                k_moments_ws<0, false, c64, 2, true, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, smask);
+                k_moments_ws<0, false, c64, 2, true, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, smask, fsp_c, fcnt, dhdr);
             else if (faint && is_c32)
-                k_moments_ws<0, false, c32, 2, false, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, smask);
+                k_moments_ws<0, false, c32, 2, false, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, smask, fsp_c, fcnt, dhdr);
             else if (faint)
-                k_moments_ws<0, false, c64, 2, false, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, smask);
+                k_moments_ws<0, false, c64, 2, false, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, smask, fsp_c, fcnt, dhdr);
             else if (!tm && is_c32)
                 k_moments_ws<0, false, c32, 2, false><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c);
             else if (!tm)
@@ -607,6 +637,11 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             else
                 k_moments_ws<0, false, c64, 2><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c);
             mark("moments");
+            if (fused) {
+                k_faint_fused_fin<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(
+                    sp, units, fsp_c, fcnt, smask, part_c, fixs_c, fix_c, dhdr, fs_c);
+                mark("faint_stats");
+            }
             dim3 gr((unsigned)((n + 255) / 256), (unsigned)NMOM);
             k_reduce_moments<<<gr, 256, 0, stream>>>(part_c, units, n, info, fs_c, faint ? 2 : 0,
                                                      mom_c, aux_c, smask, fix_c, dhdr);
@@ -631,7 +666,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         HIP_TRY(hipEventRecord(cx->join, side));
         HIP_TRY(hipStreamWaitEvent(stream, cx->join, 0));
         mark("fit_tail");  // the last cohort's fit, exposed
-    } else if (faint) {
+    } else if (faint && !fused) {
         // whole-exposure series: one pass over the series, one hypot per sample (k_faint_p1/p2/
         // fin); windows: the two-pass kernel over each window's span (same bits);
         // GPD_FAINT_STATS=2 forces the two-pass kernel (tests of that identity)
@@ -686,17 +721,17 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             if (faint) {  // the deferred samples of the state-split pass (usually none)
                 k_faint_defer<<<1, 1024, 0, stream>>>(pb, dlist, dhdr);
                 k_fix_table<<<ftab_grid, 256, 0, stream>>>(pb, dlist, dhdr, ftab);
-                k_moments_fix<<<(unsigned)std::min<long long>(P, 1024), 256, 0, stream>>>(pb, dlist, dhdr, ftab, fixp);
+                k_moments_fix<<<(unsigned)std::min<long long>(P, 1024), 256, 0, stream>>>(pb, dlist, dhdr, ftab, fixp, fixs);
                 mark("faint_defer");
             }
             if (faint && is_c32 && tmix)  // faint series: the producer/consumer kernel, state-split
-                k_moments_ws<0, false, c32, 2, true, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, smask);
+                k_moments_ws<0, false, c32, 2, true, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, smask, fsp, fcnt, dhdr);
             else if (faint && tmix)
-                k_moments_ws<0, false, c64, 2, true, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, smask);
+                k_moments_ws<0, false, c64, 2, true, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, smask, fsp, fcnt, dhdr);
             else if (faint && is_c32)
-                k_moments_ws<0, false, c32, 2, false, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, smask);
+                k_moments_ws<0, false, c32, 2, false, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, smask, fsp, fcnt, dhdr);
             else if (faint)
-                k_moments_ws<0, false, c64, 2, false, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, smask);
+                k_moments_ws<0, false, c64, 2, false, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, smask, fsp, fcnt, dhdr);
             else if (!tmix && is_c32)  // all-f64 MFMA variants (GPD_MIX=0)
                 k_moments_ws<0, false, c32, 2, false><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
             else if (!tmix)
@@ -738,7 +773,12 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         }
         if (window == 0) {
             mark("moments");
-            if (fsplit_on && faint_side) HIP_TRY(hipStreamWaitEvent(stream, cx->join, 0));  // statistics
+            if (fused) {
+                k_faint_fused_fin<<<(unsigned)((P + 255) / 256), 256, 0, stream>>>(
+                    pb, L.units, fsp, fcnt, smask, part, fixs, fixp, dhdr, fstat);
+                mark("faint_stats");
+            }
+            if (fsplit_on && faint_side && !fused) HIP_TRY(hipStreamWaitEvent(stream, cx->join, 0));  // statistics
             dim3 gr((unsigned)((P + 255) / 256), (unsigned)NMOM);
             k_reduce_moments<<<gr, 256, 0, stream>>>(part, L.units, P, info, fstat,
                                                      fsplit_on ? 2 : (faint ? 1 : 0), mom, aux,
@@ -1006,6 +1046,18 @@ int gpd_last_timings(int device, const char **names, double *ms, int cap) {
         if (ms) ms[i] = (double)f;
     }
     return n;
+}
+
+int gpd_last_faint_stats(int device, double *out, int64_t n_series) {
+    if (device < 0 || device >= gpd_device_count() || !out || n_series < 1) return GPD_E_ARG;
+    DevCtx *cx = ctx_for(device);
+    std::lock_guard<std::mutex> lk(cx->mu);
+    if (!cx->last_fstat || n_series > cx->last_fstat_P) return GPD_E_ARG;
+    if (hipSetDevice(device) != hipSuccess || hipEventSynchronize(cx->done) != hipSuccess ||
+        hipMemcpy(out, cx->last_fstat, (size_t)n_series * 16 * sizeof(double),
+                  hipMemcpyDeviceToHost) != hipSuccess)
+        return GPD_E_HIP;
+    return GPD_OK;
 }
 
 }  // extern "C"

@@ -956,6 +956,21 @@ constexpr int FST_SLOTS = 4;
 __device__ __forceinline__ bool fst_valid(unsigned flags, int st) {
     return st >= 0 && st < FST_SLOTS && (!(flags & F_ONLY_HIGH) || st == 3 || st == 2);
 }
+// |q| of the fused faint statistics (x = abs(d) through q = p̄ d, |p| = 1): sqrt of the
+// fma-formed |q|² by v_rsq_f64 and one Goldschmidt correction (≤ 1 ulp; no rescaling — |q|²
+// stays far from the subnormal and overflow ranges for metrology voltages; 0 → 0, Inf → NaN).
+// The statistics are a restatement with a stated tolerance (oracle: faint_stats_fused in
+// demod_oracle.c forms the same sums from Julia's hypot), not a bit-for-bit one.
+__device__ __forceinline__ double fs_abs(double re, double im) {
+    const double r2 = fma(re, re, im * im);
+    const double y = __builtin_amdgcn_rsq(r2);
+    double g = r2 * y, h = 0.5 * y;
+    const double r = fma(-g, h, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    g = fma(fma(-g, g, r2), h, g);
+    return r2 == 0.0 ? 0.0 : g;
+}
 
 // One complex element of storage type TS (c64: 16 B, c32: 8 B) through a buffer descriptor;
 // kept in its storage type until staged (widening at the load would wait on it there).
@@ -1045,19 +1060,28 @@ template <int DBG = 0, bool UNIT = false, class TS = c64, int POL = 0, bool MIX 
 __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double *__restrict__ tab,
                                                        long long chunk_len, long long unit_len,
                                                        double *__restrict__ part,
-                                                       unsigned *__restrict__ smask = nullptr)
+                                                       unsigned *__restrict__ smask = nullptr,
+                                                       double *__restrict__ fsp = nullptr,
+                                                       int *__restrict__ fcnt = nullptr,
+                                                       const int *__restrict__ dhdr = nullptr)
 #if GPD_OWNS(GPD_U_MOM)
 {
     __shared__ c64 qs[2][MM_TS * MM_ROW];
     __shared__ __attribute__((aligned(16))) double ts[2][MM_TS * 2 * KH];
     __shared__ int fcl[MM_PIX];
-    __shared__ int tds[2];  // FAINT: the state of the staged tile (-1: no valid sample)
+    __shared__ int tds[2];       // FAINT: the state of the staged tile (-1: no valid sample)
+    __shared__ unsigned tmk[2];  // FAINT: the staged tile's samples of that state (bit = sample)
+    // FAINT: the producer threads' statistics (K, S1, S2) — in the LDS left over (6 KB), not in
+    // registers: the faint producers are at the 256-VGPR limit of two waves per SIMD
+    __shared__ double fsl[FAINT ? 3 : 1][FAINT ? 256 : 1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const long long p0 = (long long)blockIdx.x * MM_PIX;
     const long long s_begin = (long long)blockIdx.y * chunk_len;
     long long s_end = s_begin + chunk_len;
     if (s_end > pb.N) s_end = pb.N;
     const int ntiles = s_end > s_begin ? (int)((s_end - s_begin + MM_TS - 1) / MM_TS) : 0;
+    const int tpu = (int)(unit_len / MM_TS);  // tiles per unit (units are whole tiles)
+    const long long u_first = s_begin / unit_len;
     if (tid < MM_PIX) {
         const long long p = p0 + tid;
         fcl[tid] = p < pb.P ? pb.fcop[p] : 0;
@@ -1097,7 +1121,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             0x00020000);
         const int tvoff = ptid * 16;  // slot e = ptid + 256 u of a tile starting at row s0
 
-        auto issue = [&](WsRegs<TS> &R, int it) {
+        auto issue = [&](WsRegs<TS> &R, int it) __attribute__((always_inline)) {
             if constexpr (DBG == 2 || DBG == 5) {
                 for (int r = 0; r < 4; ++r) {
                     R.f[r] = TS{1.0f + it, 0};
@@ -1133,7 +1157,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
         };
         // cos/sin rows (L2-resident table) one tile ahead in a single register set
         double2 T0, T1, T2;
-        auto issue_t = [&](int it) {
+        auto issue_t = [&](int it) __attribute__((always_inline)) {
             if constexpr (DBG == 2 || DBG == 5) {
                 T0 = T1 = T2 = double2{0.25 * it, 1.0};
                 return;
@@ -1146,7 +1170,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             T2 = __builtin_bit_cast(double2,
                                     __builtin_amdgcn_raw_buffer_load_b128(trs, vo + 8192, 0, 0));
         };
-        auto stage_q = [&](const WsRegs<TS> &R, int it, auto gen, auto partial) {
+        auto stage_q = [&](const WsRegs<TS> &R, int it, auto gen, auto partial) __attribute__((always_inline)) {
             const long long s = s_begin + (long long)it * MM_TS + ss;
             bool sok = s < s_end;
             const long long sl = s < Nm1 ? s : Nm1;
@@ -1158,7 +1182,11 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
                 const unsigned b32 = (unsigned)__builtin_amdgcn_ballot_w64(v);
                 const int ds = b32 ? __builtin_amdgcn_readlane(st, __builtin_ctz(b32)) : -1;
                 sok = v && st == ds;
-                if (ptid == 0) tds[it & 1] = ds;
+                const unsigned okm = (unsigned)__builtin_amdgcn_ballot_w64(sok);
+                if (ptid == 0) {
+                    tds[it & 1] = ds;
+                    tmk[it & 1] = okm;
+                }
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -1185,7 +1213,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
                 }
             }
         };
-        auto stage = [&](const WsRegs<TS> &R, int it, auto gen) {
+        auto stage = [&](const WsRegs<TS> &R, int it, auto gen) __attribute__((always_inline)) {
             if (it >= ntiles) return;
             if constexpr (DBG == 5) return;
             // only a chunk's last tile can be partial (chunks are whole tiles, N may not be)
@@ -1199,6 +1227,89 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             tsb[512] = T2;
         };
 
+        // FAINT: compute_mean_var_power's statistics (src/Faint.jl:89-100) fused into this
+        // pass.  While the consumers run tile i, the producers read tile i back from LDS with
+        // one series per thread (series fs_p, sample half fs_h: waves 4-5 samples 0..15, waves
+        // 6-7 samples 16..31; 16-B rows, conflict-free) and add x = |q| = |p̄ d| (= abs(d), |p| =
+        // 1) of the tile's state-ds samples as shifted sums S1 = Σ(x − K), S2 = Σ(x − K)², K =
+        // abs(d) at the first valid sample of that state (dhdr[2 + s], k_faint_defer) — the
+        // same K for every partial of the series, so the partials add and the variance
+        // M2 = S2 − S1²/n loses only ~(1 + (m − K)²/σ²) ulps (a raw Σx² − (Σx)²/n would lose
+        // m²/σ²).  Flushed per (unit, state) exactly where the consumers flush their moments:
+        // fsp[(slot·4 + 2·fs_h + {0, 1})·P + series], the counts (series-independent) by the
+        // first series group: fcnt[slot].  k_faint_fused_fin merges them in unit order.
+        const int fs_p = ptid & (MM_PIX - 1), fs_h = ptid >> 7;
+        const long long fs_k = p0 + fs_p;
+        if constexpr (FAINT) fsl[0][ptid] = fsl[1][ptid] = fsl[2][ptid] = 0.0;  // K, S1, S2
+        int fs_cs = -1, fs_n = 0;
+        unsigned fs_um = 0;
+        auto fs_flush = [&](long long slot, bool add) __attribute__((always_inline)) {
+            if (fs_k < pb.P) {
+                double *o = fsp + (slot * 4 + 2 * fs_h) * pb.P + fs_k;
+                const double s1 = fsl[1][ptid], s2 = fsl[2][ptid];
+                o[0] = add ? o[0] + s1 : s1;
+                o[pb.P] = add ? o[pb.P] + s2 : s2;
+            }
+            if (blockIdx.x == 0 && ptid == 0) fcnt[slot] = add ? fcnt[slot] + fs_n : fs_n;
+            fsl[1][ptid] = fsl[2][ptid] = 0.0;
+            fs_n = 0;
+        };
+        auto fs_tile = [&](int i) __attribute__((always_inline)) {
+            if constexpr (FAINT && DBG == 0) {
+                const int ds = __builtin_amdgcn_readfirstlane(tds[i & 1]);
+                const unsigned mk = (unsigned)__builtin_amdgcn_readfirstlane((int)tmk[i & 1]);
+                if (ds >= 0 && ds != fs_cs) {  // uniform
+                    if (fs_cs >= 0) {
+                        fs_flush((u_first + i / tpu) * FST_SLOTS + fs_cs, (fs_um >> fs_cs) & 1u);
+                        fs_um |= 1u << fs_cs;
+                    }
+                    fs_cs = ds;
+                    double K = 0.0;
+                    if (fs_k < pb.P) {
+                        const c64 z = d_at(pb, fs_k * pb.ldd + dhdr[2 + ds]);
+                        K = jl_hypot(z.re, z.im);
+                    }
+                    fsl[0][ptid] = K;
+                }
+                if (ds >= 0) {
+                    const double fsK = fsl[0][ptid];
+                    double fsS1 = fsl[1][ptid], fsS2 = fsl[2][ptid];
+                    fs_n += __builtin_popcount(mk);
+                    const unsigned hm = (mk >> (16 * fs_h)) & 0xffffu;  // wave-uniform
+                    const double2 *qt = (const double2 *)qs[i & 1];
+                    if (hm == 0xffffu) {
+#pragma unroll 1
+                        for (int s4 = 0; s4 < 16; s4 += 4) {
+                            double2 qv[4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) qv[u] = qt[mm_phys(fs_p, 16 * fs_h + s4 + u)];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                const double y = fs_abs(qv[u].x, qv[u].y) - fsK;
+                                fsS1 += y;
+                                fsS2 = fma(y, y, fsS2);
+                            }
+                        }
+                    } else {
+                        for (int s = 0; s < 16; ++s) {
+                            if (!((hm >> s) & 1u)) continue;  // uniform
+                            const double2 qv = qt[mm_phys(fs_p, 16 * fs_h + s)];
+                            const double y = fs_abs(qv.x, qv.y) - fsK;
+                            fsS1 += y;
+                            fsS2 = fma(y, y, fsS2);
+                        }
+                    }
+                    fsl[1][ptid] = fsS1;
+                    fsl[2][ptid] = fsS2;
+                }
+                if ((i + 1) % tpu == 0 || i + 1 == ntiles) {  // unit end (uniform)
+                    if (fs_cs >= 0) fs_flush((u_first + i / tpu) * FST_SLOTS + fs_cs, (fs_um >> fs_cs) & 1u);
+                    fs_cs = -1;
+                    fs_um = 0;
+                }
+            }
+        };
+
         // loader waves first: their few VALU ops and the next loads must not queue behind the
         // MFMA stream of the consumer wave on the same SIMD (fp64 MFMA and VALU share it)
         __builtin_amdgcn_s_setprio(2);
@@ -1207,7 +1318,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             if constexpr (DBG == 6) return __builtin_amdgcn_s_memtime();
             return 0;
         };
-        auto run = [&](auto gen) {
+        auto run = [&](auto gen) __attribute__((always_inline)) {
             WsRegs<TS> R0, R1;
             issue(R0, 0);
             issue_t(0);
@@ -1220,11 +1331,14 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             // with tile i+3; unrolled by two so each register set is a fixed set of VGPRs, with
             // the odd last iteration peeled so the loop body has no conditional loads
             int i = 0;
+            // (FAINT: between the barriers that publish tiles i and i+1 the consumers only read
+            // buffer i&1, so the producers' statistics read it too — fs_tile(i))
             for (; i + 1 < ntiles; i += 2) {
                 tq = tick();
                 stage(R1, i + 1, gen);
                 if constexpr (DBG == 6) { const auto t1 = tick(); pst += t1 - tq; tq = t1; }
                 issue_t(i + 2);
+                fs_tile(i);  // (R1's registers are free until their reload)
                 issue(R1, i + 3);
                 if constexpr (DBG == 6) { const auto t1 = tick(); pis += t1 - tq; tq = t1; }
                 __syncthreads();
@@ -1232,6 +1346,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
                 stage(R0, i + 2, gen);
                 if constexpr (DBG == 6) { const auto t1 = tick(); pst += t1 - tq; tq = t1; }
                 issue_t(i + 3);
+                fs_tile(i + 1);
                 issue(R0, i + 4);
                 if constexpr (DBG == 6) { const auto t1 = tick(); pis += t1 - tq; tq = t1; }
                 __syncthreads();
@@ -1239,6 +1354,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             }
             if (i < ntiles) {
                 stage(R1, i + 1, gen);
+                fs_tile(i);
                 __syncthreads();
             }
         };
@@ -1272,7 +1388,6 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
         acc32[m] = (v4f){0.0f, 0.0f, 0.0f, 0.0f};
     }
     // partial moments of one sample unit: write part[u], restart the accumulators
-    const int tpu = (int)(unit_len / MM_TS);  // tiles per unit (units are whole tiles)
     auto put = [&](double *base, int m, int n, int row, int col, double v) {
         // moment index of output element (row, col) of column tile n: series row >> 1, re/im
         // of q row & 1, harmonic 8n + (col >> 1) + 1, cos/sin col & 1 → (A, B, C, D) code
@@ -1326,7 +1441,6 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             acc32[m] = (v4f){0.0f, 0.0f, 0.0f, 0.0f};
         }
     };
-    const long long u_first = s_begin / unit_len;
     __syncthreads();  // tile 0 staged
     unsigned long long cmf = 0, cbar = 0;  // DBG == 6 only
     int cs = -1;      // FAINT: state of the accumulators (-1: empty)
@@ -1511,12 +1625,81 @@ __global__ __launch_bounds__(256) void k_reduce_moments(const double *__restrict
 #endif
 
 
+// k_faint_fused_fin: compute_mean_var_power (src/Faint.jl:89-100) of every faint series from the
+// moment pass's fused statistics — per state code s, in unit order, the counts fcnt and shifted
+// sums fsp (S1, S2 of both sample halves) of the units whose slot s was written (smask), then
+// the deferred samples' sums (fixs, k_moments_fix; when dhdr lists any of state s):
+//   m = K + S1/n,   var = (S2 − S1·(S1/n)) / (n − 1),   w = 1/var,   K = abs(d) at dhdr[2 + s],
+// and W2 = Σ_s w_s Σ|q|²_s, DEN = Σ_s w_s m_s² n_s, Q2 = Σ_s (w_s m_s)² Σ|q|²_s from the moment
+// partials' row 2 (Σ|q|² = Σ|d|² per state) — the record k_faint_p1/p2/fin write (fstat[16k …]:
+// m then w of TRANSIENT, OFF … HIGH; the TRANSIENT slot and states without samples NaN).
+// One thread per series.
+__global__ __launch_bounds__(256) void k_faint_fused_fin(Problem pb, int units,
+                                                         const double *__restrict__ fsp,
+                                                         const int *__restrict__ fcnt,
+                                                         const unsigned *__restrict__ smask,
+                                                         const double *__restrict__ part,
+                                                         const double *__restrict__ fixs,
+                                                         const double *__restrict__ fixp,
+                                                         const int *__restrict__ dhdr,
+                                                         double *__restrict__ fstat)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
+    const long long k = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (k >= pb.P) return;
+    const long long P = pb.P;
+    const int ndef = dhdr[0];
+    const unsigned dm = (unsigned)dhdr[1];
+    double *o = fstat + k * 16;
+    const double nan = __builtin_nan("");
+    o[0] = nan;  // TRANSIENT: never valid
+    o[5] = nan;
+    double W2 = 0.0, DEN = 0.0, Q2 = 0.0;
+    for (int s = 0; s < FST_SLOTS; ++s) {
+        double n = 0.0, S1 = 0.0, S2 = 0.0, D2 = 0.0;
+        for (int u = 0; u < units; ++u) {
+            if (!((smask[u] >> s) & 1u)) continue;
+            const long long slot = (long long)u * FST_SLOTS + s;
+            n += (double)fcnt[slot];
+            S1 += fsp[(slot * 4 + 0) * P + k] + fsp[(slot * 4 + 2) * P + k];
+            S2 += fsp[(slot * 4 + 1) * P + k] + fsp[(slot * 4 + 3) * P + k];
+            D2 += part[(slot * NMOM + 2) * P + k];
+        }
+        if (ndef > 0 && ((dm >> s) & 1u)) {
+            n += fixs[(long long)(3 * s + 0) * P + k];
+            S1 += fixs[(long long)(3 * s + 1) * P + k];
+            S2 += fixs[(long long)(3 * s + 2) * P + k];
+            D2 += fixp[((long long)s * NMOM + 2) * P + k];
+        }
+        double m = nan, w = nan;
+        if (n > 0) {
+            const c64 z = d_at(pb, k * pb.ldd + dhdr[2 + s]);
+            const double K = jl_hypot(z.re, z.im);
+            m = K + S1 / n;
+            w = 1.0 / ((S2 - S1 * (S1 / n)) / (n - 1.0));
+            W2 += w * D2;
+            DEN += w * m * m * n;
+            Q2 += (w * m) * (w * m) * D2;
+        }
+        o[1 + s] = m;
+        o[6 + s] = w;
+    }
+    o[10] = W2;
+    o[11] = DEN;
+    o[12] = Q2;
+}
+#else
+;
+#endif
+
+
 // k_faint_defer: the samples the state-split moment pass leaves out — valid samples whose state
 // differs from their 32-sample tile's (the state of its first valid sample) — as a list of
 // (tile, sample bits) pairs in tile order: dlist[2e], dlist[2e + 1], e < dhdr[0]; dhdr[1] = the
 // OR of 1 << state over them.  States depend on the sample only, so the list serves every series
 // (and every shard: the order is that of the tiles).  One workgroup; prefix sums per round of
-// 1024 tiles.
+// 1024 tiles.  dhdr[2 + s]: the first valid sample of state s (the shift of the fused faint
+// statistics, k_moments_ws<FAINT>; 0 when the state has none).
 __global__ __launch_bounds__(1024) void k_faint_defer(Problem pb, int *__restrict__ dlist,
                                                       int *__restrict__ dhdr)
 #if GPD_OWNS(GPD_U_ENGINE)
@@ -1524,12 +1707,14 @@ __global__ __launch_bounds__(1024) void k_faint_defer(Problem pb, int *__restric
     __shared__ int wcnt[16];
     __shared__ int sbase;
     __shared__ unsigned smk;
+    __shared__ int sfirst[FST_SLOTS];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const long long N = pb.N, nt = (N + MM_TS - 1) / MM_TS;
     if (tid == 0) {
         sbase = 0;
         smk = 0;
     }
+    if (tid < FST_SLOTS) sfirst[tid] = 0x7fffffff;
     __syncthreads();
     for (long long j0 = 0; j0 < nt; j0 += 1024) {
         const long long j = j0 + tid;
@@ -1549,10 +1734,15 @@ __global__ __launch_bounds__(1024) void k_faint_defer(Problem pb, int *__restric
                     w[s >> 2] |= (unsigned)(unsigned char)pb.state[j * MM_TS + s] << (8 * (s & 3));
             }
             int ds = -1;
+            unsigned fm = 0;
             for (int s = 0; s < MM_TS; ++s) {
                 if (s >= nb) break;
                 const int st = (int)(signed char)(w[s >> 2] >> (8 * (s & 3)));
                 if (!fst_valid(pb.flags, st)) continue;
+                if (!((fm >> st) & 1u)) {  // the tile's first sample of state st
+                    fm |= 1u << st;
+                    atomicMin(&sfirst[st], (int)(j * MM_TS + s));
+                }
                 if (ds < 0) {
                     ds = st;
                 } else if (st != ds) {
@@ -1584,6 +1774,7 @@ __global__ __launch_bounds__(1024) void k_faint_defer(Problem pb, int *__restric
         dhdr[0] = sbase;
         dhdr[1] = (int)smk;
     }
+    if (tid < FST_SLOTS) dhdr[2 + tid] = sfirst[tid] == 0x7fffffff ? 0 : sfirst[tid];
 }
 #else
 ;
@@ -1632,7 +1823,8 @@ __global__ __launch_bounds__(256) void k_fix_table(Problem pb, const int *__rest
 __global__ __launch_bounds__(256) void k_moments_fix(Problem pb, const int *__restrict__ dlist,
                                                      const int *__restrict__ dhdr,
                                                      const double *__restrict__ ftab,
-                                                     double *__restrict__ fixp)
+                                                     double *__restrict__ fixp,
+                                                     double *__restrict__ fixs = nullptr)
 #if GPD_OWNS(GPD_U_ENGINE)
 {
     const int cnt = dhdr[0];
@@ -1645,6 +1837,11 @@ __global__ __launch_bounds__(256) void k_moments_fix(Problem pb, const int *__re
         const long long doff = k * pb.ldd, foff = (long long)pb.fcop[k] * pb.ldfc;
         if (!((smk >> q) & 1u)) continue;
         double acc[12], f0r = 0.0, f0i = 0.0, w2 = 0.0;
+        double sn = 0.0, s1 = 0.0, s2 = 0.0, K = 0.0;  // fixs: the fused statistics' sums
+        if (fixs) {
+            const c64 z = d_at(pb, doff + dhdr[2 + q]);
+            K = jl_hypot(z.re, z.im);
+        }
 #pragma unroll
         for (int c = 0; c < 12; ++c) acc[c] = 0.0;
         // entries in batches of 4 with every load issued up front (a list walk one entry at a
@@ -1686,6 +1883,10 @@ __global__ __launch_bounds__(256) void k_moments_fix(Problem pb, const int *__re
                 f0r += qr;
                 f0i += qi;
                 w2 = fma(qr, qr, fma(qi, qi, w2));
+                const double y = fs_abs(qr, qi) - K;
+                sn += 1.0;
+                s1 += y;
+                s2 = fma(y, y, s2);
             }
         }
 #pragma unroll
@@ -1695,6 +1896,17 @@ __global__ __launch_bounds__(256) void k_moments_fix(Problem pb, const int *__re
             f0r += __shfl_xor(f0r, off, 64);
             f0i += __shfl_xor(f0i, off, 64);
             w2 += __shfl_xor(w2, off, 64);
+            if (fixs && hg == 0) {
+                sn += __shfl_xor(sn, off, 64);
+                s1 += __shfl_xor(s1, off, 64);
+                s2 += __shfl_xor(s2, off, 64);
+            }
+        }
+        if (fixs && hg == 0 && sl == 0) {
+            double *o = fixs + (long long)q * 3 * pb.P + k;
+            o[0] = sn;
+            o[pb.P] = s1;
+            o[2 * pb.P] = s2;
         }
         if (sl == 0) {
             double *o = fixp + (long long)q * NMOM * pb.P + k;

@@ -90,6 +90,7 @@ typedef struct {
 #define GPD_STATE_HIGH 3
 
 int gpd_version(void);                /* = GPD_ABI_VERSION                            */
+const char *gpd_build_id(void);       /* id of the sources the library was built from */
 const char *gpd_strerror(int code);   /* static string                                */
 int gpd_device_count(void);           /* visible HIP devices (0 if none)              */
 /* Free the library's cached device memory on `device` (fit workspace and the arena holding
@@ -300,6 +301,13 @@ int gpd_libm_eval(int fn, int64_t n, const double *x, const double *y, double *o
 /* Per-kernel timing of the last gpd_fit_batch_dev call on `device` (ms, HIP events on the
  * launch stream).  names/ms arrays of length cap; returns the number of entries. */
 int gpd_last_timings(int device, const char **names, double *ms, int cap);
+
+/* Faint statistics of the last fit call on `device` (test hook): the first n_series records of
+ * 16 doubles each — m of MetState code c − 1 at [16k + c] (c = 0 TRANSIENT … 4 HIGH), w at
+ * [16k + 5 + c], then Σw|d|², Σw m² n, Σ(w m)²|d|² at [16k + 10 … 12] — as the fit used them
+ * (the fused statistics of the state-split moment pass for whole-exposure harmonic fits, the
+ * separate kernels otherwise).  Waits for that call.  GPD_E_ARG if it had no faint series. */
+int gpd_last_faint_stats(int device, double *out, int64_t n_series);
 
 #ifdef __cplusplus
 }

@@ -344,6 +344,42 @@ void oracle_mean_var_power(int64_t n, const int8_t *states, const double *d_, do
     free(g);
 }
 
+/* The fused faint statistics of the state-split moment pass (r4; gpd_kernels.hpp k_moments_ws
+ * <FAINT> producers + k_faint_fused_fin): compute_mean_var_power (src/Faint.jl:89-100) in ONE
+ * pass over the valid samples as shifted sums, K_s = abs(d) at the first valid sample of state s,
+ *   S1 = Σ (|d| − K_s),  S2 = Σ (|d| − K_s)²,  m = K_s + S1/n,  w = 1 / ((S2 − S1·(S1/n)) / (n − 1)).
+ * The algorithm the device runs, restated in sample order with Julia's hypot for |d| (the device
+ * forms |q| = |p̄ d| through a hardware rsq and sums in its tile order, so its bits differ by a
+ * few ulps; the stated tolerance against the two-pass restatement above is 1e-13 relative on w).
+ * Checker only (tests/test_oracle.py, tests/test_gpu_faint_stats.py). */
+void oracle_mean_var_power_fused(int64_t n, const int8_t *states, const double *d_, uint32_t flags,
+                                 double *m5, double *w5) {
+    const cplx *d = (const cplx *)d_;
+    double K[5] = {0, 0, 0, 0, 0}, cnt[5] = {0, 0, 0, 0, 0}, s1[5] = {0, 0, 0, 0, 0},
+           s2[5] = {0, 0, 0, 0, 0};
+    for (int64_t i = 0; i < n; ++i) {
+        int ok = 1;
+        if (flags & ORACLE_ONLY_HIGH) ok = (states[i] == ST_HIGH) || (states[i] == ST_NORMAL);
+        if (states[i] == ST_TRANSIENT) ok = 0;
+        if (!ok) continue;
+        const int q = states[i] + 1;
+        const double x = jl_hypot(d[i].re, d[i].im);
+        if (cnt[q] == 0.0) K[q] = x;
+        const double y = x - K[q];
+        cnt[q] += 1.0;
+        s1[q] += y;
+        s2[q] = fma(y, y, s2[q]);
+    }
+    for (int q = 0; q < 5; ++q) {
+        if (cnt[q] == 0.0) {
+            m5[q] = w5[q] = NAN;
+            continue;
+        }
+        m5[q] = K[q] + s1[q] / cnt[q];
+        w5[q] = 1.0 / ((s2[q] - s1[q] * (s1[q] / cnt[q])) / (cnt[q] - 1.0));
+    }
+}
+
 void oracle_mean_var_power_series(int64_t n, const int8_t *states, const double *d_, uint32_t flags,
                                   double *m5, double *w5) {
     const cplx *d = (const cplx *)d_;

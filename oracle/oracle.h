@@ -65,6 +65,11 @@ void oracle_mean_var_power(int64_t n, const int8_t *states, const double *d, dou
 void oracle_mean_var_power_series(int64_t n, const int8_t *states, const double *d, uint32_t flags,
                                   double *m5, double *w5);
 
+/* The fused one-pass form of the same statistics (shifted sums, the device's moment pass, r4):
+ * m5/w5 as above; states without samples NaN. */
+void oracle_mean_var_power_fused(int64_t n, const int8_t *states, const double *d, uint32_t flags,
+                                 double *m5, double *w5);
+
 /* src/Modulation.jl:360 ϕrange = range(-π, π, 8), as Float64 values. */
 void oracle_phi_grid(double *out8);
 

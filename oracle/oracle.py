@@ -58,6 +58,8 @@ def lib():
         L.oracle_mean_var_power.restype = None
         L.oracle_mean_var_power_series.argtypes = [ctypes.c_int64, P, P, ctypes.c_uint32, P, P]
         L.oracle_mean_var_power_series.restype = None
+        L.oracle_mean_var_power_fused.argtypes = [ctypes.c_int64, P, P, ctypes.c_uint32, P, P]
+        L.oracle_mean_var_power_fused.restype = None
         L.oracle_phi_grid.argtypes = [P]
         L.oracle_phi_grid.restype = None
         OBJ = ctypes.CFUNCTYPE(ctypes.c_double, ctypes.c_void_p, ctypes.c_int,
@@ -159,6 +161,19 @@ def mean_var_power_series(states, d, onlyhigh=False):
     w5 = np.zeros(5)
     L.oracle_mean_var_power_series(d.size, _ptr(s), _ptr(d), ONLY_HIGH if onlyhigh else 0,
                                    _ptr(m5), _ptr(w5))
+    return m5, w5
+
+
+def mean_var_power_fused(states, d, onlyhigh=False):
+    """The one-pass shifted-sum form of mean_var_power_series (the device's fused statistics,
+    r4): arrays of 5, index = MetState code + 1, NaN for states without samples."""
+    L = lib()
+    s = np.ascontiguousarray(states, dtype=np.int8)
+    d = np.ascontiguousarray(d, dtype=np.complex128)
+    m5 = np.zeros(5)
+    w5 = np.zeros(5)
+    L.oracle_mean_var_power_fused(d.size, _ptr(s), _ptr(d), ONLY_HIGH if onlyhigh else 0,
+                                  _ptr(m5), _ptr(w5))
     return m5, w5
 
 

@@ -269,7 +269,8 @@ def test_faint_interleaved_states_harmonic(gpu, oracle, monkeypatch, onlyhigh):
     """State-split moments (k_moments_ws<FAINT>): valid states that change within a 32-sample
     tile, with no TRANSIENT margin, leave samples to k_faint_defer / k_moments_fix; runs of
     1..40 samples put several states in most tiles.  Harmonic fits against the oracle under the
-    tie envelope; the statistics on the side stream or serially give the same records."""
+    tie envelope, with the fused statistics and with the separate kernels; those on the side
+    stream (GPD_FAINT_SIDE=1) or serially give the same records."""
     N, P = 6000, 32
     rng = np.random.default_rng(5)
     st = np.empty(N, np.int8)
@@ -286,10 +287,14 @@ def test_faint_interleaved_states_harmonic(gpu, oracle, monkeypatch, onlyhigh):
     got = fit(gpu, B, state=st, method="harmonic", onlyhigh=onlyhigh)
     pert = perturbed_runs(oracle, B, ulps=HARM_ULPS, state=st, onlyhigh=onlyhigh)
     print(assert_fit_parity(got, ref, pert, label=f"faint/interleaved/onlyhigh={onlyhigh}"))
-    monkeypatch.setenv("GPD_FAINT_SIDE", "0")
+    # the separate statistics kernels, serially and on the side stream beside the moment pass
+    monkeypatch.setenv("GPD_FAINT_STATS", "1")
+    got1 = fit(gpu, B, state=st, method="harmonic", onlyhigh=onlyhigh)
+    print(assert_fit_parity(got1, ref, pert, label=f"faint/interleaved/separate/onlyhigh={onlyhigh}"))
+    monkeypatch.setenv("GPD_FAINT_SIDE", "1")
     got2 = fit(gpu, B, state=st, method="harmonic", onlyhigh=onlyhigh)
     for k in ("b", "phi", "chi2"):
-        assert np.array_equal(got[k], got2[k], equal_nan=True), k
+        assert np.array_equal(got1[k], got2[k], equal_nan=True), k
 
 
 def test_mjd_timestamps_quantised_harmonic(gpu, oracle):

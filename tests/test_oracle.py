@@ -102,6 +102,34 @@ def test_mean_var_power_matches_numpy(oracle):
         np.testing.assert_allclose(w[sel], 1 / a.var(ddof=1), rtol=1e-12)
 
 
+@pytest.mark.parametrize("level,noise", [(1.0, 0.3), (1.0, 1e-2), (1e3, 1e-3), (1e-6, 1e-9)])
+@pytest.mark.parametrize("onlyhigh", [False, True])
+def test_fused_mean_var_power_matches_two_pass(oracle, level, noise, onlyhigh):
+    """The fused one-pass statistics (shifted sums, K = abs(d) at each state's first valid
+    sample; the device's state-split moment pass, r4) against the two-pass restatement of
+    compute_mean_var_power (src/Faint.jl:89-100): m within 1e-15, w within 1e-13 relative — the
+    stated tolerance — also at |d|/σ ≈ 1e3, where the raw one-pass form Σx² − (Σx)²/n loses
+    six digits (and misses the tolerance by 1e3×)."""
+    rng = np.random.default_rng(int(level * 1e6) % 1000 + int(onlyhigh))
+    N = 20_000
+    st = rng.choice(np.array([0, 1, 2, 3, -1], dtype=np.int8), size=N, p=[0.1, 0.3, 0.3, 0.25, 0.05])
+    amp = np.where(st == 3, 1.1, np.where(st == 1, 0.3, 0.6)) * level
+    ph = rng.uniform(-np.pi, np.pi, N)
+    d = (amp + noise * level * rng.standard_normal(N)) * np.exp(1j * ph)
+    m2, w2 = oracle.mean_var_power_series(st, d, onlyhigh=onlyhigh)
+    m1, w1 = oracle.mean_var_power_fused(st, d, onlyhigh=onlyhigh)
+    ok = np.isfinite(w2)
+    assert ok[1:].sum() >= (2 if onlyhigh else 4)
+    np.testing.assert_allclose(m1[ok], m2[ok], rtol=1e-15)
+    np.testing.assert_allclose(w1[ok], w2[ok], rtol=1e-13)
+    assert np.isnan(m1[0]) and np.isnan(w1[0])  # TRANSIENT: never valid
+    if level == 1e3:  # the raw one-pass form the shift avoids
+        valid = (st == 3) & ~(np.isnan(d))
+        a = np.abs(d[valid])
+        raw = (np.sum(a * a) - np.sum(a) ** 2 / a.size) / (a.size - 1)
+        assert abs(1 / raw / w2[4] - 1) > 1e-11
+
+
 def test_mean_var_power_single_sample_state_is_nan(oracle):
     d = np.ones(10, dtype=np.complex128) * (1 + 1j)
     st = np.full(10, 2, dtype=np.int8)
