@@ -12,7 +12,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEEP = ("k_faint_p1", "k_faint_p2", "k_faint_fin", "k_moments_ws", "k_reduce_moments", "k_fit_exact",
-        "k_fit_harmonic", "k_prepare", "k_table", "k_faint_defer", "k_fix_table", "k_moments_fix")
+        "k_fit_harmonic", "k_prepare", "k_table", "k_faint_defer", "k_fix_table", "k_moments_fix",
+        "k_faint_fused_fin")
 
 
 def short(name):
