@@ -178,7 +178,7 @@ def timings(device: int = 0):
     """Per-kernel HIP-event timings (ms) of the last gpd_fit_batch_dev call on `device`; a stage
     that ran once per series cohort (the pipelined harmonic path) is summed over its cohorts."""
     L = load()
-    cap = 40
+    cap = 160  # >= kMaxTimers (gpd_engine.hip)
     names = (ctypes.c_char_p * cap)()
     ms = (ctypes.c_double * cap)()
     n = L.gpd_last_timings(device, names, ms, cap)

@@ -85,7 +85,17 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, jobs: 
     pending = [u for u in SOURCES if not only or u in only]
     if only:  # the other units from the release build
         rel = os.path.join(HERE, "build", "release")
-        objs += [os.path.join(rel, u.replace(".hip", ".o")) for u in SOURCES if u not in only]
+        reuse = [os.path.join(rel, u.replace(".hip", ".o")) for u in SOURCES if u not in only]
+        # every kernel takes Problem & co. by value: a release object older than a shared header
+        # would link silently against another struct layout (advisor r3) — refuse it
+        deps = [os.path.join(CSRC, h) for h in HEADERS] + \
+            [os.path.join(HERE, "..", "include", "gpdemod.h")]
+        newest = max(os.path.getmtime(p) for p in deps)
+        stale = [o for o in reuse if not os.path.exists(o) or os.path.getmtime(o) < newest]
+        if stale:
+            raise RuntimeError("--only: release objects older than the headers (rebuild the "
+                               "release library first): " + ", ".join(map(os.path.basename, stale)))
+        objs += reuse
     while pending or procs:
         while pending and len(procs) < jobs:
             src = pending.pop(0)

@@ -48,9 +48,11 @@ void set_err(char *buf, size_t len, const char *fmt, ...) {
         }                                                                                \
     } while (0)
 
-constexpr int kMaxTimers = 40;   // named kernel intervals of the last call
-constexpr int kMaxEv = 96;       // timing events of the last call (both streams)
 constexpr int kMaxCohorts = 16;  // series cohorts of the pipelined harmonic path
+// timing events / named intervals of the last call (both streams): ≤ 7 per cohort plus the
+// per-call stages, so the pipelined path never runs out (advisor r3)
+constexpr int kMaxEv = 8 * kMaxCohorts + 16;
+constexpr int kMaxTimers = 8 * kMaxCohorts + 16;
 // exact fits of short spans take one wave per series once the series outnumber two 256-thread
 // workgroups per CU (one round of those); below, the 256-thread workgroup's lower latency per
 // evaluation wins (r3: 32 series 0.98 vs 1.56 ms; 16 000 windows 41.6 vs 17.0 ms)
@@ -113,6 +115,7 @@ struct Layout {
     long long unit_len; // samples per unit
     size_t smask, dlist, fixp, ftab;  // faint state-split moments (k_moments_ws<FAINT>)
     size_t fsp, fcnt, fixs;           // fused faint statistics (k_moments_ws<FAINT> producers)
+    size_t prep;                      // k_prepare_part's partial (count, min, max) per workgroup
     bool fs1;           // faint statistics in one pass (k_faint_p1/p2/fin), cohorts of fs_pc
     long long fs_pc;    // series per cohort
     int fs_mmax;        // samples per thread and part: ⌈N/2048⌉
@@ -192,6 +195,7 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     const long long nch = U;  // partial-moment sets (units)
     L.info = take(sizeof(Info));
     L.prof = take(PROF_LEN * sizeof(unsigned long long));  // diagnostic counters
+    L.prep = take((size_t)((N + PREP_PER - 1) / PREP_PER) * 3 * sizeof(double));  // k_prepare_part
     // cos/sin table, padded to whole MM_TS-sample tiles (k_table_mix fills the padding)
     L.tab = take(harmonic ? (size_t)((N + MM_TS - 1) / MM_TS * MM_TS) * 2 * KH * sizeof(double) : 0);
     // windowed series: k_moments_win writes mom directly (no partial moments)
@@ -201,7 +205,9 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     L.part = take(harmonic && !windowed
                       ? (size_t)nch * (fsplit ? FST_SLOTS : 1) * NMOM * P * sizeof(double) : 0);
     L.smask = take(fsplit ? (size_t)U * sizeof(unsigned) : 0);
-    L.dlist = take(fsplit ? (size_t)(2 * ((N + MM_TS - 1) / MM_TS) + 6) * sizeof(int) : 0);
+    // (+ the header, + k_faint_defer_count's 6 ints per block of 1024 tiles)
+    L.dlist = take(fsplit ? (size_t)(2 * ((N + MM_TS - 1) / MM_TS) + 6 +
+                             6 * ((N + MM_TS - 1) / MM_TS / 1024 + 1)) * sizeof(int) : 0);
     L.fixp = take(fsplit ? (size_t)FST_SLOTS * NMOM * P * sizeof(double) : 0);
     L.ftab = take(fsplit ? (size_t)((N + MM_TS - 1) / MM_TS) * MM_TS * 2 * KH * sizeof(double) : 0);
     // fused faint statistics: per (unit, state) slot, S1/S2 of the two sample halves per series,
@@ -489,7 +495,12 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     // GPD_SYNC_DEBUG=1: synchronise after every stage and name the stage that faulted
     static const bool sync_debug = getenv("GPD_SYNC_DEBUG") != nullptr;
     auto rec = [&](hipStream_t s) -> int {  // a timing event on stream s (index, or -1)
-        if (ne >= kMaxEv) return -1;
+        if (ne >= kMaxEv) {
+            static bool warned = false;
+            if (!warned) fprintf(stderr, "gpdemod: timing events exhausted; timings truncated\n");
+            warned = true;
+            return -1;
+        }
         (void)hipEventRecord(cx->ev[ne], s);
         return ne++;
     };
@@ -518,7 +529,12 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         return e == hipSuccess ? hipStreamSynchronize(stream) : e;
     };
 
-    k_prepare<<<1, 1024, 0, stream>>>(pb, info);
+    {
+        const unsigned np = (unsigned)((N + PREP_PER - 1) / PREP_PER);
+        double *pp = (double *)(ws + L.prep);
+        k_prepare_part<<<np, 256, 0, stream>>>(pb, pp);
+        k_prepare_fin<<<1, 256, 0, stream>>>(pp, (int)np, info);
+    }
     HIP_TRY(hipMemsetAsync(count, 0, sizeof(int), stream));
     mark("prepare");
     // Pipelined harmonic path (whole-exposure series, fits only, without fitoffsets): the
@@ -565,6 +581,12 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     unsigned *smask = (unsigned *)(ws + L.smask);
     int *dlist = (int *)(ws + L.dlist);
     int *dhdr = dlist + 2 * ((N + MM_TS - 1) / MM_TS);
+    int *dbsum = dhdr + 6;
+    const unsigned defer_blocks = (unsigned)(((N + MM_TS - 1) / MM_TS + 1023) / 1024);
+    auto faint_defer = [&]() {
+        k_faint_defer_count<<<defer_blocks, 1024, 0, stream>>>(pb, dbsum);
+        k_faint_defer_list<<<defer_blocks, 1024, 0, stream>>>(pb, dbsum, dlist, dhdr);
+    };
     double *fixp = (double *)(ws + L.fixp), *ftab = (double *)(ws + L.ftab);
     const unsigned ftab_grid = (unsigned)((N + MM_TS - 1) / MM_TS * MM_TS / 256 + 1);
     if (cohorts > 1) {
@@ -615,11 +637,11 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             moment_grid(N, n, cx->n_cu, true, true, units, ulen, chunk, nch, faint);
             dim3 g((unsigned)((n + MM_PIX - 1) / MM_PIX), (unsigned)nch);
             if (faint && c == 0) {
-                k_faint_defer<<<1, 1024, 0, stream>>>(pb, dlist, dhdr);
+                faint_defer();
                 k_fix_table<<<ftab_grid, 256, 0, stream>>>(pb, dlist, dhdr, ftab);
                 mark("faint_defer");
             }
-            if (faint) k_moments_fix<<<(unsigned)std::min<long long>(n, 1024), 256, 0, stream>>>(sp, dlist, dhdr, ftab, fix_c, fixs_c);
+            if (faint) k_moments_fix<<<dim3((unsigned)n, FST_SLOTS), 256, 0, stream>>>(sp, dlist, dhdr, ftab, fix_c, fixs_c);
             if (faint && is_c32 && tm)
                 k_moments_ws<0, false, c32, 2, true, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, smask, fsp_c, fcnt, dhdr);
             else if (faint && tm)
@@ -719,9 +741,9 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         } else if (use_mfma) {
             dim3 g((unsigned)((P + MM_PIX - 1) / MM_PIX), (unsigned)L.nch);
             if (faint) {  // the deferred samples of the state-split pass (usually none)
-                k_faint_defer<<<1, 1024, 0, stream>>>(pb, dlist, dhdr);
+                faint_defer();
                 k_fix_table<<<ftab_grid, 256, 0, stream>>>(pb, dlist, dhdr, ftab);
-                k_moments_fix<<<(unsigned)std::min<long long>(P, 1024), 256, 0, stream>>>(pb, dlist, dhdr, ftab, fixp, fixs);
+                k_moments_fix<<<dim3((unsigned)P, FST_SLOTS), 256, 0, stream>>>(pb, dlist, dhdr, ftab, fixp, fixs);
                 mark("faint_defer");
             }
             if (faint && is_c32 && tmix)  // faint series: the producer/consumer kernel, state-split

@@ -243,19 +243,38 @@ __device__ __forceinline__ void store_param(Param *out, double *raw, long long k
 }
 
 // ---------------------------------------------------------------------------------------
-// k_prepare: one workgroup.  Counts valid samples and classifies fl(ωt) for the harmonic path.
-__global__ __launch_bounds__(1024) void k_prepare(Problem pb, Info *info)
+// k_prepare: counts valid samples and classifies fl(ωt) for the harmonic path.  Many
+// workgroups (k_prepare_part: PREP_PER samples per workgroup, loads issued before use) write
+// partial (count, min, max) triples; k_prepare_fin combines them.  The count is an exact integer
+// and min/max are order-free, so the result does not depend on the split (r4; it was one
+// latency-bound 1024-thread workgroup, 53-73 µs per call).
+constexpr int PREP_PER = 4096;  // samples per k_prepare_part workgroup (256 threads × 16)
+__global__ __launch_bounds__(256) void k_prepare_part(Problem pb, double *__restrict__ part)
 #if GPD_OWNS(GPD_U_ENGINE)
 {
-    __shared__ double red[16 * 3];
+    __shared__ double red[4 * 3];
     double cnt = 0.0, xmn = 1.0e308, xmx = 0.0;
-    for (long long i = threadIdx.x; i < pb.N; i += 1024) {
-        int st;
-        if (!sample_valid(pb, i, st)) continue;
-        const double x = fabs(pb.omega * gld(pb.t + i));
-        cnt += 1.0;
-        xmn = fmin(xmn, x);
-        xmx = fmax(xmx, x);
+    const long long base = (long long)blockIdx.x * PREP_PER + threadIdx.x;
+    constexpr int U = PREP_PER / 256;
+    double tv[U];
+    int sv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const long long i = base + 256LL * u;
+        const long long ic = i < pb.N ? i : pb.N - 1;
+        tv[u] = gld(pb.t + ic);
+        sv[u] = pb.state ? (int)gld(pb.state + ic) : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const long long i = base + 256LL * u;
+        const int st = sv[u];
+        bool ok = i < pb.N;
+        if (pb.state) ok = ok && st != -1 && (!(pb.flags & F_ONLY_HIGH) || st == 3 || st == 2);
+        const double x = fabs(pb.omega * tv[u]);
+        cnt += ok ? 1.0 : 0.0;
+        xmn = ok ? fmin(xmn, x) : xmn;
+        xmx = ok ? fmax(xmx, x) : xmx;
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
@@ -271,7 +290,46 @@ __global__ __launch_bounds__(1024) void k_prepare(Problem pb, Info *info)
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int w = 1; w < 16; ++w) {
+        for (int w = 1; w < 4; ++w) {
+            cnt += red[w * 3];
+            xmn = fmin(xmn, red[w * 3 + 1]);
+            xmx = fmax(xmx, red[w * 3 + 2]);
+        }
+        part[3 * blockIdx.x] = cnt;
+        part[3 * blockIdx.x + 1] = xmn;
+        part[3 * blockIdx.x + 2] = xmx;
+    }
+}
+#else
+;
+#endif
+
+__global__ __launch_bounds__(256) void k_prepare_fin(const double *__restrict__ part, int nparts,
+                                                     Info *info)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
+    __shared__ double red[4 * 3];
+    double cnt = 0.0, xmn = 1.0e308, xmx = 0.0;
+    for (int b = threadIdx.x; b < nparts; b += 256) {
+        cnt += part[3 * b];
+        xmn = fmin(xmn, part[3 * b + 1]);
+        xmx = fmax(xmx, part[3 * b + 2]);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        cnt += __shfl_xor(cnt, off, 64);
+        xmn = fmin(xmn, __shfl_xor(xmn, off, 64));
+        xmx = fmax(xmx, __shfl_xor(xmx, off, 64));
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) {
+        red[wave * 3] = cnt;
+        red[wave * 3 + 1] = xmn;
+        red[wave * 3 + 2] = xmx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; ++w) {
             cnt += red[w * 3];
             xmn = fmin(xmn, red[w * 3 + 1]);
             xmx = fmax(xmx, red[w * 3 + 2]);
@@ -1697,84 +1755,122 @@ __global__ __launch_bounds__(256) void k_faint_fused_fin(Problem pb, int units,
 // differs from their 32-sample tile's (the state of its first valid sample) — as a list of
 // (tile, sample bits) pairs in tile order: dlist[2e], dlist[2e + 1], e < dhdr[0]; dhdr[1] = the
 // OR of 1 << state over them.  States depend on the sample only, so the list serves every series
-// (and every shard: the order is that of the tiles).  One workgroup; prefix sums per round of
-// 1024 tiles.  dhdr[2 + s]: the first valid sample of state s (the shift of the fused faint
-// statistics, k_moments_ws<FAINT>; 0 when the state has none).
-__global__ __launch_bounds__(1024) void k_faint_defer(Problem pb, int *__restrict__ dlist,
-                                                      int *__restrict__ dhdr)
+// (and every shard: the order is that of the tiles).  dhdr[2 + s]: the first valid sample of
+// state s (the shift of the fused faint statistics, k_moments_ws<FAINT>; 0 when the state has
+// none).  Two launches over blocks of 1024 tiles (r4; was one latency-bound workgroup walking
+// every tile): k_faint_defer_count writes each block's count / state mask / first samples into
+// bsum[6b …], k_faint_defer_list writes the entries at the block's offset (the sum of the
+// counts before it) in tile order, and its block 0 the header.
+__device__ __forceinline__ void defer_tile(const Problem &pb, long long j, unsigned &dm,
+                                           unsigned &sm, int (&first)[FST_SLOTS]) {
+    const long long N = pb.N;
+    // the tile's 32 state bytes in two 16-B loads when the array is 16-B aligned
+    unsigned w[8];
+    const long long nb = N - j * MM_TS;
+    if (nb >= MM_TS && (((unsigned long long)pb.state) & 15) == 0) {
+        const uint4 *src = (const uint4 *)(pb.state + j * MM_TS);
+        const uint4 a = src[0], b = src[1];
+        w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+        w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+    } else {
+        for (int q = 0; q < 8; ++q) w[q] = 0;
+        for (int s = 0; s < nb && s < MM_TS; ++s)
+            w[s >> 2] |= (unsigned)(unsigned char)pb.state[j * MM_TS + s] << (8 * (s & 3));
+    }
+    int ds = -1;
+    unsigned fm = 0;
+    dm = sm = 0;
+    for (int s = 0; s < MM_TS; ++s) {
+        if (s >= nb) break;
+        const int st = (int)(signed char)(w[s >> 2] >> (8 * (s & 3)));
+        if (!fst_valid(pb.flags, st)) continue;
+        if (!((fm >> st) & 1u)) {  // the tile's first sample of state st
+            fm |= 1u << st;
+            first[st] = min(first[st], (int)(j * MM_TS + s));
+        }
+        if (ds < 0) {
+            ds = st;
+        } else if (st != ds) {
+            dm |= 1u << s;
+            sm |= 1u << st;
+        }
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_faint_defer_count(Problem pb, int *__restrict__ bsum)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
+    __shared__ int wcnt[16];
+    __shared__ unsigned smk;
+    __shared__ int sfirst[FST_SLOTS];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const long long nt = (pb.N + MM_TS - 1) / MM_TS, j = (long long)blockIdx.x * 1024 + tid;
+    if (tid == 0) smk = 0;
+    if (tid < FST_SLOTS) sfirst[tid] = 0x7fffffff;
+    __syncthreads();
+    unsigned dm = 0, sm = 0;
+    int first[FST_SLOTS] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
+    if (j < nt) defer_tile(pb, j, dm, sm, first);
+    const unsigned long long b = __builtin_amdgcn_ballot_w64(dm != 0);
+    if (lane == 0) wcnt[wave] = __builtin_popcountll(b);
+    if (sm) atomicOr(&smk, sm);
+#pragma unroll
+    for (int s = 0; s < FST_SLOTS; ++s)
+        if (first[s] != 0x7fffffff) atomicMin(&sfirst[s], first[s]);
+    __syncthreads();
+    if (tid == 0) {
+        int tot = 0;
+        for (int w = 0; w < 16; ++w) tot += wcnt[w];
+        int *o = bsum + 6 * blockIdx.x;
+        o[0] = tot;
+        o[1] = (int)smk;
+        for (int s = 0; s < FST_SLOTS; ++s) o[2 + s] = sfirst[s];
+    }
+}
+#else
+;
+#endif
+
+__global__ __launch_bounds__(1024) void k_faint_defer_list(Problem pb, const int *__restrict__ bsum,
+                                                           int *__restrict__ dlist,
+                                                           int *__restrict__ dhdr)
 #if GPD_OWNS(GPD_U_ENGINE)
 {
     __shared__ int wcnt[16];
     __shared__ int sbase;
-    __shared__ unsigned smk;
-    __shared__ int sfirst[FST_SLOTS];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const long long N = pb.N, nt = (N + MM_TS - 1) / MM_TS;
+    const long long nt = (pb.N + MM_TS - 1) / MM_TS, j = (long long)blockIdx.x * 1024 + tid;
     if (tid == 0) {
-        sbase = 0;
-        smk = 0;
-    }
-    if (tid < FST_SLOTS) sfirst[tid] = 0x7fffffff;
-    __syncthreads();
-    for (long long j0 = 0; j0 < nt; j0 += 1024) {
-        const long long j = j0 + tid;
-        unsigned dm = 0, sm = 0;
-        if (j < nt) {
-            // the tile's 32 state bytes in two 16-B loads when the array is 16-B aligned
-            unsigned w[8];
-            const long long nb = N - j * MM_TS;
-            if (nb >= MM_TS && (((unsigned long long)pb.state) & 15) == 0) {
-                const uint4 *src = (const uint4 *)(pb.state + j * MM_TS);
-                const uint4 a = src[0], b = src[1];
-                w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
-                w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
-            } else {
-                for (int q = 0; q < 8; ++q) w[q] = 0;
-                for (int s = 0; s < nb; ++s)
-                    w[s >> 2] |= (unsigned)(unsigned char)pb.state[j * MM_TS + s] << (8 * (s & 3));
-            }
-            int ds = -1;
-            unsigned fm = 0;
-            for (int s = 0; s < MM_TS; ++s) {
-                if (s >= nb) break;
-                const int st = (int)(signed char)(w[s >> 2] >> (8 * (s & 3)));
-                if (!fst_valid(pb.flags, st)) continue;
-                if (!((fm >> st) & 1u)) {  // the tile's first sample of state st
-                    fm |= 1u << st;
-                    atomicMin(&sfirst[st], (int)(j * MM_TS + s));
-                }
-                if (ds < 0) {
-                    ds = st;
-                } else if (st != ds) {
-                    dm |= 1u << s;
-                    sm |= 1u << st;
-                }
-            }
-        }
-        const unsigned long long b = __builtin_amdgcn_ballot_w64(dm != 0);
-        const int before = __builtin_popcountll(b & ((1ull << lane) - 1ull));
-        if (lane == 0) wcnt[wave] = __builtin_popcountll(b);
-        if (sm) atomicOr(&smk, sm);
-        __syncthreads();
-        int off = sbase;
-        for (int w = 0; w < wave; ++w) off += wcnt[w];
-        if (dm) {
-            dlist[2 * (off + before)] = (int)j;
-            dlist[2 * (off + before) + 1] = (int)dm;
-        }
-        __syncthreads();
-        if (tid == 0) {
+        int off = 0;
+        for (unsigned q = 0; q < blockIdx.x; ++q) off += bsum[6 * q];
+        sbase = off;
+        if (blockIdx.x == 0) {  // the header: totals over every block
             int tot = 0;
-            for (int w = 0; w < 16; ++w) tot += wcnt[w];
-            sbase += tot;
+            unsigned sm = 0;
+            int first[FST_SLOTS] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
+            for (unsigned q = 0; q < gridDim.x; ++q) {
+                tot += bsum[6 * q];
+                sm |= (unsigned)bsum[6 * q + 1];
+                for (int s = 0; s < FST_SLOTS; ++s) first[s] = min(first[s], bsum[6 * q + 2 + s]);
+            }
+            dhdr[0] = tot;
+            dhdr[1] = (int)sm;
+            for (int s = 0; s < FST_SLOTS; ++s) dhdr[2 + s] = first[s] == 0x7fffffff ? 0 : first[s];
         }
-        __syncthreads();
     }
-    if (tid == 0) {
-        dhdr[0] = sbase;
-        dhdr[1] = (int)smk;
+    unsigned dm = 0, sm = 0;
+    int first[FST_SLOTS] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
+    if (j < nt) defer_tile(pb, j, dm, sm, first);
+    const unsigned long long b = __builtin_amdgcn_ballot_w64(dm != 0);
+    const int before = __builtin_popcountll(b & ((1ull << lane) - 1ull));
+    if (lane == 0) wcnt[wave] = __builtin_popcountll(b);
+    __syncthreads();
+    int off = sbase;
+    for (int w = 0; w < wave; ++w) off += wcnt[w];
+    if (dm) {
+        dlist[2 * (off + before)] = (int)j;
+        dlist[2 * (off + before) + 1] = (int)dm;
     }
-    if (tid < FST_SLOTS) dhdr[2 + tid] = sfirst[tid] == 0x7fffffff ? 0 : sfirst[tid];
 }
 #else
 ;
@@ -1816,8 +1912,8 @@ __global__ __launch_bounds__(256) void k_fix_table(Problem pb, const int *__rest
 // k_moments_fix: the unweighted moments q = p̄ d of the samples k_faint_defer lists, per state:
 // fixp[(q·NMOM + row)·P + k], the rows of k_moments_ws (Σq, Σ|q|², then A, B, C, D per
 // harmonic; every state of dhdr[1] written, nothing when the list is empty).  One workgroup
-// per series (≤ 1024 workgroups, each looping over series; with an empty list they return at
-// once); thread = (harmonic group hg of 3 harmonics, sample lane sl of 32); lane sl takes
+// per (series, state) (grid P × FST_SLOTS; with an empty list or a state without deferred
+// samples they return at once); thread = (harmonic group hg of 3 harmonics, sample lane sl of 32); lane sl takes
 // sample sl of each listed tile in list order (cos/sin n x from k_fix_table; entries in batches
 // of 4), the lanes are reduced by a fixed xor tree.
 __global__ __launch_bounds__(256) void k_moments_fix(Problem pb, const int *__restrict__ dlist,
@@ -1832,10 +1928,11 @@ __global__ __launch_bounds__(256) void k_moments_fix(Problem pb, const int *__re
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int hg = wave * 2 + (lane >> 5), sl = lane & 31;
     const unsigned smk = (unsigned)dhdr[1];
-    for (long long k = blockIdx.x; k < pb.P; k += gridDim.x)
-    for (int q = 0; q < FST_SLOTS; ++q) {
+    const long long k = blockIdx.x;  // one workgroup per (series, state)
+    const int q = blockIdx.y;
+    if (!((smk >> q) & 1u)) return;
+    {
         const long long doff = k * pb.ldd, foff = (long long)pb.fcop[k] * pb.ldfc;
-        if (!((smk >> q) & 1u)) continue;
         double acc[12], f0r = 0.0, f0i = 0.0, w2 = 0.0;
         double sn = 0.0, s1 = 0.0, s2 = 0.0, K = 0.0;  // fixs: the fused statistics' sums
         if (fixs) {

@@ -160,7 +160,46 @@ typedef struct {
     int nfev;
     uint64_t perturb;  /* 0, or a seed: χ² *= 1 + u per evaluation (tie-sensitivity probe) */
     double perturb_ulps; /* |u| = 2^-52 (≤ 1), or uniform in [0, perturb_ulps·2^-52] */
+    int order;         /* summation order of the cost's sums: 0 = CR8 (the product's), else an
+                          alternative order the reference's own loops may take (red_slot) */
 } chi2_ctx;
+
+/* Alternative summation orders (the reference-ceiling probe, bench.py cpu_baseline): Julia's
+ * `@simd` loops (src/Modulation.jl:181,301) and BLAS zdotc (:143-144) leave the order to the
+ * compiler / BLAS kernel, so the reference's own χ² differs by ulps from one CPU to another.
+ * order 1: strictly sequential (a loop without @simd); order L > 1: what a vectorised loop with
+ * L accumulators does — sample i (counted over the valid samples, as the reference's
+ * data[valid] vectors are) adds into accumulator i mod L for i < n - n mod L, the remainder into
+ * a scalar tail; at the end the unrolled vectors (width V = 4 for L = 16: AVX2 × 4 unroll; V = 8
+ * for L = 32: AVX-512 × 4) are added one after the other, the vector lanes by a halving tree,
+ * then the tail.  Test infrastructure only; the product keeps CR8. */
+static inline int64_t red_slot(const chi2_ctx *c, int64_t i) {
+    if (c->order == 0) return c->orig[i];
+    if (c->order == 1) return 0;
+    const int64_t L = c->order;
+    return i < c->n - c->n % L ? i % L : L;
+}
+
+static void red_total(const chi2_ctx *c, const gsum_t *g, double *out) {
+    if (c->order == 0) {
+        gsum_total(g, out);
+        return;
+    }
+    for (int q = 0; q < g->nv; ++q) {
+        if (c->order == 1) {
+            out[q] = g->v[q][0];
+            continue;
+        }
+        const int L = c->order, V = L >= 32 ? 8 : 4, U = L / V;
+        double acc[8];
+        for (int l = 0; l < V; ++l) acc[l] = g->v[q][l];
+        for (int u = 1; u < U; ++u)
+            for (int l = 0; l < V; ++l) acc[l] = g->v[q][u * V + l] + acc[l];
+        for (int h = V / 2; h >= 1; h >>= 1)
+            for (int l = 0; l < h; ++l) acc[l] = acc[l] + acc[l + h];
+        out[q] = acc[0] + g->v[q][L];
+    }
+}
 
 static uint64_t mix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -191,7 +230,7 @@ static double chi2_eval(chi2_ctx *c, double b, double phi) {
         for (int64_t i = 0; i < n; ++i) {
             double wi = c->w ? c->w[i] : 1.0;
             cplx m = model[i], dd = c->d[i];
-            const int64_t o = c->orig[i];
+            const int64_t o = red_slot(c, i);
             GSLOT(g, o, 0) += wi;
             GSLOT(g, o, 1) += wi * m.re;
             GSLOT(g, o, 2) += wi * m.im;
@@ -203,7 +242,7 @@ static double chi2_eval(chi2_ctx *c, double b, double phi) {
             GSLOT(g, o, 6) += pr.re;
             GSLOT(g, o, 7) += pr.im;
         }
-        gsum_total(g, tot);
+        red_total(c, g, tot);
         double a11 = tot[0], a22 = tot[3];
         cplx a12 = {tot[1], tot[2]}, b1 = {tot[4], tot[5]}, b2 = {tot[6], tot[7]};
         /* SMatrix{2,2}([a11 a12; conj(a12) a22]) \ [b1, b2]  — StaticArrays 2×2 Cramer */
@@ -235,13 +274,13 @@ static double chi2_eval(chi2_ctx *c, double b, double phi) {
             cplx mwc = {mw.re, -mw.im};
             cplx x = cmul(mwc, c->d[i]);
             cplx y = cmul(mwc, model[i]);
-            const int64_t o = c->orig[i];
+            const int64_t o = red_slot(c, i);
             GSLOT(g, o, 0) += x.re;
             GSLOT(g, o, 1) += x.im;
             GSLOT(g, o, 2) += y.re;
             GSLOT(g, o, 3) += y.im;
         }
-        gsum_total(g, tot);
+        red_total(c, g, tot);
         cplx num = {tot[0], tot[1]}, den = {tot[2], tot[3]};
         cplx aa = cdiv(num, den);
         mod->c_re = 0;
@@ -258,9 +297,9 @@ static double chi2_eval(chi2_ctx *c, double b, double phi) {
         for (int64_t i = 0; i < n; ++i) {
             double rr = model[i].re - c->d[i].re, ri = model[i].im - c->d[i].im;
             double a2 = rr * rr + ri * ri;
-            GSLOT(g, c->orig[i], 0) += (c->w ? c->w[i] : 1.0) * a2;
+            GSLOT(g, red_slot(c, i), 0) += (c->w ? c->w[i] : 1.0) * a2;
         }
-        gsum_total(g, &s);
+        red_total(c, g, &s);
     }
     if (c->perturb) {
         const uint64_t r = mix64(c->perturb ^ ((uint64_t)c->nfev << 20));
@@ -295,6 +334,7 @@ double oracle_chi2(int64_t n, const double *t, const double *d, const double *w,
     c.mod = mod;
     c.nfev = 0;
     c.perturb = 0;
+    c.order = 0;
     double r = chi2_eval(&c, b, phi);
     free(c.model);
     free(orig);
@@ -526,6 +566,7 @@ static void fit_pixel(int64_t n, const double *t, const cplx *dcol, const cplx *
     c.nfev = 0;
     c.perturb = perturb;
     c.perturb_ulps = perturb_ulps;
+    c.order = (int)((flags >> ORACLE_ORDER_SHIFT) & 0xffu);
 
     double x[2];
     if (xinit) {

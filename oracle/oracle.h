@@ -27,6 +27,9 @@ typedef struct {
 #define ORACLE_FIT_OFFSETS 1u
 #define ORACLE_RECENTER 2u
 #define ORACLE_ONLY_HIGH 4u
+/* oracle-only: bits 16-23 select an alternative summation order of the cost (demod_oracle.c
+ * red_slot: 0 = CR8, 1 = sequential, 16 / 32 = vectorised with 16 / 32 accumulators) */
+#define ORACLE_ORDER_SHIFT 16
 
 /* χ²(b,ϕ) for one series, reference arithmetic (src/Modulation.jl:122-148,174-195,299-326).
  * w == NULL means w ≡ 1.  On return *mod holds a (and c) at (b,ϕ). */

@@ -94,9 +94,17 @@ def newuoa(f, x0, rhobeg, rhoend, maxfun=None, npt=None):
 
 
 def fit_batch(t, d, fc, fc_of_pixel, state=None, omega=M_2PI, xinit=None, flags=RECENTER,
-              maxfun=60, want_output=False, nthreads=0, perturb_seed=0, perturb_ulps=1.0):
+              maxfun=60, want_output=False, nthreads=0, perturb_seed=0, perturb_ulps=1.0,
+              order=0):
     """Oracle batch fit.  d: (n_pixels, n_samples) complex128 (row k = pixel column k),
-    fc: (n_fc, n_samples) complex128, fc_of_pixel: (n_pixels,) int32."""
+    fc: (n_fc, n_samples) complex128, fc_of_pixel: (n_pixels,) int32.  order: the cost's
+    summation order — 0 = CR8 (the product's canonical order), 1 = sequential, 16 / 32 = a
+    vectorised loop with 16 / 32 accumulators (AVX2 / AVX-512 × 4 unroll): the orders Julia's
+    @simd loops and BLAS zdotc may take on a CPU (demod_oracle.c red_slot; the reference-ceiling
+    probe of bench.py)."""
+    if order not in (0, 1, 16, 32):
+        raise ValueError(f"order {order}: 0, 1, 16 or 32")
+    flags = int(flags) | (int(order) << 16)
     L = lib()
     t = np.ascontiguousarray(t, dtype=np.float64)
     d = np.ascontiguousarray(d, dtype=np.complex128)

@@ -60,13 +60,17 @@ def test_windows_match_oracle(gpu, oracle, N, nwindow, method):
         sp = np.minimum(nwindow, N - nwindow * np.arange(got.shape[0]))
         print(assert_exact_bitwise(got[sp < 256].reshape(-1), ref[sp < 256].reshape(-1),
                                    label="short windows"))
-        # every harmonic window (≥ 256 samples) lands within NEWUOA's rhoend (1e-3) of the
-        # oracle: tools/window_sweep.py measured max deviations 6.2e-4 / 5.6e-4 / 5.1e-4 /
-        # 2.3e-4 / 4.1e-5 at w = 256 / 300 / 345 / 400 / 500 (1024 series each), and 1.5e-3 at
-        # w = 200 — windows below 256 samples are fitted exactly (profiles/r3/window_sweep.json)
+        # every harmonic window (≥ 256 samples) lands near NEWUOA's rhoend (1e-3) of the
+        # oracle: tools/window_sweep.py (4 exposures of 8 windows × 32 diodes per length,
+        # synth.make_batch(8·w, 32, seed=100..103), 12 draws at 128 ulp) measured max deviations
+        # 6.2e-4 / 5.6e-4 / 5.1e-4 / 2.3e-4 / 4.1e-5 at w = 256 / 300 / 345 / 400 / 500, and
+        # 1.5e-3 at w = 200 — windows below 256 samples are fitted exactly
+        # (profiles/r3/window_sweep.json).  One sweep pins the bound, so windows below 400
+        # samples keep a 3x margin (2e-3; advisor r3), the longer ones 1e-3.
+        bound = 2e-3 if nwindow < 400 else 1e-3
         print(assert_fit_parity(got[sp >= 256].reshape(-1), ref[sp >= 256].reshape(-1),
                                 [p[sp >= 256].reshape(-1) for p in pert],
-                                label=f"windows {method} N={N} w={nwindow}", max_dev=1e-3)
+                                label=f"windows {method} N={N} w={nwindow}", max_dev=bound)
               if np.any(sp >= 256) else "no harmonic windows")
     # output rows of window w use window w's parameters (src/GPPupilDemodulation.jl:207)
     for w in range(ref.shape[0]):

@@ -90,6 +90,25 @@ def test_fit_recovers_truth(oracle):
     assert np.all(par["b"] >= 0)  # sign normalisation
 
 
+@pytest.mark.parametrize("order", [1, 16, 32])
+def test_alternative_summation_orders(oracle, order):
+    """The reference-ceiling probe (bench.py): the cost's sums in another order a CPU may take
+    (sequential, or a vectorised loop with 16 / 32 accumulators).  χ² at a fixed point moves by
+    ulps only; the fits stay the same minimum to NEWUOA's rhoend; order 0 is CR8 itself."""
+    B = synth.make_batch(4000, 8, seed=9)
+    a = (B["t"], B["d"], B["fc"], B["fc_of_pixel"])
+    ref = oracle.fit_batch(*a, flags=oracle.RECENTER)
+    same = oracle.fit_batch(*a, flags=oracle.RECENTER, order=0)
+    assert np.array_equal(same, ref)
+    alt = oracle.fit_batch(*a, flags=oracle.RECENTER, order=order)
+    assert np.all(np.abs(alt["b"] - ref["b"]) <= 1e-3 * np.abs(ref["b"]))
+    assert np.all(np.abs(alt["chi2"] - ref["chi2"]) <= 1e-6 * ref["chi2"])
+    # the order really differs: the fitted χ² bits are not all equal
+    assert not np.array_equal(alt["chi2"], ref["chi2"])
+    with pytest.raises(ValueError):
+        oracle.fit_batch(*a, order=7)
+
+
 def test_mean_var_power_matches_numpy(oracle):
     rng = np.random.default_rng(0)
     d = rng.standard_normal(3000) + 1j * rng.standard_normal(3000)
