@@ -213,6 +213,151 @@ __device__ __forceinline__ void drive_fit(F &f, const Problem &pb, double (&x)[2
     }
 }
 
+// A/B: inline the NEWUOA phases at their one call site each in drive_fit_sched
+#if defined(GPD_SCHED_INLINE) && GPD_SCHED_INLINE
+#define GPD_SCHED_INL [[clang::always_inline]]
+#else
+#define GPD_SCHED_INL
+#endif
+// The same driver for a wave of lane-per-series fits (k_fit_harmonic, r4): every lane's drive —
+// the 8-point grid, NEWUOB (NewuoaCo, gpd_newuoa.hpp), the π-flip check and its re-fit — is a
+// sequence of heavy phases (objective evaluations, TRSAPP, BIGLAG, BIGDEN, UPDATE) joined by
+// light code.  Each round the wave picks the phase most of its lanes wait at (ties: evaluation,
+// TRSAPP, UPDATE, BIGLAG, BIGDEN), runs it for those lanes and then their light code up to
+// their next heavy phase; the others wait.  A phase then executes about as often as the lane
+// needing it most (a greedy schedule over recorded NEWUOA traces: 1.2 M instead of 1.9 M cycles
+// per 64-series wave), where run()'s goto structure made the wave execute the union of the
+// lanes' orders.  Per lane the arithmetic and its order are drive_fit's and run()'s, so the
+// records are the same bits (tests/test_abi.py::test_newuoa_coroutine_equals_run_bitwise,
+// and on the device every harmonic parity test).  Lanes whose expansion went out of range
+// (f.fallback) stop: their series is re-fitted by the exact evaluator.
+template <class F, class NW>
+__device__ __forceinline__ void drive_fit_sched(F &f, const Problem &pb, double (&x)[2],
+                                                int &status, NW &nw) {
+    NewuoaCo<2, 5, true> co;
+    enum { S_GRID, S_RUN1, S_FLIPA, S_FLIPB, S_RUN2, S_DONE };
+    int stage, ph, gk = 0, best = 0;
+    double fb = 0.0, lkl = 0.0, php = 0.0, px[2];
+    bool g = false;  // glue pending (NEWUOB started or resumed)
+    if (pb.has_xinit) {
+        x[0] = pb.x0;
+        x[1] = pb.x1;
+        co.start(nw, x, 1.0, 1e-3, pb.maxfun);
+        stage = S_RUN1;
+        g = true;
+    } else {
+        stage = S_GRID;
+        ph = NW_EVAL;
+        px[0] = 0.1;
+        px[1] = c_phi_grid[0];
+    }
+    for (;;) {
+        if (g) {  // NEWUOB's light code up to its next heavy phase (one inlined copy)
+            co.glue(nw);
+            g = false;
+            ph = co.phase;
+            if (ph == NW_EVAL) {
+                px[0] = co.x[0];
+                px[1] = co.x[1];
+            } else if (ph == NW_DONE) {
+                x[0] = co.x[0];
+                x[1] = co.x[1];
+                if (co.ret >= pb.maxfun) status |= ST_MAXFUN;
+                if (stage == S_RUN1) {  // lklval = lkl(x), then lkl at ϕ ∓ π (:408-410)
+                    stage = S_FLIPA;
+                    ph = NW_EVAL;
+                    px[0] = x[0];
+                    px[1] = x[1];
+                } else {
+                    stage = S_DONE;
+                }
+            }
+        }
+        if (f.fallback) ph = NW_DONE;
+        const unsigned long long mE = __builtin_amdgcn_ballot_w64(ph == NW_EVAL);
+        const unsigned long long mT = __builtin_amdgcn_ballot_w64(ph == NW_TRSAPP);
+        const unsigned long long mU = __builtin_amdgcn_ballot_w64(ph == NW_UPDATE);
+        const unsigned long long mL = __builtin_amdgcn_ballot_w64(ph == NW_BIGLAG);
+        const unsigned long long mD = __builtin_amdgcn_ballot_w64(ph == NW_BIGDEN);
+        if ((mE | mT | mU | mL | mD) == 0) break;
+        int P = NW_EVAL, cmax = __builtin_popcountll(mE);
+        const int cT = __builtin_popcountll(mT), cU = __builtin_popcountll(mU),
+                  cL = __builtin_popcountll(mL), cD = __builtin_popcountll(mD);
+        if (cT > cmax) { P = NW_TRSAPP; cmax = cT; }
+        if (cU > cmax) { P = NW_UPDATE; cmax = cU; }
+        if (cL > cmax) { P = NW_BIGLAG; cmax = cL; }
+        if (cD > cmax) { P = NW_BIGDEN; cmax = cD; }
+        if (ph != P) continue;
+#if defined(GPD_DIAG)
+        const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
+#endif
+        if (P == NW_EVAL) {
+            const double fv = f(px);
+            if (stage == S_RUN1 || stage == S_RUN2) {
+                co.f = fv;  // NW_EVAL's resume label was set when the point was requested
+                g = true;
+            } else if (stage == S_GRID) {  // findmin: first NaN wins, else first minimum
+                if (gk == 0) {
+                    fb = fv;
+                } else if (!(fb != fb) && ((fv != fv) || fb > fv)) {
+                    best = gk;
+                    fb = fv;
+                }
+                if (++gk < 8) {
+                    px[1] = c_phi_grid[gk];
+                } else {
+                    x[0] = 0.1;
+                    x[1] = c_phi_grid[best];
+                    co.start(nw, x, 1.0, 1e-3, pb.maxfun);
+                    stage = S_RUN1;
+                    g = true;
+                }
+            } else if (stage == S_FLIPA) {
+                lkl = fv;
+                php = x[1] + (x[1] < 0 ? PI_F64 : -PI_F64);
+                px[1] = php;
+                stage = S_FLIPB;
+            } else {  // S_FLIPB: "bad minima" (src/Modulation.jl:411-414)
+                if (lkl > fv) {
+                    status |= ST_REFIT;
+                    x[1] = php;
+                    co.start(nw, x, 1.0, 1e-3, pb.maxfun);
+                    stage = S_RUN2;
+                    g = true;
+                } else {
+                    stage = S_DONE;
+                    ph = NW_DONE;
+                }
+            }
+        } else {
+            if (P == NW_TRSAPP) {
+                GPD_SCHED_INL nw.trsapp(co.delta, nw.d, co.crvmin);
+                co.lbl = co.L_TRS_POST;
+            } else if (P == NW_UPDATE) {
+                GPD_SCHED_INL nw.update(co.idz, co.beta, co.knew);
+                co.lbl = co.L_UPD_POST;
+            } else if (P == NW_BIGLAG) {
+                GPD_SCHED_INL nw.biglag(co.idz, co.knew, co.dstep, co.alpha);
+                co.lbl = co.L_VLAG;
+            } else {
+                GPD_SCHED_INL nw.bigden(co.idz, co.kopt, co.knew, co.beta);
+                co.lbl = co.L290;
+            }
+            g = true;
+        }
+#if defined(GPD_DIAG)
+        {  // lane-level cycles per phase in prof_[slot], wave-level in prof_[8 + slot]
+            const int slot = P == NW_TRSAPP ? 0 : P == NW_BIGLAG ? 1 : P == NW_BIGDEN ? 2
+                           : P == NW_UPDATE ? 3 : 7;
+            const unsigned long long dt = __builtin_amdgcn_s_memtime() - tp0;
+            nw.prof_[slot] += dt;
+            if ((int)threadIdx.x == __builtin_amdgcn_readfirstlane((int)threadIdx.x))
+                nw.prof_[8 + slot] += dt;
+        }
+#endif
+    }
+}
+
 template <class F>
 __device__ __forceinline__ void drive_fit(F &f, const Problem &pb, double (&x)[2], int &status) {
     Newuoa<2, 5> nw;  // per-thread state (exact path: replicated in every thread)
@@ -2267,6 +2412,10 @@ __device__ __forceinline__ void harm_offsets(HarmChi2 &f, const Problem &pb, lon
 #ifndef GPD_FIT_MINB
 #define GPD_FIT_MINB 1
 #endif
+// 1: the phase-scheduled driver (drive_fit_sched, r4); 0: drive_fit + run() (A/B builds)
+#ifndef GPD_FIT_SCHED
+#define GPD_FIT_SCHED 1
+#endif
 __global__ __launch_bounds__(64, GPD_FIT_MINB) void k_fit_harmonic(Problem pb, const Info *__restrict__ info,
                                                      const double *__restrict__ mom,
                                                      const double *__restrict__ aux,
@@ -2317,7 +2466,11 @@ __global__ __launch_bounds__(64, GPD_FIT_MINB) void k_fit_harmonic(Problem pb, c
 #pragma unroll
     for (int q = 0; q < 16; ++q) nwpool[threadIdx.x].prof_[q] = 0;
 #endif
+#if GPD_FIT_SCHED
+    drive_fit_sched(f, pb, x, status, nwpool[threadIdx.x]);
+#else
     drive_fit(f, pb, x, status, nwpool[threadIdx.x]);
+#endif
     const double chi2 = f(x);  // likelihood[idx] = lkl(x) (src/Modulation.jl:416)
     if (f.prof) {
         atomicAdd(&pb.prof[PROF_FIT + 0], f.prof_cycles);

@@ -160,6 +160,73 @@ def test_device_newuoa_equals_oracle_newuoa_bitwise(tmp_path, oracle):
         assert fx[0] == fo
 
 
+DEVCO = r'''
+#define __host__
+#define __device__
+#define __forceinline__ inline
+#include <cmath>
+#include "%s/gpd_newuoa.hpp"
+typedef double (*cb_t)(void*, int, const double*);
+template <bool D>
+static int co_run(double* x, double rb, double re, int maxfun, cb_t cb, double* fx) {
+  gpd::Newuoa<2,5,D> nw; gpd::NewuoaCo<2,5,D> co; double x0[2]={x[0],x[1]};
+  co.start(nw, x0, rb, re, maxfun);
+  co.glue(nw);
+  while (co.phase != gpd::NW_DONE) {
+    double fv = 0.0;
+    if (co.phase == gpd::NW_EVAL) { double xx[2] = {co.x[0], co.x[1]}; fv = cb(nullptr, 2, xx); }
+    co.exec(nw, fv);
+  }
+  x[0]=co.x[0]; x[1]=co.x[1]; *fx = co.fx; return co.ret;
+}
+extern "C" int devco(double* x, double rb, double re, int maxfun, cb_t cb, double* fx, int direct) {
+  return direct ? co_run<true>(x, rb, re, maxfun, cb, fx) : co_run<false>(x, rb, re, maxfun, cb, fx); }
+''' % CSRC
+
+
+def test_newuoa_coroutine_equals_run_bitwise(tmp_path, oracle):
+    """The resumable NEWUOB (NewuoaCo, the form k_fit_harmonic schedules phase by phase) gives
+    run()'s and the oracle's iterates bit for bit: the same points evaluated in the same order,
+    the same result, evaluation count and f — for χ² landscapes of the harmonic path, standard
+    test functions, maxfun below NPT and a few evaluations, both state layouts."""
+    L = _host_build(tmp_path, DEVCO, "devco")
+    OBJ = oracle.lib()._OBJ
+    L.devco.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_double, ctypes.c_int, OBJ,
+                        ctypes.c_void_p, ctypes.c_int]
+    B = synth.make_batch(2000, 24, seed=12)
+    grid = oracle.phi_grid()
+    funcs = [lambda x: (1 - x[0]) ** 2 + 100 * (x[1] - x[0] ** 2) ** 2,
+             lambda x: np.sin(3 * x[0]) * np.cos(2 * x[1]) + 0.1 * (x[0] ** 2 + x[1] ** 2),
+             lambda x: (x[0] - 0.3) ** 2 + 4.0 * (x[1] + 0.2) ** 2]
+    starts = [np.array([-1.2, 1.0]), np.array([0.1, 0.5]), np.array([2.0, -1.0])]
+    for k in range(24):
+        p = np.exp(1j * np.angle(B["fc"][B["fc_of_pixel"][k]]))
+        f = (lambda d: lambda x: oracle.chi2(B["t"], d, p, x[0], x[1])[0])(B["d"][k])
+        funcs.append(f)
+        starts.append(np.array([0.1, grid[int(np.argmin([f([0.1, g]) for g in grid]))]]))
+    for i, (f, x0) in enumerate(zip(funcs, starts)):
+        for maxfun in ((60, 3, 7) if i < 3 else (60,)):
+            seen = {}
+            for direct in (0, 1):
+                pts = []
+
+                def wrapped(ctx, n, xp):
+                    x = np.ctypeslib.as_array(xp, shape=(n,)).copy()
+                    pts.append(x)
+                    return float(f(x))
+                cb = OBJ(wrapped)
+                xd = x0.copy()
+                fx = np.zeros(1)
+                nd = L.devco(xd.ctypes.data, 1.0, 1e-3, maxfun, cb, fx.ctypes.data, direct)
+                seen[direct] = (nd, xd, fx[0], np.array(pts))
+            xo, fo, no = oracle.newuoa(f, x0, 1.0, 1e-3, maxfun=maxfun)
+            for direct, (nd, xd, fd, pts) in seen.items():
+                assert nd == no, (i, maxfun, direct)
+                np.testing.assert_array_equal(xd, xo)
+                assert fd == fo or (np.isnan(fd) and np.isnan(fo))
+            np.testing.assert_array_equal(seen[0][3], seen[1][3])
+
+
 BESSEL = r'''
 #define __host__
 #define __device__

@@ -126,7 +126,14 @@ def test_sincos_is_sin_and_cos(oracle):
     """Julia's sincos returns the very values of sin and cos (exp(Complex(0, β)) and sin(θ) of
     the model agree)."""
     rng = np.random.default_rng(7)
-    for x in argument_sets(rng, 20000).values():
+    sets = list(argument_sets(rng, 20000).values())
+    # the device NEWUOA's trial angles (TRSAPP / BIGLAG / BIGDEN take one sincos where the
+    # oracle's NEWUOA calls cos and sin, gpd_newuoa.hpp): dang·(i + s), s ∈ [-½, ½], and tiny ones
+    dang = 6.283185307179586476925286766559 / 50.0
+    sets.append(dang * (np.arange(50)[:, None] + np.linspace(-0.5, 0.5, 2001)[None, :]).ravel())
+    tiny = np.ldexp(1.0, np.arange(-1074, 3).astype(np.int64))
+    sets.append(np.concatenate([tiny, -tiny, 1.3 * tiny]))
+    for x in sets:
         sc = oracle.jl_eval("sincos", x)
         assert same_bits(sc[:, 0], oracle.jl_eval("sin", x))
         assert same_bits(sc[:, 1], oracle.jl_eval("cos", x))
