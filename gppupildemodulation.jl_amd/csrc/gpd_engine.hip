@@ -182,7 +182,7 @@ void moment_grid(long long N, long long P, int n_cu, bool harmonic, bool mfma, i
 
 Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic, bool phbuf,
             bool mfma, int n_cu, bool harm_offs, bool windowed = false, int exact_g = 1,
-            bool fp32 = false) {
+            bool fp32 = false, long long xround = 0) {
     Layout L{};
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -228,9 +228,10 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     L.fcid = take(harm_offs ? (size_t)n_fc * sizeof(int32_t) : 0);
     L.d0 = take(harm_offs ? (size_t)2 * P * sizeof(double) : 0);
     // exact evaluator: one model-cache slot of N complex per workgroup of the fit grid
-    // (min(P, 1024) workgroups), or per series with the multi-workgroup split, when that stays
-    // below 8 GB
-    const long long mc_slots = exact_g > 1 ? P : std::min<long long>(P, 1024);
+    // (min(P, 1024) workgroups), or per series with the multi-workgroup split (per series of a
+    // round, xround, for the persistent cohort form), when that stays below 8 GB
+    const long long mc_slots = exact_g > 1 ? (xround > 0 ? std::min(P, xround) : P)
+                                           : std::min<long long>(P, 1024);
     const size_t mc_bytes = (size_t)mc_slots * (size_t)N * sizeof(c64);
     L.mstride = (!harmonic && mc_bytes <= (size_t(8) << 30)) ? N : 0;
     L.mcache = take(L.mstride ? mc_bytes : 0);
@@ -426,8 +427,26 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             if ((f == 1 || f == 2 || f == 4 || f == 8) && p8 * f <= (long long)cx->n_cu) exact_g = f;
         }
     }
+    // Large whole-exposure exact batches, cohort form (r4, GPD_EXACT_COHORT=1): every series
+    // split over G = 8 workgroups and the grid persistent — exactly the workgroups resident at
+    // two per CU, a multiple of 8·G — so 2·n_cu / 8 series are in flight, their samples, model
+    // cache slots and shared phasor columns within the Infinity Cache over their ~70 passes.
+    // The per-series barrier needs all G parts resident: the grid never exceeds what the chip
+    // holds at once.  The records are the G = 1 records (canonical order).
+    long long xround = 0;
+    unsigned xgrid = 0;
+    if (want_exact && !bphi && window == 0 && exact_g == 1 && !fp32 && P * 8 > cx->n_cu &&
+        getenv("GPD_EXACT_COHORT") && atoi(getenv("GPD_EXACT_COHORT")) > 0 &&
+        N >= (long long)CR_SLOTS) {
+        const long long cap = (2LL * cx->n_cu) / 64 * 64;  // two 256-thread workgroups per CU
+        if (cap >= 64) {
+            exact_g = 8;
+            xgrid = (unsigned)cap;
+            xround = cap / 8;
+        }
+    }
     const Layout L = plan(N, P, n_fc, faint, harmonic, phbuf, use_mfma, cx->n_cu, harm_offs,
-                          window > 0, exact_g, fp32);
+                          window > 0, exact_g, fp32, xround);
     if (cx->ws_cap < L.total) {
         if (cx->ws) {
             HIP_TRY(hipDeviceSynchronize());
@@ -872,6 +891,10 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                     "n/a\n", (double)z[4] / nw, (double)zn[8] / nw, (double)zn[9] / nw,
                     (double)zn[11] / nw, (double)zn[12] / nw, (double)zn[13] / nw,
                     (double)zn[14] / nw);
+            // the phase-scheduled driver (drive_fit_sched): slot 5/13 = its glue (lane/wave
+            // level), slot 6 = rounds per wave, slot 7/15 = evaluation rounds (lane/wave)
+            fprintf(stderr, "fit_prof sched per wave: glue %.3g cycles, rounds %.3g, eval phase %.3g "
+                    "cycles\n", (double)zn[13] / nw, (double)zn[6] / nw, (double)zn[15] / nw);
 #endif
         } else {
             Problem pf = pb;
@@ -917,10 +940,11 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             HIP_TRY(prof_reset());
         }
         const unsigned fit_grid =
-            exact_g > 1 ? (unsigned)((P + 7) / 8 * 8 * exact_g) : exact_grid;
+            xgrid ? xgrid : exact_g > 1 ? (unsigned)((P + 7) / 8 * 8 * exact_g) : exact_grid;
         // two waves per SIMD (k_fit_exact MINB = 2) when the grid needs more than one round of
-        // one-wave-per-SIMD workgroups; GPD_EXACT_WAVES=1|2 forces it (A/B and tests)
-        bool two_waves = exact_g == 1 && (long long)fit_grid * (EXACT_WG / 64) > 4LL * cx->n_cu;
+        // one-wave-per-SIMD workgroups, and for the persistent cohort form (its grid is two
+        // workgroups per CU); GPD_EXACT_WAVES=1|2 forces it (A/B and tests)
+        bool two_waves = xgrid || (exact_g == 1 && (long long)fit_grid * (EXACT_WG / 64) > 4LL * cx->n_cu);
         if (const char *e = getenv("GPD_EXACT_WAVES")) two_waves = atoi(e) == 2 && exact_g == 1;
         // short spans (every series or window ≤ 2048 samples = one sample per canonical slot,
         // e.g. windows of ≤ 4 s at 500 Hz): one wave per series (k_fit_exact WGT = 64; the same

@@ -200,19 +200,27 @@ __device__ __forceinline__ void drive_fit(F &f, const Problem &pb, double (&x)[2
         x[1] = g;
     }
     double fx;
-    int nf = nw.run(x, 1.0, 1e-3, pb.maxfun, f, fx);
-    if (nf >= pb.maxfun) status |= ST_MAXFUN;
-    const double lklval = f(x);
-    const double php = x[1] + (x[1] < 0 ? PI_F64 : -PI_F64);
-    double xf[2] = {x[0], php};
-    if (lklval > f(xf)) {  // "bad minima" (src/Modulation.jl:411-414)
+    // NEWUOB, then the π-flip check and at most one re-fit from ϕ ∓ π (src/Modulation.jl:407-414)
+    // — one call site of run() in a two-pass loop, so the inlined NEWUOA exists once in the
+    // kernel's code (r4: the harmonic fit kernel 19.5 k → ~10 k instructions, against a 64 KB
+    // instruction cache shared by two CUs), the same operations in the same order
+    for (int pass = 0;; ++pass) {
+        const int nf = nw.run(x, 1.0, 1e-3, pb.maxfun, f, fx);
+        if (nf >= pb.maxfun) status |= ST_MAXFUN;
+        if (pass > 0) break;
+        const double lklval = f(x);
+        const double php = x[1] + (x[1] < 0 ? PI_F64 : -PI_F64);
+        double xf[2] = {x[0], php};
+        if (!(lklval > f(xf))) break;  // "bad minima" (src/Modulation.jl:411-414)
         status |= ST_REFIT;
         x[1] = php;
-        nf = nw.run(x, 1.0, 1e-3, pb.maxfun, f, fx);
-        if (nf >= pb.maxfun) status |= ST_MAXFUN;
     }
 }
 
+// A/B: 0 = greedy (the phase most lanes wait at), 1 = fixed cyclic order of the phases
+#ifndef GPD_SCHED_POLICY
+#define GPD_SCHED_POLICY 0
+#endif
 // A/B: inline the NEWUOA phases at their one call site each in drive_fit_sched
 #if defined(GPD_SCHED_INLINE) && GPD_SCHED_INLINE
 #define GPD_SCHED_INL [[clang::always_inline]]
@@ -239,6 +247,8 @@ __device__ __forceinline__ void drive_fit_sched(F &f, const Problem &pb, double 
     int stage, ph, gk = 0, best = 0;
     double fb = 0.0, lkl = 0.0, php = 0.0, px[2];
     bool g = false;  // glue pending (NEWUOB started or resumed)
+    int last = 4;    // GPD_SCHED_POLICY 1: index of the last phase run (cyclic order)
+    (void)last;
     if (pb.has_xinit) {
         x[0] = pb.x0;
         x[1] = pb.x1;
@@ -252,6 +262,12 @@ __device__ __forceinline__ void drive_fit_sched(F &f, const Problem &pb, double 
         px[1] = c_phi_grid[0];
     }
     for (;;) {
+#if defined(GPD_DIAG)
+        {  // rounds per wave (slot 6, first active lane)
+            if ((int)threadIdx.x == __builtin_amdgcn_readfirstlane((int)threadIdx.x)) nw.prof_[6] += 1;
+        }
+        const unsigned long long tg0 = __builtin_amdgcn_s_memtime();
+#endif
         if (g) {  // NEWUOB's light code up to its next heavy phase (one inlined copy)
             co.glue(nw);
             g = false;
@@ -274,19 +290,46 @@ __device__ __forceinline__ void drive_fit_sched(F &f, const Problem &pb, double 
             }
         }
         if (f.fallback) ph = NW_DONE;
+#if defined(GPD_DIAG)
+        {  // glue cycles: lane-level slot 5, wave-level slot 13
+            const unsigned long long dt = __builtin_amdgcn_s_memtime() - tg0;
+            nw.prof_[5] += dt;
+            if ((int)threadIdx.x == __builtin_amdgcn_readfirstlane((int)threadIdx.x)) nw.prof_[13] += dt;
+        }
+#endif
         const unsigned long long mE = __builtin_amdgcn_ballot_w64(ph == NW_EVAL);
         const unsigned long long mT = __builtin_amdgcn_ballot_w64(ph == NW_TRSAPP);
         const unsigned long long mU = __builtin_amdgcn_ballot_w64(ph == NW_UPDATE);
         const unsigned long long mL = __builtin_amdgcn_ballot_w64(ph == NW_BIGLAG);
         const unsigned long long mD = __builtin_amdgcn_ballot_w64(ph == NW_BIGDEN);
         if ((mE | mT | mU | mL | mD) == 0) break;
-        int P = NW_EVAL, cmax = __builtin_popcountll(mE);
-        const int cT = __builtin_popcountll(mT), cU = __builtin_popcountll(mU),
-                  cL = __builtin_popcountll(mL), cD = __builtin_popcountll(mD);
-        if (cT > cmax) { P = NW_TRSAPP; cmax = cT; }
-        if (cU > cmax) { P = NW_UPDATE; cmax = cU; }
-        if (cL > cmax) { P = NW_BIGLAG; cmax = cL; }
-        if (cD > cmax) { P = NW_BIGDEN; cmax = cD; }
+        int P = NW_EVAL;
+#if GPD_SCHED_POLICY == 1
+        {  // fixed cyclic order TRSAPP, BIGLAG, BIGDEN, evaluation, UPDATE: the next phase
+           // after the last one run that has a lane waiting (run()'s own order of phases)
+            const unsigned long long mk[5] = {mT, mL, mD, mE, mU};
+            const int ph_of[5] = {NW_TRSAPP, NW_BIGLAG, NW_BIGDEN, NW_EVAL, NW_UPDATE};
+#pragma unroll
+            for (int q = 1; q <= 5; ++q) {
+                const int c = (last + q) % 5;
+                if (mk[c]) {
+                    P = ph_of[c];
+                    last = c;
+                    break;
+                }
+            }
+        }
+#else
+        {  // greedy: the phase most lanes wait at
+            int cmax = __builtin_popcountll(mE);
+            const int cT = __builtin_popcountll(mT), cU = __builtin_popcountll(mU),
+                      cL = __builtin_popcountll(mL), cD = __builtin_popcountll(mD);
+            if (cT > cmax) { P = NW_TRSAPP; cmax = cT; }
+            if (cU > cmax) { P = NW_UPDATE; cmax = cU; }
+            if (cL > cmax) { P = NW_BIGLAG; cmax = cL; }
+            if (cD > cmax) { P = NW_BIGDEN; cmax = cD; }
+        }
+#endif
         if (ph != P) continue;
 #if defined(GPD_DIAG)
         const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
@@ -2412,9 +2455,10 @@ __device__ __forceinline__ void harm_offsets(HarmChi2 &f, const Problem &pb, lon
 #ifndef GPD_FIT_MINB
 #define GPD_FIT_MINB 1
 #endif
-// 1: the phase-scheduled driver (drive_fit_sched, r4); 0: drive_fit + run() (A/B builds)
+// 1: the phase-scheduled driver (drive_fit_sched, r4; measured slower);
+// 0: drive_fit + run() (default)
 #ifndef GPD_FIT_SCHED
-#define GPD_FIT_SCHED 1
+#define GPD_FIT_SCHED 0
 #endif
 __global__ __launch_bounds__(64, GPD_FIT_MINB) void k_fit_harmonic(Problem pb, const Info *__restrict__ info,
                                                      const double *__restrict__ mom,
@@ -3238,13 +3282,20 @@ __global__ __launch_bounds__(WGT, MINB) void k_fit_exact(Problem pb, const Info 
     __shared__ Newuoa<2, 5, true> nwx[WGT / 64];
     const double nvalid = (double)info->nvalid;
     if (WGT == EXACT_WG && G > 1) {  // one series per G workgroups (whole exposures, no list)
-        const long long k = xser(blockIdx.x, G);
+      // persistent over rounds of gridDim.x / G series (r4, large batches: gridDim.x = the
+      // resident workgroups, a multiple of 8·G, so a series' G parts are in one round and move
+      // on together; the series in flight — their samples and model cache slots — stay within
+      // the 256 MB Infinity Cache across the ~70 passes of their fits).  The model cache has a
+      // slot per series of a round (mstride apart); with one round (gridDim.x ≥ G·P) slot = k.
+      const long long per_round = gridDim.x / G;
+      for (long long bb = blockIdx.x;; bb += gridDim.x) {
+        const long long k = xser(bb, G);
         if (k >= pb.P) return;  // uniform per series: all its parts leave together
-        const int g = xpart(blockIdx.x, G);
+        const int g = xpart(bb, G);
         ExactChi2<FAINT, OFFS, PHBUF, (MINB == 2 ? 8 : CR_UR), WGT> f;
         setup_exact(f, pb, k, PHBUF ? phbuf : nullptr, lds, nvalid, G, g,
                     Xchg{xtot + k * (2 * CR_BLOCKS * CR_NV), xcnt + k});
-        if (mcache) f.mc = mcache + k * mstride;
+        if (mcache) f.mc = mcache + (k % per_round) * mstride;
         if (FAINT) {
 #pragma unroll
             for (int q = 0; q < 5; ++q) {
@@ -3268,7 +3319,8 @@ __global__ __launch_bounds__(WGT, MINB) void k_fit_exact(Problem pb, const Info 
             atomicAdd(&pb.prof[PROF_FIT + 2], f.pc[2]);
             atomicAdd(&pb.prof[PROF_FIT + 3], __builtin_amdgcn_s_memtime() - tf);
         }
-        return;
+        __syncthreads();  // lds and the NEWUOA state are reused by the next round's series
+      }
     }
     const long long total = list ? (long long)(*count) : pb.P;
     for (long long idx = blockIdx.x; idx < total; idx += gridDim.x) {

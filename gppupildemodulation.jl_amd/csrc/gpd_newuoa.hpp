@@ -168,6 +168,79 @@ struct Newuoa {
     double xbase[N], xopt[N], xnew[N], xpt[NPT][N], fval[NPT], gq[N], hq[NH], pq[NPT];
     double bmat[NDIM][N], zmat[NPT][NPTM], d[N], vlag[NDIM], w[NDIM];
 
+
+    // Powell's search over the trial angles i·2π/50 (TRSAPP's boundary iterations, BIGLAG):
+    // f(0) = fbeg, f(i) = val(i) for i = 1..49.  The published loop walks i in order keeping the
+    // first strictly better value (better(a, b); NaN is never better) and the values around it;
+    // with GPD_NW_TREE the 49 values are formed seven at a time and the first best index is found
+    // by a tree (right wins only when strictly better, or when left is NaN) — the same index, so
+    // the same fbest = f(isave), tempa = f(isave − 1) (f(−1) = f(49)) and tempb = f(isave + 1)
+    // (f(50) = fbeg), recomputed from val() with the same operations: the same bits, with a
+    // dependency chain of 7 × 3 selects instead of 49 × 4.
+    template <class V, class B>
+    GPD_HD static void angle_search(double fbeg, V &&val, B &&better, int &isave, double &fbest,
+                                    double &tempa, double &tempb) {
+#if defined(GPD_NW_TREE) && GPD_NW_TREE
+        if (fbeg != fbeg) {  // a NaN start: the published loop never moves
+            isave = 0;
+            fbest = fbeg;
+            tempa = val(49);
+            tempb = val(1);
+            return;
+        }
+        auto pick = [&](double lv, int li, double rv, int ri, double &ov, int &oi) {
+            const bool r = better(rv, lv) || (lv != lv && rv == rv);
+            ov = r ? rv : lv;
+            oi = r ? ri : li;
+        };
+        int bi = 0;
+        double bv = fbeg;
+#pragma unroll
+        for (int c = 0; c < 7; ++c) {
+            double v[7];
+#pragma unroll
+            for (int u = 0; u < 7; ++u) v[u] = val(7 * c + u + 1);
+            const int i0 = 7 * c + 1;
+            double a, b2, cc, e, f2, gv;
+            int ia, ib, ic, ie, jf, ig;
+            pick(v[0], i0, v[1], i0 + 1, a, ia);
+            pick(v[2], i0 + 2, v[3], i0 + 3, b2, ib);
+            pick(v[4], i0 + 4, v[5], i0 + 5, cc, ic);
+            pick(a, ia, b2, ib, e, ie);
+            pick(cc, ic, v[6], i0 + 6, f2, jf);
+            pick(e, ie, f2, jf, gv, ig);
+            if (better(gv, bv)) {
+                bv = gv;
+                bi = ig;
+            }
+        }
+        isave = bi;
+        fbest = bv;
+        tempa = bi == 0 ? val(49) : bi == 1 ? fbeg : val(bi - 1);
+        tempb = bi == 49 ? fbeg : val(bi + 1);
+#else
+        double fsav = fbeg, fnew = fbeg;
+        fbest = fbeg;
+        tempa = 0.0;
+        tempb = 0.0;
+        isave = 0;
+#pragma unroll 7  // 49 = 7·7 trial angles: independent values, ILP across 7
+        for (int i = 1; i <= 49; ++i) {
+            fnew = val(i);
+            if (better(fnew, fbest)) {
+                fbest = fnew;
+                isave = i;
+                tempa = fsav;
+            } else if (i == isave + 1) {
+                tempb = fnew;
+            }
+            fsav = fnew;
+        }
+        if (isave == 0) tempa = fnew;
+        if (isave == 49) tempb = fbeg;
+#endif
+    }
+
     // ---------------------------------------------------- hd = ∇²Q · v (TRSAPP label 170)
     GPD_HD void hess_mul(const double (&v)[N], double (&hd)[N]) const {
 #pragma unroll
@@ -293,25 +366,17 @@ struct Newuoa {
             }
             const double cf = 0.5 * (shs - dhd);
             const double qbeg = sg + cf;
-            double qsav = qbeg, qmin = qbeg, qnew = qbeg, tempa = 0.0, tempb = 0.0;
-            int isave = 0;
+            double qmin, tempa, tempb;
+            int isave;
             const int iu = 49;
             const double dang = kTwoPi / (double)(iu + 1);
-            #pragma unroll 7  // 49 = 7·7 trial angles: independent values, ILP across 7
-            for (int i = 1; i <= iu; ++i) {
-                const double cth = kAngCos[i], sth = kAngSin[i];
-                qnew = (sg + cf * cth) * cth + (dg + dhs * cth) * sth;
-                if (qnew < qmin) {
-                    qmin = qnew;
-                    isave = i;
-                    tempa = qsav;
-                } else if (i == isave + 1) {
-                    tempb = qnew;
-                }
-                qsav = qnew;
-            }
-            if (isave == 0) tempa = qnew;
-            if (isave == iu) tempb = qbeg;
+            angle_search(
+                qbeg,
+                [&](int i) {
+                    const double cth = kAngCos[i], sth = kAngSin[i];
+                    return (sg + cf * cth) * cth + (dg + dhs * cth) * sth;
+                },
+                [](double a, double b) { return a < b; }, isave, qmin, tempa, tempb);
             double ang = 0.0;
             if (tempa != tempb) {
                 tempa = tempa - qmin;
@@ -437,26 +502,17 @@ struct Newuoa {
             cf1 = 0.5 * cf1;
             cf4 = 0.5 * cf4 - cf1;
             const double taubeg = cf1 + cf2 + cf4;
-            double taumax = taubeg, tauold = taubeg, tempa = 0.0, tempb = 0.0;
-            tau = taubeg;
-            int isave = 0;
+            double taumax, tempa, tempb;
+            int isave;
             const int iu = 49;
             const double dang = kTwoPi / (double)(iu + 1);
-            #pragma unroll 7  // 49 = 7·7 trial angles: independent values, ILP across 7
-            for (int i = 1; i <= iu; ++i) {
-                const double cth = kAngCos[i], sth = kAngSin[i];
-                tau = cf1 + (cf2 + cf4 * cth) * cth + (cf3 + cf5 * cth) * sth;
-                if (fabs(tau) > fabs(taumax)) {
-                    taumax = tau;
-                    isave = i;
-                    tempa = tauold;
-                } else if (i == isave + 1) {
-                    tempb = tau;
-                }
-                tauold = tau;
-            }
-            if (isave == 0) tempa = tau;
-            if (isave == iu) tempb = taubeg;
+            angle_search(
+                taubeg,
+                [&](int i) {
+                    const double cth = kAngCos[i], sth = kAngSin[i];
+                    return cf1 + (cf2 + cf4 * cth) * cth + (cf3 + cf5 * cth) * sth;
+                },
+                [](double a, double b) { return fabs(a) > fabs(b); }, isave, taumax, tempa, tempb);
             double stp = 0.0;
             if (tempa != tempb) {
                 tempa = tempa - taumax;
@@ -1409,6 +1465,20 @@ struct Newuoa {
 // executes about as often as the lane that needs it most, not the union of all orders.  The
 // arithmetic is run()'s, statement for statement (same operations, same order): the same bits
 // (tests/test_abi.py::test_newuoa_coroutine_equals_run_bitwise).
+// glue()'s dispatch (A/B, GPD_GLUE_SEQ): a switch on the label in a loop, or the label blocks
+// tested one after the other in program order (a `break` leaves a block; the loop takes the few
+// backward transitions) — the same transitions either way
+#if defined(GPD_GLUE_SEQ) && GPD_GLUE_SEQ
+#define NW_SW_OPEN {
+#define NW_SW_CLOSE }
+#define NW_CASE(X) if (lbl == X) do {
+#define NW_END } while (0);
+#else
+#define NW_SW_OPEN switch (lbl) {
+#define NW_SW_CLOSE }
+#define NW_CASE(X) case X: {
+#define NW_END }
+#endif
 enum NwPhase { NW_EVAL = 0, NW_TRSAPP = 1, NW_BIGLAG = 2, NW_BIGDEN = 3, NW_UPDATE = 4, NW_DONE = 5 };
 
 template <int N, int NPT, bool DIRECT = false>
@@ -1490,8 +1560,8 @@ struct NewuoaCo {
     // run()'s code between heavy phases, label by label (inlined: its object lives in registers)
     GPD_HD void glue(NW &nw) {
         for (;;) {
-            switch (lbl) {
-            case L_INIT_PRE: {
+            NW_SW_OPEN
+            NW_CASE(L_INIT_PRE)
                 nf = init_nf;
                 nfm = nf - 1;
                 nfmm = nf - 1 - N;
@@ -1542,8 +1612,8 @@ struct NewuoaCo {
                 lbl = L_INIT_POST;
                 phase = NW_EVAL;
                 return;
-            }
-            case L_INIT_POST: {
+            NW_END
+            NW_CASE(L_INIT_POST)
                 NW::wr_(nw.fval, nf - 1, f);
                 if (nf == 1) {
                     fbeg = f;
@@ -1625,17 +1695,19 @@ struct NewuoaCo {
                 }
                 lbl = L90;
                 break;
-            }
-            case L90:
+            NW_END
+            NW_CASE(L90)
                 nfsav = nf;
                 lbl = L100;
                 break;
-            case L100:
+            NW_END
+            NW_CASE(L100)
                 knew = 0;
                 lbl = L_TRS_POST;
                 phase = NW_TRSAPP;
                 return;
-            case L_TRS_POST: {
+            NW_END
+            NW_CASE(L_TRS_POST)
                 dsq = 0.0;
 #pragma unroll
                 for (int i = 0; i < N; ++i) dsq = dsq + nw.d[i] * nw.d[i];
@@ -1659,8 +1731,8 @@ struct NewuoaCo {
                 }
                 lbl = L120;
                 break;
-            }
-            case L120:
+            NW_END
+            NW_CASE(L120)
                 if (dsq <= 1.0e-3 * xoptsq) nw.shift_base(xoptsq, idz);
                 if (knew > 0) {
                     lbl = L_VLAG;
@@ -1669,7 +1741,8 @@ struct NewuoaCo {
                 }
                 lbl = L_VLAG;
                 break;
-            case L_VLAG: {
+            NW_END
+            NW_CASE(L_VLAG)
 #pragma unroll
                 for (int k = 0; k < NPT; ++k) {
                     double suma = 0.0, sumb = 0.0, sum = 0.0;
@@ -1724,8 +1797,8 @@ struct NewuoaCo {
                 }
                 lbl = L290;
                 break;
-            }
-            case L290:
+            NW_END
+            NW_CASE(L290)
 #pragma unroll
                 for (int i = 0; i < N; ++i) {
                     nw.xnew[i] = nw.xopt[i] + nw.d[i];
@@ -1740,7 +1813,8 @@ struct NewuoaCo {
                 lbl = L_EVAL_POST;
                 phase = NW_EVAL;
                 return;
-            case L_EVAL_POST: {
+            NW_END
+            NW_CASE(L_EVAL_POST)
                 if (knew == -1) {
                     lbl = L530;
                     break;
@@ -1831,8 +1905,8 @@ struct NewuoaCo {
                 lbl = L_UPD_POST;
                 phase = NW_UPDATE;
                 return;
-            }
-            case L_UPD_POST: {
+            NW_END
+            NW_CASE(L_UPD_POST)
                 NW::wr_(nw.fval, knew - 1, f);
                 const double pqk = NW::rd_(nw.pq, knew - 1);
                 int ih = 0;
@@ -1911,8 +1985,8 @@ struct NewuoaCo {
                 knew = 0;
                 lbl = L460;
                 break;
-            }
-            case L460: {
+            NW_END
+            NW_CASE(L460)
                 double distsq = 4.0 * delta * delta;
 #pragma unroll
                 for (int k = 0; k < NPT; ++k) {
@@ -1937,8 +2011,8 @@ struct NewuoaCo {
                 }
                 lbl = L490;
                 break;
-            }
-            case L490:
+            NW_END
+            NW_CASE(L490)
                 if (rho > rhoend) {
                     delta = 0.5 * rho;
                     ratio = rho / rhoend;
@@ -1955,13 +2029,15 @@ struct NewuoaCo {
                 }
                 lbl = knew == -1 ? L290 : L530;
                 break;
-            default:  // L530
+            NW_END
+            NW_CASE(L530)  // default
                 nw.finish(x, fopt, f);
                 fx = f;
                 ret = nf;
                 phase = NW_DONE;
                 return;
-            }
+            NW_END
+            NW_SW_CLOSE
         }
     }
 };

@@ -132,10 +132,12 @@ extern "C" int devnw(double* x, double rb, double re, int maxfun, cb_t cb, doubl
 ''' % CSRC
 
 
-def test_device_newuoa_equals_oracle_newuoa_bitwise(tmp_path, oracle):
+@pytest.mark.parametrize("nw_tree", [0, 1])
+def test_device_newuoa_equals_oracle_newuoa_bitwise(tmp_path, oracle, nw_tree):
     """The device NEWUOA (gpd_newuoa.hpp, an independent structured implementation) compiled for
-    the host follows the oracle's Fortran-structured NEWUOA bit for bit."""
-    L = _host_build(tmp_path, DEVNW, "devnw")
+    the host follows the oracle's Fortran-structured NEWUOA bit for bit — with the trial-angle
+    searches sequential or as a tree (GPD_NW_TREE)."""
+    L = _host_build(tmp_path, "#define GPD_NW_TREE %d\n" % nw_tree + DEVNW, f"devnw{nw_tree}")
     OBJ = oracle.lib()._OBJ
     L.devnw.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_double, ctypes.c_int, OBJ,
                         ctypes.c_void_p]
@@ -184,12 +186,14 @@ extern "C" int devco(double* x, double rb, double re, int maxfun, cb_t cb, doubl
 ''' % CSRC
 
 
-def test_newuoa_coroutine_equals_run_bitwise(tmp_path, oracle):
+@pytest.mark.parametrize("glue_seq,nw_tree", [(0, 0), (1, 0), (0, 1)])
+def test_newuoa_coroutine_equals_run_bitwise(tmp_path, oracle, glue_seq, nw_tree):
     """The resumable NEWUOB (NewuoaCo, the form k_fit_harmonic schedules phase by phase) gives
     run()'s and the oracle's iterates bit for bit: the same points evaluated in the same order,
     the same result, evaluation count and f — for χ² landscapes of the harmonic path, standard
     test functions, maxfun below NPT and a few evaluations, both state layouts."""
-    L = _host_build(tmp_path, DEVCO, "devco")
+    L = _host_build(tmp_path, "#define GPD_GLUE_SEQ %d\n#define GPD_NW_TREE %d\n" % (glue_seq, nw_tree)
+                    + DEVCO, f"devco{glue_seq}{nw_tree}")
     OBJ = oracle.lib()._OBJ
     L.devco.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_double, ctypes.c_int, OBJ,
                         ctypes.c_void_p, ctypes.c_int]
@@ -225,6 +229,56 @@ def test_newuoa_coroutine_equals_run_bitwise(tmp_path, oracle):
                 np.testing.assert_array_equal(xd, xo)
                 assert fd == fo or (np.isnan(fd) and np.isnan(fo))
             np.testing.assert_array_equal(seen[0][3], seen[1][3])
+
+
+ANGSEARCH = r'''
+#define __host__
+#define __device__
+#define __forceinline__ inline
+#include <cmath>
+#include "%s/gpd_newuoa.hpp"
+extern "C" void search(const double* f, int mode, int* isave, double* out) {
+  double fb, ta, tb;
+  auto val = [&](int i) { return f[i]; };
+  if (mode == 0)
+    gpd::Newuoa<2,5>::angle_search(f[0], val, [](double a, double b) { return a < b; }, *isave, fb, ta, tb);
+  else
+    gpd::Newuoa<2,5>::angle_search(f[0], val, [](double a, double b) { return std::fabs(a) > std::fabs(b); }, *isave, fb, ta, tb);
+  out[0] = fb; out[1] = ta; out[2] = tb;
+}
+''' % CSRC
+
+
+def test_angle_search_tree_equals_sequential(tmp_path):
+    """NEWUOA's trial-angle search (TRSAPP: first minimum; BIGLAG: first maximum of |f|) as the
+    published sequential loop and as the tree of GPD_NW_TREE: the same index and values on random
+    values, ties (first index wins), ±0, ±inf and NaNs anywhere, the start value included."""
+    libs = [_host_build(tmp_path, "#define GPD_NW_TREE %d\n" % t + ANGSEARCH, f"as{t}") for t in (0, 1)]
+    for L in libs:
+        L.search.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    rng = np.random.default_rng(5)
+    specials = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1.0, -1.0])
+    for trial in range(20000):
+        kind = trial % 4
+        if kind == 0:
+            f = rng.normal(size=50)
+        elif kind == 1:  # few distinct values: ties everywhere
+            f = rng.integers(-3, 4, size=50).astype(np.float64)
+        elif kind == 2:  # specials sprinkled
+            f = rng.normal(size=50)
+            idx = rng.integers(0, 50, size=rng.integers(1, 8))
+            f[idx] = rng.choice(specials, size=idx.size)
+        else:
+            f = rng.choice(specials, size=50)
+        f = np.ascontiguousarray(f)
+        for mode in (0, 1):
+            res = []
+            for L in libs:
+                isave = ctypes.c_int(-1)
+                out = np.zeros(3)
+                L.search(f.ctypes.data, mode, ctypes.byref(isave), out.ctypes.data)
+                res.append((isave.value, out.tobytes()))
+            assert res[0] == res[1], (trial, mode, f)
 
 
 BESSEL = r'''

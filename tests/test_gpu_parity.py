@@ -440,6 +440,30 @@ def test_one_exposure_exact_every_split(gpu, oracle, monkeypatch, fitoffsets):
         print(assert_exact_bitwise(r, ref, label=f"C2 exact G={G or 'auto'} offsets={fitoffsets}"))
 
 
+@pytest.mark.parametrize("faint,fitoffsets", [(False, False), (True, False), (False, True)])
+def test_exact_cohort_form_records_bitwise(gpu, oracle, monkeypatch, faint, fitoffsets):
+    """Large exact batches in the cohort form (GPD_EXACT_COHORT=1: every series split over
+    G = 8 workgroups, a persistent grid of the resident workgroups working through rounds of
+    series, model-cache slots per series of a round): records byte-identical to the G = 1 batch
+    path and the oracle's bits — with more series than one round holds (a ragged last round)."""
+    P, N = 200, 6000
+    B = synth.make_batch(N, P, seed=77, offsets=fitoffsets)
+    st = None
+    if faint:
+        st = np.full(N, 2, dtype=np.int8)
+        st[500:1500] = 3
+        st[3000:4200] = 1
+        st[1495:1505] = -1
+        B["d"] = B["d"] * np.where(st == 3, 1.1, np.where(st == 1, 0.3, 0.6))[None, :]
+    monkeypatch.delenv("GPD_EXACT_COHORT", raising=False)
+    base = fit(gpu, B, method="exact", state=st, fitoffsets=fitoffsets)
+    monkeypatch.setenv("GPD_EXACT_COHORT", "1")
+    coh = fit(gpu, B, method="exact", state=st, fitoffsets=fitoffsets)
+    assert coh.tobytes() == base.tobytes()
+    ref = oracle_fit(oracle, B, state=st, fitoffsets=fitoffsets)
+    print(assert_exact_bitwise(coh, ref, label=f"exact cohort faint={faint} offsets={fitoffsets}"))
+
+
 @pytest.mark.parametrize("xinit,b_range", [(None, (0.3, 2.5)), ((8.0, 0.3), (0.3, 2.5)),
                                            (None, (6.0, 7.5))])
 def test_exact_model_regime_boundaries(gpu, oracle, xinit, b_range):

@@ -19,3 +19,10 @@ for u in 16 24 64; do
   GPD_UNITS=$u timeout -k 10 100 python tools/faint_time.py --reps 5 | sed "s/^/{\"units\": $u, \"r\": /; s/\$/}/" >> gpurun_out/r4b/c5_units.jsonl || exit 1
 done
 cat gpurun_out/r4b/c5_units.jsonl
+# exact evaluator: cohort form (G = 8, persistent, MALL-resident rounds) vs the G = 1 batch path
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py -k "cohort_form" > gpurun_out/r4b/cohort_tests.log 2>&1 || { tail -30 gpurun_out/r4b/cohort_tests.log; exit 1; }
+tail -1 gpurun_out/r4b/cohort_tests.log
+for c in 0 1; do
+  GPD_EXACT_COHORT=$c timeout -k 10 200 python tools/faint_time.py --method exact --reps 2 | sed "s/^/{\"cohort\": $c, \"r\": /; s/\$/}/" >> gpurun_out/r4b/exact.jsonl || exit 1
+done
+cat gpurun_out/r4b/exact.jsonl
