@@ -435,18 +435,44 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     // holds at once.  The records are the G = 1 records (canonical order).
     long long xround = 0;
     unsigned xgrid = 0;
+    // LDS model cache (r4): with G = 8 each thread of a part owns one canonical chain of
+    // ⌈N / 2048⌉ samples; the head of every chain's model (xlml samples, as many as the CU's LDS
+    // holds beside the kernel's static LDS) stays in LDS between the first and the residual
+    // pass, the rest in the part's global slot.  One workgroup per CU.  GPD_EXACT_LMC=0: off.
+    const bool lmc_on = !(getenv("GPD_EXACT_LMC") && atoi(getenv("GPD_EXACT_LMC")) == 0);
+    const char *coh = getenv("GPD_EXACT_COHORT");
+    const int coh_mode = coh ? atoi(coh) : 0;
     if (want_exact && !bphi && window == 0 && exact_g == 1 && !fp32 && P * 8 > cx->n_cu &&
-        getenv("GPD_EXACT_COHORT") && atoi(getenv("GPD_EXACT_COHORT")) > 0 &&
-        N >= (long long)CR_SLOTS) {
-        const long long cap = (2LL * cx->n_cu) / 64 * 64;  // two 256-thread workgroups per CU
+        coh_mode > 0 && N >= (long long)CR_SLOTS) {
+        // cohort form: two 256-thread workgroups per CU (global model cache), or one with the
+        // LDS model cache
+        const long long cap = ((lmc_on ? 1LL : 2LL) * cx->n_cu) / 64 * 64;
         if (cap >= 64) {
             exact_g = 8;
             xgrid = (unsigned)cap;
             xround = cap / 8;
         }
     }
+    int xlml = 0;
+    size_t xlds_bytes = 0;
+    if (want_exact && !bphi && window == 0 && exact_g == CR_BLOCKS && !fp32 && lmc_on) {
+        hipFuncAttributes fa;
+        HIP_TRY(hipFuncGetAttributes(&fa, (const void *)k_fit_exact<false, true, false>));
+        int lds_max = 0;
+        HIP_TRY(hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor,
+                                      device));
+        const long long chain = (N + CR_SLOTS - 1) / CR_SLOTS;
+        const long long room = ((long long)lds_max - (long long)fa.sharedSizeBytes - 256) /
+                               ((long long)EXACT_WG * (long long)sizeof(c64));
+        xlml = (int)std::max<long long>(0, std::min<long long>(room, chain));
+        xlds_bytes = (size_t)xlml * EXACT_WG * sizeof(c64);
+    }
     const Layout L = plan(N, P, n_fc, faint, harmonic, phbuf, use_mfma, cx->n_cu, harm_offs,
                           window > 0, exact_g, fp32, xround);
+    if (xlml > 0 && L.mstride == 0 && (long long)xlml * CR_SLOTS < N) {  // no global tail slot
+        xlml = 0;
+        xlds_bytes = 0;
+    }
     if (cx->ws_cap < L.total) {
         if (cx->ws) {
             HIP_TRY(hipDeviceSynchronize());
@@ -944,7 +970,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         // two waves per SIMD (k_fit_exact MINB = 2) when the grid needs more than one round of
         // one-wave-per-SIMD workgroups, and for the persistent cohort form (its grid is two
         // workgroups per CU); GPD_EXACT_WAVES=1|2 forces it (A/B and tests)
-        bool two_waves = xgrid || (exact_g == 1 && (long long)fit_grid * (EXACT_WG / 64) > 4LL * cx->n_cu);
+        bool two_waves = (xgrid && xlml == 0) ||
+                         (exact_g == 1 && (long long)fit_grid * (EXACT_WG / 64) > 4LL * cx->n_cu);
         if (const char *e = getenv("GPD_EXACT_WAVES")) two_waves = atoi(e) == 2 && exact_g == 1;
         // short spans (every series or window ≤ 2048 samples = one sample per canonical slot,
         // e.g. windows of ≤ 4 s at 500 Hz): one wave per series (k_fit_exact WGT = 64; the same
@@ -970,11 +997,16 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                 pb, info, ph, fstat, nullptr, nullptr, outp, raw, 0,                            \
                 L.mstride ? (c64 *)(ws + L.mcache) : nullptr, L.mstride, exact_g,               \
                 (double *)(ws + L.xtot), (unsigned *)(ws + L.xcnt));                            \
-        else                                                                                    \
-            k_fit_exact<FA, OF, PH><<<fit_grid, EXACT_WG, 0, stream>>>(                       \
+        else {                                                                                  \
+            if (xlds_bytes > 0)                                                                 \
+                HIP_TRY(hipFuncSetAttribute((const void *)k_fit_exact<FA, OF, PH>,              \
+                                            hipFuncAttributeMaxDynamicSharedMemorySize,          \
+                                            (int)xlds_bytes));                                   \
+            k_fit_exact<FA, OF, PH><<<fit_grid, EXACT_WG, xlds_bytes, stream>>>(              \
                 pb, info, ph, fstat, nullptr, nullptr, outp, raw, 0,                            \
                 L.mstride ? (c64 *)(ws + L.mcache) : nullptr, L.mstride, exact_g,               \
-                (double *)(ws + L.xtot), (unsigned *)(ws + L.xcnt));                            \
+                (double *)(ws + L.xtot), (unsigned *)(ws + L.xcnt), xlml);                      \
+        }                                                                                       \
     } while (0)
         if (faint) {
             if (offs) { if (phbuf) GPD_LAUNCH_EXACT(true, true, true); else GPD_LAUNCH_EXACT(true, true, false); }

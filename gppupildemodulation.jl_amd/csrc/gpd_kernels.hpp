@@ -2599,6 +2599,11 @@ struct ExactChi2 {
     // pass computed (same values, so the same sums) instead of re-evaluating sin/sincos and the
     // FC phasor; element i − s0 of the series' slot
     c64 *mc;
+    // LDS-resident head of the model cache (r4, G = 8: each thread owns exactly one canonical
+    // chain, so chain sample m = (i − s0) / 2048 of thread t sits at lmc[m·WGT + t] for m < lml;
+    // the chain's later samples stay in the global slot mc).  lml = 0: all in mc.
+    __attribute__((address_space(3))) c64 *lmc;
+    int lml;
     // multi-workgroup split: G workgroups per series, this one is g; x: the series' exchange
     int G, g;
     Xchg x;
@@ -2702,9 +2707,28 @@ struct ExactChi2 {
     }
     __device__ __forceinline__ void load_res(const View &v, long long i, Raw &r) const {
         r.st = v.state ? (int)v.state[i] : 0;
-        const gmc64 *mcg = (const gmc64 *)mc;
-        r.f = c64{mcg[i - s0].re, mcg[i - s0].im};
+        const int mm = (int)((i - s0) >> 11);  // wave-uniform: the chain's sample index
+        if (mm < lml) {
+            const __attribute__((address_space(3))) c64 *q = lmc + mm * WGT + (int)threadIdx.x;
+            r.f = c64{q->re, q->im};
+        } else {
+            const gmc64 *mcg = (const gmc64 *)mc;
+            r.f = c64{mcg[i - s0].re, mcg[i - s0].im};
+        }
         r.d = d_of(v, doff + i);
+    }
+    // the first pass's store of sample i's model into the cache (LDS head or global slot)
+    __device__ __forceinline__ void mc_put(long long i, const c64 &m) const {
+        const int mm = (int)((i - s0) >> 11);
+        if (mm < lml) {
+            __attribute__((address_space(3))) c64 *q = lmc + mm * WGT + (int)threadIdx.x;
+            q->re = m.re;
+            q->im = m.im;
+        } else {
+            gmc64 *mcg = (gmc64 *)mc;
+            mcg[i - s0].re = m.re;
+            mcg[i - s0].im = m.im;
+        }
     }
     // sample_valid on a loaded state (TRANSIENT dropped, onlyhigh keeps HIGH ∪ NORMAL)
     __device__ __forceinline__ bool valid_st(const View &v, int st) const {
@@ -3056,7 +3080,7 @@ struct ExactChi2 {
         ++nfev;
         const double b = xx[0], phi = xx[1];
         const View V = view();
-        gmc64 *mcg = (gmc64 *)mc;
+        const bool mcg = mc != nullptr || lml > 0;  // a model cache (global and/or LDS)
         const unsigned long long tp0 = prof ? __builtin_amdgcn_s_memtime() : 0;
         if (OFFS) {
             double v[8];  // a11, a12(2), a22, b1(2), b2(2)
@@ -3068,10 +3092,7 @@ struct ExactChi2 {
                     c64 p;
                     double w;
                     pw_of(r, p, w);
-                    if (mcg) {
-                        mcg[i - s0].re = m.re;
-                        mcg[i - s0].im = m.im;
-                    }
+                    if (mcg) mc_put(i, m);
                     const c64 dd = r.d;
                     a[0] += w;
                     a[1] += w * m.re;
@@ -3104,10 +3125,7 @@ struct ExactChi2 {
                 [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch32(X, b, phi, mb); },
                 [&](long long i, const Raw &r, const c64 &m, double (&a)[4]) {
                     if (!valid_st(V, r.st)) return;
-                    if (mcg) {
-                        mcg[i - s0].re = m.re;
-                        mcg[i - s0].im = m.im;
-                    }
+                    if (mcg) mc_put(i, m);
                     const float w = weight32(r.st);
                     const f2 m2 = {(float)m.re, (float)m.im}, d2 = {(float)r.d.re, (float)r.d.im};
                     const f2 mwc = {m2.re * w, -(m2.im * w)};
@@ -3132,10 +3150,7 @@ struct ExactChi2 {
                     c64 p;
                     double w;
                     pw_of(r, p, w);
-                    if (mcg) {
-                        mcg[i - s0].re = m.re;
-                        mcg[i - s0].im = m.im;
-                    }
+                    if (mcg) mc_put(i, m);
                     const c64 mwc = {m.re * w, -(m.im * w)};  // conj(model .* weight)
                     const c64 xv = cmul(mwc, r.d);
                     const c64 yv = cmul(mwc, m);
@@ -3226,6 +3241,8 @@ __device__ __forceinline__ void setup_exact(F &f, const Problem &pb, long long k
     f.src = phbuf ? phbuf + fcol * pb.N : nullptr;
     f.lds = lds;
     f.mc = nullptr;
+    f.lmc = nullptr;
+    f.lml = 0;
     f.s0 = sp.s0;
     f.s1 = sp.s1;
     f.G = G;
@@ -3273,10 +3290,13 @@ __global__ __launch_bounds__(WGT, MINB) void k_fit_exact(Problem pb, const Info 
                                                         c64 *__restrict__ mcache = nullptr,
                                                         long long mstride = 0, int G = 1,
                                                         double *__restrict__ xtot = nullptr,
-                                                        unsigned *__restrict__ xcnt = nullptr)
+                                                        unsigned *__restrict__ xcnt = nullptr,
+                                                        int lml = 0)
 #if GPD_OWNS(GPD_U_EXACT | GPD_U_EXACT64)
 {
     __shared__ double lds[EXACT_LDS];
+    // G = 8 with lml > 0: the head of every chain's model cache in dynamic LDS (lml·WGT c64)
+    extern __shared__ __attribute__((aligned(16))) double xlds_dyn[];
     // NEWUOA state: one copy per wave in LDS (all lanes of a wave run the same iteration and
     // read/write the same addresses), instead of replicated in every thread's registers
     __shared__ Newuoa<2, 5, true> nwx[WGT / 64];
@@ -3296,6 +3316,10 @@ __global__ __launch_bounds__(WGT, MINB) void k_fit_exact(Problem pb, const Info 
         setup_exact(f, pb, k, PHBUF ? phbuf : nullptr, lds, nvalid, G, g,
                     Xchg{xtot + k * (2 * CR_BLOCKS * CR_NV), xcnt + k});
         if (mcache) f.mc = mcache + (k % per_round) * mstride;
+        if (G == CR_BLOCKS && lml > 0) {  // one chain per thread (one canonical block per part)
+            f.lmc = (__attribute__((address_space(3))) c64 *)xlds_dyn;
+            f.lml = lml;
+        }
         if (FAINT) {
 #pragma unroll
             for (int q = 0; q < 5; ++q) {

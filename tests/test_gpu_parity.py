@@ -426,11 +426,17 @@ def test_one_exposure_exact_every_split(gpu, oracle, monkeypatch, fitoffsets):
     B = _exposure(100_000, seed=42, offsets=fitoffsets)
     ref = oracle_fit(oracle, B, fitoffsets=fitoffsets)
     recs = {}
-    for G in ("1", "2", "4", "8", None):
+    # "8-global": G = 8 with the whole model cache in global memory (GPD_EXACT_LMC=0) instead
+    # of the chains' heads in LDS (the default at G = 8)
+    for G in ("1", "2", "4", "8", "8-global", None):
         if G is None:
             monkeypatch.delenv("GPD_EXACT_G", raising=False)
         else:
-            monkeypatch.setenv("GPD_EXACT_G", G)
+            monkeypatch.setenv("GPD_EXACT_G", G[:1])
+        if G == "8-global":
+            monkeypatch.setenv("GPD_EXACT_LMC", "0")
+        else:
+            monkeypatch.delenv("GPD_EXACT_LMC", raising=False)
         fit(gpu, B, fitoffsets=fitoffsets, method="exact")  # warm (workspace)
         t0 = time.perf_counter()
         recs[G] = fit(gpu, B, fitoffsets=fitoffsets, method="exact")
@@ -460,6 +466,11 @@ def test_exact_cohort_form_records_bitwise(gpu, oracle, monkeypatch, faint, fito
     monkeypatch.setenv("GPD_EXACT_COHORT", "1")
     coh = fit(gpu, B, method="exact", state=st, fitoffsets=fitoffsets)
     assert coh.tobytes() == base.tobytes()
+    # the cohort form with the whole model cache in global memory (two workgroups per CU)
+    monkeypatch.setenv("GPD_EXACT_LMC", "0")
+    cog = fit(gpu, B, method="exact", state=st, fitoffsets=fitoffsets)
+    monkeypatch.delenv("GPD_EXACT_LMC")
+    assert cog.tobytes() == base.tobytes()
     ref = oracle_fit(oracle, B, state=st, fitoffsets=fitoffsets)
     print(assert_exact_bitwise(coh, ref, label=f"exact cohort faint={faint} offsets={fitoffsets}"))
 
