@@ -438,8 +438,11 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     // LDS model cache (r4): with G = 8 each thread of a part owns one canonical chain of
     // ⌈N / 2048⌉ samples; the head of every chain's model (xlml samples, as many as the CU's LDS
     // holds beside the kernel's static LDS) stays in LDS between the first and the residual
-    // pass, the rest in the part's global slot.  One workgroup per CU.  GPD_EXACT_LMC=0: off.
-    const bool lmc_on = !(getenv("GPD_EXACT_LMC") && atoi(getenv("GPD_EXACT_LMC")) == 0);
+    // pass, the rest in the part's global slot.  One workgroup per CU.  Measured slower than
+    // the global cache (C2 exact 3.32 → 3.46 ms, the residual pass 2.05 → 2.49 M cycles per
+    // workgroup; the C5 cohort form 375 → 486 ms at one workgroup per CU instead of two,
+    // profiles/r4/exact_lmc/), so opt-in: GPD_EXACT_LMC=1.
+    const bool lmc_on = getenv("GPD_EXACT_LMC") && atoi(getenv("GPD_EXACT_LMC")) == 1;
     const char *coh = getenv("GPD_EXACT_COHORT");
     const int coh_mode = coh ? atoi(coh) : 0;
     if (want_exact && !bphi && window == 0 && exact_g == 1 && !fp32 && P * 8 > cx->n_cu &&

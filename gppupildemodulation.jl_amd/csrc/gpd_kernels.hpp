@@ -2631,6 +2631,14 @@ struct ExactChi2 {
         const __attribute__((address_space(1))) float *xr;  // F_FP32 phase table
         double omega;
         bool only_high;
+        // the model cache, read once per evaluation (members of an out-of-line functor are
+        // read through its pointer, again after every store that may alias it)
+        __attribute__((address_space(1))) c64 *mc;
+        __attribute__((address_space(3))) c64 *lmc;
+        int lml;
+        long long s0;
+        long long doff, foff;   // series column / raw FC column offsets
+        const double *m5, *w5;  // faint power and weight per state (the functor's)
     };
     __device__ __forceinline__ View view() const {
         View v;
@@ -2644,21 +2652,40 @@ struct ExactChi2 {
         v.omega = pb->omega;
         v.only_high = (pb->flags & F_ONLY_HIGH) != 0;
         v.xr = (const __attribute__((address_space(1))) float *)(fp32 ? pb->xr32 : nullptr);
+        v.mc = (__attribute__((address_space(1))) c64 *)mc;
+        v.lmc = lmc;
+        v.lml = lml;
+        v.s0 = s0;
+        v.doff = doff;
+        v.foff = foff;
+        v.m5 = m5;
+        v.w5 = w5;
         return v;
     }
     typedef __attribute__((address_space(1))) c64 gmc64;
     static __device__ __forceinline__ c64 ld(gc64 *p) { return c64{p->re, p->im}; }
+    // the streamed per-series arrays (series, phasor column, model cache): non-temporal with
+    // -DGPD_EXACT_NT=1 (A/B), so that the shared phases and states keep their L2 lines
+    typedef double nv2d __attribute__((ext_vector_type(2)));
+    static __device__ __forceinline__ c64 ld_s(gc64 *p) {
+#if defined(GPD_EXACT_NT) && GPD_EXACT_NT
+        const nv2d v = __builtin_nontemporal_load((const __attribute__((address_space(1))) nv2d *)p);
+        return c64{v.x, v.y};
+#else
+        return c64{p->re, p->im};
+#endif
+    }
     // weight of a valid sample (FAINT: w of its state; the power m is inside the cached model)
-    __device__ __forceinline__ double weight_of(int st) const {
+    static __device__ __forceinline__ double weight_of(const View &v, int st) {
         if (!FAINT) return 1.0;
-        double ww = w5[0];
+        double ww = v.w5[0];
 #pragma unroll
-        for (int q = 1; q < 5; ++q) ww = (st + 1 == q) ? w5[q] : ww;
+        for (int q = 1; q < 5; ++q) ww = (st + 1 == q) ? v.w5[q] : ww;
         return ww;
     }
     static __device__ __forceinline__ c64 ld(gc32 *p) { return c64{(double)p->re, (double)p->im}; }
     __device__ __forceinline__ c64 d_of(const View &v, long long off) const {
-        return v.d32 ? ld(v.d32 + off) : ld(v.d + off);
+        return v.d32 ? ld(v.d32 + off) : ld_s(v.d + off);
     }
     // sample_valid (TRANSIENT dropped, onlyhigh keeps HIGH ∪ NORMAL), src/Modulation.jl:373-382
     __device__ __forceinline__ bool valid(const View &v, long long i, int &st) const {
@@ -2675,13 +2702,13 @@ struct ExactChi2 {
         int st;
         if (!valid(v, i, st)) return false;
         const c64 ph = PHBUF ? ld(v.src + i)
-                             : fc_phasor(v.fc32 ? ld(v.fc32 + foff + i) : ld(v.fc + foff + i));
+                             : fc_phasor(v.fc32 ? ld(v.fc32 + v.foff + i) : ld(v.fc + v.foff + i));
         if (FAINT) {
-            double m = m5[0], ww = w5[0];
+            double m = v.m5[0], ww = v.w5[0];
 #pragma unroll
             for (int q = 1; q < 5; ++q) {
-                m = (st + 1 == q) ? m5[q] : m;
-                ww = (st + 1 == q) ? w5[q] : ww;
+                m = (st + 1 == q) ? v.m5[q] : m;
+                ww = (st + 1 == q) ? v.w5[q] : ww;
             }
             p = {m * ph.re, m * ph.im};  // power .* FCphasor (src/Modulation.jl:396)
             w = ww;
@@ -2702,32 +2729,36 @@ struct ExactChi2 {
     __device__ __forceinline__ void load_raw(const View &v, long long i, Raw &r) const {
         r.st = v.state ? (int)v.state[i] : 0;
         r.t = v.xr ? (double)v.xr[i] : v.t[i];  // F_FP32: the reduced phase instead of t
-        r.f = PHBUF ? ld(v.src + i) : (v.fc32 ? ld(v.fc32 + foff + i) : ld(v.fc + foff + i));
-        r.d = d_of(v, doff + i);
+        r.f = PHBUF ? ld_s(v.src + i) : (v.fc32 ? ld(v.fc32 + v.foff + i) : ld_s(v.fc + v.foff + i));
+        r.d = d_of(v, v.doff + i);
     }
     __device__ __forceinline__ void load_res(const View &v, long long i, Raw &r) const {
         r.st = v.state ? (int)v.state[i] : 0;
-        const int mm = (int)((i - s0) >> 11);  // wave-uniform: the chain's sample index
-        if (mm < lml) {
-            const __attribute__((address_space(3))) c64 *q = lmc + mm * WGT + (int)threadIdx.x;
+        const long long e = i - v.s0;
+        const int mm = (int)(e >> 11);  // wave-uniform: the chain's sample index
+        if (mm < v.lml) {
+            const __attribute__((address_space(3))) c64 *q = v.lmc + mm * WGT + (int)threadIdx.x;
             r.f = c64{q->re, q->im};
         } else {
-            const gmc64 *mcg = (const gmc64 *)mc;
-            r.f = c64{mcg[i - s0].re, mcg[i - s0].im};
+            r.f = ld_s(v.mc + e);
         }
-        r.d = d_of(v, doff + i);
+        r.d = d_of(v, v.doff + i);
     }
     // the first pass's store of sample i's model into the cache (LDS head or global slot)
-    __device__ __forceinline__ void mc_put(long long i, const c64 &m) const {
-        const int mm = (int)((i - s0) >> 11);
-        if (mm < lml) {
-            __attribute__((address_space(3))) c64 *q = lmc + mm * WGT + (int)threadIdx.x;
+    __device__ __forceinline__ static void mc_put(const View &v, long long i, const c64 &m) {
+        const long long e = i - v.s0;
+        const int mm = (int)(e >> 11);
+        if (mm < v.lml) {
+            __attribute__((address_space(3))) c64 *q = v.lmc + mm * WGT + (int)threadIdx.x;
             q->re = m.re;
             q->im = m.im;
         } else {
-            gmc64 *mcg = (gmc64 *)mc;
-            mcg[i - s0].re = m.re;
-            mcg[i - s0].im = m.im;
+#if defined(GPD_EXACT_NT) && GPD_EXACT_NT
+            __builtin_nontemporal_store(nv2d{m.re, m.im}, (__attribute__((address_space(1))) nv2d *)(v.mc + e));
+#else
+            v.mc[e].re = m.re;
+            v.mc[e].im = m.im;
+#endif
         }
     }
     // sample_valid on a loaded state (TRANSIENT dropped, onlyhigh keeps HIGH ∪ NORMAL)
@@ -2738,14 +2769,14 @@ struct ExactChi2 {
         return true;
     }
     // load() on a loaded sample: power·phasor and weight
-    __device__ __forceinline__ void pw_of(const Raw &r, c64 &p, double &w) const {
+    static __device__ __forceinline__ void pw_of(const View &v, const Raw &r, c64 &p, double &w) {
         const c64 ph = PHBUF ? r.f : fc_phasor(r.f);
         if (FAINT) {
-            double m = m5[0], ww = w5[0];
+            double m = v.m5[0], ww = v.w5[0];
 #pragma unroll
             for (int q = 1; q < 5; ++q) {
-                m = (r.st + 1 == q) ? m5[q] : m;
-                ww = (r.st + 1 == q) ? w5[q] : ww;
+                m = (r.st + 1 == q) ? v.m5[q] : m;
+                ww = (r.st + 1 == q) ? v.w5[q] : ww;
             }
             p = {m * ph.re, m * ph.im};  // power .* FCphasor (src/Modulation.jl:396)
             w = ww;
@@ -2759,13 +2790,13 @@ struct ExactChi2 {
     // regime's branch-free form runs for all U in one basic block; otherwise the general
     // functions.  Either way each sample's model has model()'s bits (gpd_jlmath.h).
     template <int U>
-    __device__ __forceinline__ void model_batch(const Raw (&X)[U], double b, double phi,
-                                                c64 (&m)[U]) const {
+    __device__ __forceinline__ void model_batch(const View &v, const Raw (&X)[U], double b,
+                                                double phi, c64 (&m)[U]) const {
         double th[U], s[U], be[U];
         int ph = 1, cw = 1, sm = 1;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            th[u] = pb->omega * X[u].t;
+            th[u] = v.omega * X[u].t;
             th[u] = th[u] + phi;
             ph &= jlm_sin_ph_in(th[u]);
             cw &= jlm_sin_cwx_in(th[u]);
@@ -2814,7 +2845,7 @@ struct ExactChi2 {
         for (int u = 0; u < U; ++u) {
             c64 p;
             double w;
-            pw_of(X[u], p, w);
+            pw_of(v, X[u], p, w);
             m[u] = cmul(p, e[u]);  // power * exp(ȷ b sin(ωt+ϕ)) (src/Modulation.jl:137)
         }
     }
@@ -2837,8 +2868,10 @@ struct ExactChi2 {
     static __device__ __forceinline__ f2 fmul2(f2 a, f2 b) {
         return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
     }
-    __device__ __forceinline__ float weight32(int st) const { return (float)weight_of(st); }
-    __device__ __forceinline__ f2 power_phasor32(const Raw &r) const {
+    static __device__ __forceinline__ float weight32(const View &v, int st) {
+        return (float)weight_of(v, st);
+    }
+    static __device__ __forceinline__ f2 power_phasor32(const View &v, const Raw &r) {
         const float fr = (float)r.f.re, fi = (float)r.f.im;
         f2 ph;
         if (PHBUF) {  // the phasor buffer holds the Float64 phasor
@@ -2848,9 +2881,9 @@ struct ExactChi2 {
             ph = {fr * inv, fi * inv};
         }
         if (FAINT) {
-            double m = m5[0];
+            double m = v.m5[0];
 #pragma unroll
-            for (int q = 1; q < 5; ++q) m = (r.st + 1 == q) ? m5[q] : m;
+            for (int q = 1; q < 5; ++q) m = (r.st + 1 == q) ? v.m5[q] : m;
             const float mf = (float)m;
             ph = {mf * ph.re, mf * ph.im};
         }
@@ -2883,12 +2916,12 @@ struct ExactChi2 {
         return fmul2(p, f2{cs, sn});
     }
     template <int U>
-    __device__ __forceinline__ void model_batch32(const Raw (&X)[U], double b, double phi,
-                                                  c64 (&m)[U]) const {
+    __device__ __forceinline__ void model_batch32(const View &v, const Raw (&X)[U], double b,
+                                                  double phi, c64 (&m)[U]) const {
         const float bf = (float)b, pf = (float)phi;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const f2 mm = model32((float)X[u].t, power_phasor32(X[u]), bf, pf);
+            const f2 mm = model32((float)X[u].t, power_phasor32(v, X[u]), bf, pf);
             m[u] = c64{(double)mm.re, (double)mm.im};
         }
     }
@@ -3086,13 +3119,13 @@ struct ExactChi2 {
             double v[8];  // a11, a12(2), a22, b1(2), b2(2)
             cr_sum2m<8>(
                 [&](long long i, Raw &r) { load_raw(V, i, r); },
-                [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch(X, b, phi, mb); },
+                [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch(V, X, b, phi, mb); },
                 [&](long long i, const Raw &r, const c64 &m, double (&a)[8]) {
                     if (!valid_st(V, r.st)) return;
                     c64 p;
                     double w;
-                    pw_of(r, p, w);
-                    if (mcg) mc_put(i, m);
+                    pw_of(V, r, p, w);
+                    if (mcg) mc_put(V, i, m);
                     const c64 dd = r.d;
                     a[0] += w;
                     a[1] += w * m.re;
@@ -3122,11 +3155,11 @@ struct ExactChi2 {
             double v[4];  // num(2), den(2): Float32 products, Float64 sums
             cr_sum2m<4>(
                 [&](long long i, Raw &r) { load_raw(V, i, r); },
-                [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch32(X, b, phi, mb); },
+                [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch32(V, X, b, phi, mb); },
                 [&](long long i, const Raw &r, const c64 &m, double (&a)[4]) {
                     if (!valid_st(V, r.st)) return;
-                    if (mcg) mc_put(i, m);
-                    const float w = weight32(r.st);
+                    if (mcg) mc_put(V, i, m);
+                    const float w = weight32(V, r.st);
                     const f2 m2 = {(float)m.re, (float)m.im}, d2 = {(float)r.d.re, (float)r.d.im};
                     const f2 mwc = {m2.re * w, -(m2.im * w)};
                     const f2 xv = fmul2(mwc, d2), yv = fmul2(mwc, m2);
@@ -3144,13 +3177,13 @@ struct ExactChi2 {
             double v[4];  // num(2), den(2)
             cr_sum2m<4>(
                 [&](long long i, Raw &r) { load_raw(V, i, r); },
-                [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch(X, b, phi, mb); },
+                [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch(V, X, b, phi, mb); },
                 [&](long long i, const Raw &r, const c64 &m, double (&a)[4]) {
                     if (!valid_st(V, r.st)) return;
                     c64 p;
                     double w;
-                    pw_of(r, p, w);
-                    if (mcg) mc_put(i, m);
+                    pw_of(V, r, p, w);
+                    if (mcg) mc_put(V, i, m);
                     const c64 mwc = {m.re * w, -(m.im * w)};  // conj(model .* weight)
                     const c64 xv = cmul(mwc, r.d);
                     const c64 yv = cmul(mwc, m);
@@ -3191,16 +3224,16 @@ struct ExactChi2 {
                                   [&](long long i, const Raw &r, double (&a)[1]) {
                                       if (!valid_st(V, r.st)) return;
                                       resid32(f2{(float)r.f.re, (float)r.f.im}, r.d,
-                                              weight32(r.st), a);
+                                              weight32(V, r.st), a);
                                   },
                                   s);
             } else {
                 cr_sum2<1, UR>([&](long long i, Raw &r) { load_raw(V, i, r); },
                                   [&](long long i, const Raw &r, double (&a)[1]) {
                                       if (!valid_st(V, r.st)) return;
-                                      const f2 m2 = model32((float)r.t, power_phasor32(r),
+                                      const f2 m2 = model32((float)r.t, power_phasor32(V, r),
                                                             (float)b, (float)phi);
-                                      resid32(m2, r.d, weight32(r.st), a);
+                                      resid32(m2, r.d, weight32(V, r.st), a);
                                   },
                                   s);
             }
@@ -3208,7 +3241,7 @@ struct ExactChi2 {
             cr_sum2<1, UR>([&](long long i, Raw &r) { load_res(V, i, r); },
                        [&](long long i, const Raw &r, double (&a)[1]) {
                            if (!valid_st(V, r.st)) return;
-                           resid(r.f, r.d, weight_of(r.st), a);
+                           resid(r.f, r.d, weight_of(V, r.st), a);
                        },
                        s);
         } else {
@@ -3217,7 +3250,7 @@ struct ExactChi2 {
                     c64 p;
                     double w;
                     if (!load(V, i, p, w)) return;
-                    resid(model(V, i, p, b, phi), d_of(V, doff + i), w, a);
+                    resid(model(V, i, p, b, phi), d_of(V, V.doff + i), w, a);
                 },
                 s);
         }

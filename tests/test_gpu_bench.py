@@ -13,7 +13,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def test_bench_json_contract():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--pixels", "512",
-                        "--samples", "8192", "--steps", "2", "--warmup", "1", "--cpu-pixels", "16"],
+                        "--samples", "8192", "--steps", "2", "--warmup", "1", "--cpu-pixels", "16",
+                        "--sustain", "0.3"],
                        capture_output=True, text=True, timeout=110, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -32,6 +33,8 @@ def test_bench_json_contract():
     cb = out["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0
     assert out["fits"]["nan"] == 0
+    su = out["sustained"]
+    assert su["steps"] >= 10 and su["ms_per_step_min"] <= su["ms_per_step_mean"] <= su["ms_per_step_max"]
 
 
 def _run_bench(nproc, extra, tmp, tag, backend="gloo", launcher=None):

@@ -426,15 +426,15 @@ def test_one_exposure_exact_every_split(gpu, oracle, monkeypatch, fitoffsets):
     B = _exposure(100_000, seed=42, offsets=fitoffsets)
     ref = oracle_fit(oracle, B, fitoffsets=fitoffsets)
     recs = {}
-    # "8-global": G = 8 with the whole model cache in global memory (GPD_EXACT_LMC=0) instead
-    # of the chains' heads in LDS (the default at G = 8)
-    for G in ("1", "2", "4", "8", "8-global", None):
+    # "8-lds": G = 8 with the head of every chain's model cache in LDS (GPD_EXACT_LMC=1, opt-in)
+    # instead of the whole cache in global memory
+    for G in ("1", "2", "4", "8", "8-lds", None):
         if G is None:
             monkeypatch.delenv("GPD_EXACT_G", raising=False)
         else:
             monkeypatch.setenv("GPD_EXACT_G", G[:1])
-        if G == "8-global":
-            monkeypatch.setenv("GPD_EXACT_LMC", "0")
+        if G == "8-lds":
+            monkeypatch.setenv("GPD_EXACT_LMC", "1")
         else:
             monkeypatch.delenv("GPD_EXACT_LMC", raising=False)
         fit(gpu, B, fitoffsets=fitoffsets, method="exact")  # warm (workspace)
@@ -466,8 +466,8 @@ def test_exact_cohort_form_records_bitwise(gpu, oracle, monkeypatch, faint, fito
     monkeypatch.setenv("GPD_EXACT_COHORT", "1")
     coh = fit(gpu, B, method="exact", state=st, fitoffsets=fitoffsets)
     assert coh.tobytes() == base.tobytes()
-    # the cohort form with the whole model cache in global memory (two workgroups per CU)
-    monkeypatch.setenv("GPD_EXACT_LMC", "0")
+    # the cohort form with the chains' heads of the model cache in LDS (one workgroup per CU)
+    monkeypatch.setenv("GPD_EXACT_LMC", "1")
     cog = fit(gpu, B, method="exact", state=st, fitoffsets=fitoffsets)
     monkeypatch.delenv("GPD_EXACT_LMC")
     assert cog.tobytes() == base.tobytes()

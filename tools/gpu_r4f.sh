@@ -5,7 +5,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd "$R"
-O=gpurun_out/r4f
+O=gpurun_out/${TAG:-r4f}
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shards.py tests/test_gpu_faint_stats.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
