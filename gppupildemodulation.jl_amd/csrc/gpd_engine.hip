@@ -962,6 +962,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             // GPD_XSPIN_TEST=1 (tests): the per-series barrier gives up at once (poison path)
             if (getenv("GPD_XSPIN_TEST") && atoi(getenv("GPD_XSPIN_TEST")) > 0) pb.flags |= F_XSPIN_TEST;
         }
+        // GPD_EXACT_FAST=0 (A/B, tests): the evaluator's general load path everywhere
+        if (getenv("GPD_EXACT_FAST") && atoi(getenv("GPD_EXACT_FAST")) == 0) pb.flags |= F_NOFAST;
         // GPD_FIT_PROF (diagnostics): per-phase cycles of the multi-workgroup exact fit
         static const bool xprof = getenv("GPD_FIT_PROF") != nullptr;
         if (xprof && exact_g > 1 && !bphi) {

@@ -58,6 +58,8 @@ constexpr uint32_t F_PROF = 0x80000000u;  // internal: k_fit_harmonic cycle spli
 // internal (tests, GPD_XSPIN_TEST=1): the multi-workgroup exact fit's barrier gives up at once
 // instead of after ~1 s, so the give-up path (poisoned series, GPD_ST_SYNC) runs on demand
 constexpr uint32_t F_XSPIN_TEST = 0x40000000u;
+// internal (A/B, tests): the exact evaluator's general load path even where FAST applies
+constexpr uint32_t F_NOFAST = 0x20000000u;
 // Diagnostic cycle counters (GPD_FIT_PROF, GPD_MOMENTS=ws_prof) live in the workspace, reached
 // through Problem::prof: [0..3] fit split (objective, whole fit, evals, exact exchange),
 // [8..15] moment-kernel roles, [16..31] NEWUOA phases (diagnostics build: lane- and wave-level)
@@ -2583,6 +2585,9 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 // WGT: threads per series — EXACT_WG (256: thread t owns slot t of each canonical block), or 64
 // for short spans (k_fit_exact with WGT = 64: lane l owns the block's slots l, l+64, l+128,
 // l+192 and reduces them as block_sum's four waves would — the same sums, one wave per series).
+#ifndef GPD_EXACT_NT
+#define GPD_EXACT_NT 1
+#endif
 template <bool FAINT, bool OFFS, bool PHBUF, int UR = CR_UR, int WGT = EXACT_WG>
 struct ExactChi2 {
     static constexpr bool kOffs = OFFS;
@@ -2664,11 +2669,12 @@ struct ExactChi2 {
     }
     typedef __attribute__((address_space(1))) c64 gmc64;
     static __device__ __forceinline__ c64 ld(gc64 *p) { return c64{p->re, p->im}; }
-    // the streamed per-series arrays (series, phasor column, model cache): non-temporal with
-    // -DGPD_EXACT_NT=1 (A/B), so that the shared phases and states keep their L2 lines
+    // the streamed per-series arrays (series, phasor column, model cache): non-temporal, so
+    // that the shared phases and states keep their L2 lines (r4: C5 exact 302-306 → 287-288 ms;
+    // -DGPD_EXACT_NT=0 for plain loads and stores)
     typedef double nv2d __attribute__((ext_vector_type(2)));
     static __device__ __forceinline__ c64 ld_s(gc64 *p) {
-#if defined(GPD_EXACT_NT) && GPD_EXACT_NT
+#if GPD_EXACT_NT
         const nv2d v = __builtin_nontemporal_load((const __attribute__((address_space(1))) nv2d *)p);
         return c64{v.x, v.y};
 #else
@@ -2726,13 +2732,33 @@ struct ExactChi2 {
         double t;
         int st;
     };
+    // FAST (r4): ComplexF64 storage, Float64 arithmetic, no LDS model cache, and the state
+    // array present exactly when FAINT — every load of a sample unconditional, so that the
+    // compiler counts the prefetched batch's loads exactly and waits only for the batch in use
+    // (with the runtime storage / fp32 / state selects it fell back to waiting for all
+    // outstanding loads on every path that might skip one).
+    template <bool FAST = false>
     __device__ __forceinline__ void load_raw(const View &v, long long i, Raw &r) const {
+        if constexpr (FAST) {
+            r.st = FAINT ? (int)v.state[i] : 0;
+            r.t = v.t[i];
+            r.f = PHBUF ? ld_s(v.src + i) : ld_s(v.fc + v.foff + i);
+            r.d = ld_s(v.d + v.doff + i);
+            return;
+        }
         r.st = v.state ? (int)v.state[i] : 0;
         r.t = v.xr ? (double)v.xr[i] : v.t[i];  // F_FP32: the reduced phase instead of t
         r.f = PHBUF ? ld_s(v.src + i) : (v.fc32 ? ld(v.fc32 + v.foff + i) : ld_s(v.fc + v.foff + i));
         r.d = d_of(v, v.doff + i);
     }
+    template <bool FAST = false>
     __device__ __forceinline__ void load_res(const View &v, long long i, Raw &r) const {
+        if constexpr (FAST) {
+            r.st = FAINT ? (int)v.state[i] : 0;
+            r.f = ld_s(v.mc + (i - v.s0));
+            r.d = ld_s(v.d + v.doff + i);
+            return;
+        }
         r.st = v.state ? (int)v.state[i] : 0;
         const long long e = i - v.s0;
         const int mm = (int)(e >> 11);  // wave-uniform: the chain's sample index
@@ -2745,15 +2771,16 @@ struct ExactChi2 {
         r.d = d_of(v, v.doff + i);
     }
     // the first pass's store of sample i's model into the cache (LDS head or global slot)
+    template <bool FAST = false>
     __device__ __forceinline__ static void mc_put(const View &v, long long i, const c64 &m) {
         const long long e = i - v.s0;
         const int mm = (int)(e >> 11);
-        if (mm < v.lml) {
+        if (!FAST && mm < v.lml) {
             __attribute__((address_space(3))) c64 *q = v.lmc + mm * WGT + (int)threadIdx.x;
             q->re = m.re;
             q->im = m.im;
         } else {
-#if defined(GPD_EXACT_NT) && GPD_EXACT_NT
+#if GPD_EXACT_NT
             __builtin_nontemporal_store(nv2d{m.re, m.im}, (__attribute__((address_space(1))) nv2d *)(v.mc + e));
 #else
             v.mc[e].re = m.re;
@@ -2762,8 +2789,9 @@ struct ExactChi2 {
         }
     }
     // sample_valid on a loaded state (TRANSIENT dropped, onlyhigh keeps HIGH ∪ NORMAL)
+    template <bool FAST = false>
     __device__ __forceinline__ bool valid_st(const View &v, int st) const {
-        if (v.state == nullptr) return true;
+        if (FAST ? !FAINT : v.state == nullptr) return true;
         if (st == -1) return false;
         if (v.only_high) return st == 3 || st == 2;
         return true;
@@ -3111,21 +3139,26 @@ struct ExactChi2 {
 
     __device__ double operator()(const double (&xx)[2]) {
         ++nfev;
-        const double b = xx[0], phi = xx[1];
         const View V = view();
+        const bool fast = V.d32 == nullptr && V.fc32 == nullptr && !fp32 && V.lml == 0 &&
+                          (FAINT == (V.state != nullptr)) && !(pb->flags & F_NOFAST);
+        return fast ? eval<true>(V, xx[0], xx[1]) : eval<false>(V, xx[0], xx[1]);
+    }
+    template <bool FAST>
+    __device__ __forceinline__ double eval(const View &V, const double b, const double phi) {
         const bool mcg = mc != nullptr || lml > 0;  // a model cache (global and/or LDS)
         const unsigned long long tp0 = prof ? __builtin_amdgcn_s_memtime() : 0;
         if (OFFS) {
             double v[8];  // a11, a12(2), a22, b1(2), b2(2)
             cr_sum2m<8>(
-                [&](long long i, Raw &r) { load_raw(V, i, r); },
+                [&](long long i, Raw &r) { load_raw<FAST>(V, i, r); },
                 [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch(V, X, b, phi, mb); },
                 [&](long long i, const Raw &r, const c64 &m, double (&a)[8]) {
-                    if (!valid_st(V, r.st)) return;
+                    if (!valid_st<FAST>(V, r.st)) return;
                     c64 p;
                     double w;
                     pw_of(V, r, p, w);
-                    if (mcg) mc_put(V, i, m);
+                    if (mcg) mc_put<FAST>(V, i, m);
                     const c64 dd = r.d;
                     a[0] += w;
                     a[1] += w * m.re;
@@ -3151,14 +3184,14 @@ struct ExactChi2 {
             c_im = cc.im;
             a_re = aa.re;
             a_im = aa.im;
-        } else if (fp32) {
+        } else if (!FAST && fp32) {
             double v[4];  // num(2), den(2): Float32 products, Float64 sums
             cr_sum2m<4>(
-                [&](long long i, Raw &r) { load_raw(V, i, r); },
+                [&](long long i, Raw &r) { load_raw<FAST>(V, i, r); },
                 [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch32(V, X, b, phi, mb); },
                 [&](long long i, const Raw &r, const c64 &m, double (&a)[4]) {
-                    if (!valid_st(V, r.st)) return;
-                    if (mcg) mc_put(V, i, m);
+                    if (!valid_st<FAST>(V, r.st)) return;
+                    if (mcg) mc_put<FAST>(V, i, m);
                     const float w = weight32(V, r.st);
                     const f2 m2 = {(float)m.re, (float)m.im}, d2 = {(float)r.d.re, (float)r.d.im};
                     const f2 mwc = {m2.re * w, -(m2.im * w)};
@@ -3176,14 +3209,14 @@ struct ExactChi2 {
         } else {
             double v[4];  // num(2), den(2)
             cr_sum2m<4>(
-                [&](long long i, Raw &r) { load_raw(V, i, r); },
+                [&](long long i, Raw &r) { load_raw<FAST>(V, i, r); },
                 [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch(V, X, b, phi, mb); },
                 [&](long long i, const Raw &r, const c64 &m, double (&a)[4]) {
-                    if (!valid_st(V, r.st)) return;
+                    if (!valid_st<FAST>(V, r.st)) return;
                     c64 p;
                     double w;
                     pw_of(V, r, p, w);
-                    if (mcg) mc_put(V, i, m);
+                    if (mcg) mc_put<FAST>(V, i, m);
                     const c64 mwc = {m.re * w, -(m.im * w)};  // conj(model .* weight)
                     const c64 xv = cmul(mwc, r.d);
                     const c64 yv = cmul(mwc, m);
@@ -3212,7 +3245,7 @@ struct ExactChi2 {
             const double rr = mm.re - dd.re, ri = mm.im - dd.im;
             a[0] += w * (rr * rr + ri * ri);
         };
-        if (fp32) {  // Float32 residual, Float64 sum
+        if (!FAST && fp32) {  // Float32 residual, Float64 sum
             const f2 a2 = {(float)a_re, (float)a_im};
             auto resid32 = [&](const f2 &m2, const c64 &dd, float w, double (&a)[1]) {
                 const f2 mm = fmul2(a2, m2);
@@ -3220,17 +3253,17 @@ struct ExactChi2 {
                 a[0] += (double)(w * (rr * rr + ri * ri));
             };
             if (mcg) {
-                cr_sum2<1, UR>([&](long long i, Raw &r) { load_res(V, i, r); },
+                cr_sum2<1, UR>([&](long long i, Raw &r) { load_res<FAST>(V, i, r); },
                                   [&](long long i, const Raw &r, double (&a)[1]) {
-                                      if (!valid_st(V, r.st)) return;
+                                      if (!valid_st<FAST>(V, r.st)) return;
                                       resid32(f2{(float)r.f.re, (float)r.f.im}, r.d,
                                               weight32(V, r.st), a);
                                   },
                                   s);
             } else {
-                cr_sum2<1, UR>([&](long long i, Raw &r) { load_raw(V, i, r); },
+                cr_sum2<1, UR>([&](long long i, Raw &r) { load_raw<FAST>(V, i, r); },
                                   [&](long long i, const Raw &r, double (&a)[1]) {
-                                      if (!valid_st(V, r.st)) return;
+                                      if (!valid_st<FAST>(V, r.st)) return;
                                       const f2 m2 = model32((float)r.t, power_phasor32(V, r),
                                                             (float)b, (float)phi);
                                       resid32(m2, r.d, weight32(V, r.st), a);
@@ -3238,9 +3271,9 @@ struct ExactChi2 {
                                   s);
             }
         } else if (mcg) {  // the model the same thread wrote for element i in the first pass
-            cr_sum2<1, UR>([&](long long i, Raw &r) { load_res(V, i, r); },
+            cr_sum2<1, UR>([&](long long i, Raw &r) { load_res<FAST>(V, i, r); },
                        [&](long long i, const Raw &r, double (&a)[1]) {
-                           if (!valid_st(V, r.st)) return;
+                           if (!valid_st<FAST>(V, r.st)) return;
                            resid(r.f, r.d, weight_of(V, r.st), a);
                        },
                        s);

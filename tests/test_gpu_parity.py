@@ -475,6 +475,30 @@ def test_exact_cohort_form_records_bitwise(gpu, oracle, monkeypatch, faint, fito
     print(assert_exact_bitwise(coh, ref, label=f"exact cohort faint={faint} offsets={fitoffsets}"))
 
 
+@pytest.mark.parametrize("faint,fitoffsets", [(False, False), (True, False), (False, True)])
+def test_exact_fast_loads_equal_the_general_path(gpu, oracle, monkeypatch, faint, fitoffsets):
+    """The exact evaluator's FAST form (ComplexF64 storage, Float64 arithmetic: every sample's
+    loads unconditional, r4) and its general form (runtime storage / state selects,
+    GPD_EXACT_FAST=0) give the same records, bit for bit, and those are the oracle's."""
+    P, N = 64, 9000
+    B = synth.make_batch(N, P, seed=91, offsets=fitoffsets)
+    st = None
+    if faint:
+        st = np.full(N, 2, dtype=np.int8)
+        st[700:2100] = 3
+        st[5000:6100] = 1
+        st[2095:2110] = -1
+        B["d"] = B["d"] * np.where(st == 3, 1.1, np.where(st == 1, 0.3, 0.6))[None, :]
+    monkeypatch.delenv("GPD_EXACT_FAST", raising=False)
+    fast = fit(gpu, B, method="exact", state=st, fitoffsets=fitoffsets)
+    monkeypatch.setenv("GPD_EXACT_FAST", "0")
+    gen = fit(gpu, B, method="exact", state=st, fitoffsets=fitoffsets)
+    monkeypatch.delenv("GPD_EXACT_FAST")
+    assert fast.tobytes() == gen.tobytes()
+    ref = oracle_fit(oracle, B, state=st, fitoffsets=fitoffsets)
+    print(assert_exact_bitwise(fast, ref, label=f"exact fast faint={faint} offsets={fitoffsets}"))
+
+
 @pytest.mark.parametrize("xinit,b_range", [(None, (0.3, 2.5)), ((8.0, 0.3), (0.3, 2.5)),
                                            (None, (6.0, 7.5))])
 def test_exact_model_regime_boundaries(gpu, oracle, xinit, b_range):

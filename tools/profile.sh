@@ -13,9 +13,9 @@ export TMPDIR=/tmp
 cd /tmp
 ARGS=("$@")
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- \
-    python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu --no-f64 --no-c4 "${ARGS[@]}" > "$OUT/bench_trace.json"
+    python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu --no-f64 --no-c4 --sustain 0 "${ARGS[@]}" > "$OUT/bench_trace.json"
 timeout -k 10 500 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_moments -f csv -d "$OUT/pmc_fetch" -o pmc -- \
-    python3 "$R/bench.py" --steps 2 --warmup 0 --no-cpu --no-f64 --no-c4 "${ARGS[@]}" > "$OUT/bench_pmc_fetch.json"
+    python3 "$R/bench.py" --steps 2 --warmup 0 --no-cpu --no-f64 --no-c4 --sustain 0 "${ARGS[@]}" > "$OUT/bench_pmc_fetch.json"
 timeout -k 10 500 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_moments -f csv -d "$OUT/pmc_write" -o pmc -- \
-    python3 "$R/bench.py" --steps 2 --warmup 0 --no-cpu --no-f64 --no-c4 "${ARGS[@]}" > "$OUT/bench_pmc_write.json"
+    python3 "$R/bench.py" --steps 2 --warmup 0 --no-cpu --no-f64 --no-c4 --sustain 0 "${ARGS[@]}" > "$OUT/bench_pmc_write.json"
 find "$OUT" -name "*.csv" | sort
