@@ -442,14 +442,20 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     // the global cache (C2 exact 3.32 → 3.46 ms, the residual pass 2.05 → 2.49 M cycles per
     // workgroup; the C5 cohort form 375 → 486 ms at one workgroup per CU instead of two,
     // profiles/r4/exact_lmc/), so opt-in: GPD_EXACT_LMC=1.
-    const bool lmc_on = getenv("GPD_EXACT_LMC") && atoi(getenv("GPD_EXACT_LMC")) == 1;
+    bool lmc_on = getenv("GPD_EXACT_LMC") && atoi(getenv("GPD_EXACT_LMC")) == 1;
+    // Split form (r4): at G = 8 every canonical chain shared by two threads of a 512-thread part
+    // (k_fit_exact WGT = 512, ExactChi2::cr_split_chain): two waves per SIMD where the G = 8
+    // form has one; the same records.  GPD_EXACT_SPLIT=0: the 256-thread parts.
+    const bool split_on = !(getenv("GPD_EXACT_SPLIT") && atoi(getenv("GPD_EXACT_SPLIT")) == 0) &&
+                          !fp32;
+    if (split_on) lmc_on = false;
     const char *coh = getenv("GPD_EXACT_COHORT");
     const int coh_mode = coh ? atoi(coh) : 0;
     if (want_exact && !bphi && window == 0 && exact_g == 1 && !fp32 && P * 8 > cx->n_cu &&
         coh_mode > 0 && N >= (long long)CR_SLOTS) {
         // cohort form: two 256-thread workgroups per CU (global model cache), or one with the
-        // LDS model cache
-        const long long cap = ((lmc_on ? 1LL : 2LL) * cx->n_cu) / 64 * 64;
+        // LDS model cache or in the split form
+        const long long cap = ((lmc_on || split_on ? 1LL : 2LL) * cx->n_cu) / 64 * 64;
         if (cap >= 64) {
             exact_g = 8;
             xgrid = (unsigned)cap;
@@ -476,6 +482,11 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         xlml = 0;
         xlds_bytes = 0;
     }
+    // the split form needs the model cache (its sums run through cr_sum2m only) and hands its
+    // terms over in 2 × CR_U × NV × 256 doubles of LDS (NV = 8 with offsets, 4 without)
+    const bool split = split_on && want_exact && !bphi && window == 0 && exact_g == CR_BLOCKS &&
+                       L.mstride != 0 && xlml == 0;
+    const size_t split_lds = split ? (size_t)2 * CR_U * (offs ? 8 : 4) * EXACT_WG * sizeof(double) : 0;
     if (cx->ws_cap < L.total) {
         if (cx->ws) {
             HIP_TRY(hipDeviceSynchronize());
@@ -997,7 +1008,15 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             k_fit_exact<FA, OF, PH, 2, 64><<<grid64, 64, 0, stream>>>(                         \
                 pb, info, ph, fstat, nullptr, nullptr, outp, raw, 0, nullptr, 0, 1, nullptr,    \
                 nullptr);                                                                       \
-        else if (two_waves)                                                                     \
+        else if (split) {                                                                       \
+            HIP_TRY(hipFuncSetAttribute((const void *)k_fit_exact<FA, OF, PH, 1, 2 * EXACT_WG>,  \
+                                        hipFuncAttributeMaxDynamicSharedMemorySize,              \
+                                        (int)split_lds));                                        \
+            k_fit_exact<FA, OF, PH, 1, 2 * EXACT_WG><<<fit_grid, 2 * EXACT_WG, split_lds,       \
+                                                       stream>>>(                               \
+                pb, info, ph, fstat, nullptr, nullptr, outp, raw, 0, (c64 *)(ws + L.mcache),    \
+                L.mstride, exact_g, (double *)(ws + L.xtot), (unsigned *)(ws + L.xcnt), 0);     \
+        } else if (two_waves)                                                                   \
             k_fit_exact<FA, OF, PH, 2><<<fit_grid, EXACT_WG, 0, stream>>>(                    \
                 pb, info, ph, fstat, nullptr, nullptr, outp, raw, 0,                            \
                 L.mstride ? (c64 *)(ws + L.mcache) : nullptr, L.mstride, exact_g,               \

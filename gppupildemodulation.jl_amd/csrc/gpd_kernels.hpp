@@ -32,6 +32,7 @@
 #define GPD_U_MOM 0x44    // units 2, 6: k_moments_ws (Float64 / Float32 storage)
 #define GPD_U_EXACT 0xF198  // units 3, 4, 7, 8 / 12-15: k_fit_exact (faint × offsets, MINB 1 / 2)
 #define GPD_U_EXACT64 0xF0000  // units 16-19: k_fit_exact one wave per series (faint × offsets)
+#define GPD_U_EXACT512 0xF00000  // units 20-23: k_fit_exact split form, 512 threads per part
 #define GPD_U_CHI2X 0xE20  // units 5, 9, 10, 11: k_chi2_exact, k_refine_exact
 
 namespace gpd {
@@ -2609,6 +2610,8 @@ struct ExactChi2 {
     // the chain's later samples stay in the global slot mc).  lml = 0: all in mc.
     __attribute__((address_space(3))) c64 *lmc;
     int lml;
+    // the split form's (WGT = 512) term hand-over buffers in LDS: 2 × U × NV × 256 doubles
+    __attribute__((address_space(3))) double *xbuf;
     // multi-workgroup split: G workgroups per series, this one is g; x: the series' exchange
     int G, g;
     Xchg x;
@@ -3007,6 +3010,11 @@ struct ExactChi2 {
     template <int NV, class C>
     __device__ __forceinline__ void cr_sum_blocks(C &&chain, double (&tot)[NV]) {
         ldouble *lp = (ldouble *)lds;
+        if constexpr (WGT == 2 * EXACT_WG) {  // the split form sums through cr_sum2m only (the
+#pragma unroll                                // engine runs it with a model cache)
+            for (int k = 0; k < NV; ++k) tot[k] = __builtin_nan("");
+            return;
+        }
         if (sync_fail) {  // the series' barrier was poisoned: every part stops passing samples
 #pragma unroll
             for (int k = 0; k < NV; ++k) tot[k] = __builtin_nan("");
@@ -3058,17 +3066,29 @@ struct ExactChi2 {
             if (G == 1) {
 #pragma unroll
                 for (int k = 0; k < NV; ++k) tot[k] = (blk == 0) ? acc[k] : tot[k] + acc[k];
-            } else if (threadIdx.x < NV) {
-                double v = acc[0];
-#pragma unroll
-                for (int k = 1; k < NV; ++k) v = ((int)threadIdx.x == k) ? acc[k] : v;
-                gu64 *slot = (gu64 *)(x.tot + ((nbar + 1) & 1) * (CR_BLOCKS * CR_NV) +
-                                      blk * CR_NV + threadIdx.x);
-                __hip_atomic_store(slot, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                xpublish<NV>(blk, acc);
             }
         }
         if (G == 1) return;
+        xfinish<NV>(tot);
+    }
+    // G > 1: block blk's totals into the series' exchange slot of the next barrier
+    template <int NV>
+    __device__ __forceinline__ void xpublish(int blk, const double (&acc)[NV]) {
+        if (threadIdx.x < NV) {
+            double v = acc[0];
+#pragma unroll
+            for (int k = 1; k < NV; ++k) v = ((int)threadIdx.x == k) ? acc[k] : v;
+            gu64 *slot = (gu64 *)(x.tot + ((nbar + 1) & 1) * (CR_BLOCKS * CR_NV) +
+                                  blk * CR_NV + threadIdx.x);
+            __hip_atomic_store(slot, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    // G > 1: the series' barrier, then the 8 block totals added in block order
+    template <int NV>
+    __device__ __forceinline__ void xfinish(double (&tot)[NV]) {
         const unsigned long long tb = prof ? __builtin_amdgcn_s_memtime() : 0;
         xbarrier();
         if (prof) pc[2] += __builtin_amdgcn_s_memtime() - tb;
@@ -3103,6 +3123,10 @@ struct ExactChi2 {
     // in chain order.
     template <int NV, int U = CR_U, class L, class B, class A>
     __device__ __forceinline__ void cr_sum2m(L &&load, B &&batch, A &&accum, double (&tot)[NV]) {
+        if constexpr (WGT == 2 * EXACT_WG) {
+            cr_sum2m_split<NV, U>(load, batch, accum, tot);
+            return;
+        }
         cr_sum_blocks<NV>(
             [&](long long i0, double (&acc)[NV]) {
                 const int M = i0 < s1 ? (int)((s1 - 1 - i0) / CR_SLOTS + 1) : 0;
@@ -3135,6 +3159,111 @@ struct ExactChi2 {
                 if (m0 < M) run(A_, m0);
             },
             tot);
+    }
+    // The split form (r4, WGT = 512 threads per part, G = 8): canonical chain c = g·256 + t of
+    // the part (t = thread mod 256) is shared by thread t (h = 0: the chain's samples m = 0, 2,
+    // 4, …) and thread t + 256 (h = 1: m = 1, 3, 5, …).  Each evaluates its own samples' terms
+    // (accum into zeroed temporaries: a term x becomes 0.0 + x, which differs from x only for
+    // x = −0.0, and a chain sum is never −0.0, so adding either gives the same bits); thread
+    // t + 256 hands its terms over through LDS and thread t adds both in chain order.  Then the
+    // chains of waves 0-3 are reduced as block_sum<256> does (butterfly, then the four wave
+    // totals left to right) and exchanged with the other parts as in cr_sum_blocks — the G = 8
+    // sums, bit for bit, with two waves per SIMD instead of one.  Every thread runs the same
+    // number of iterations (bounded by the part's longest chain; loads of samples past a
+    // chain's end are clamped to the span's last sample and their terms discarded).
+    template <int NV, int U, class L, class B, class A>
+    __device__ __forceinline__ void cr_split_chain(L &&load, B &&batch, A &&accum,
+                                                   double (&acc)[NV]) {
+        const int t = (int)threadIdx.x & (EXACT_WG - 1), h = (int)threadIdx.x / EXACT_WG;
+        const long long c0 = s0 + (long long)g * EXACT_WG;  // the part's first chain
+        const long long i0 = c0 + t;
+        const int M = i0 < s1 ? (int)((s1 - 1 - i0) / CR_SLOTS + 1) : 0;
+        const int Mmax = c0 < s1 ? (int)((s1 - 1 - c0) / CR_SLOTS + 1) : 0;
+        const int J = (Mmax + 1) >> 1;  // sample pairs of the longest chain
+#pragma unroll
+        for (int k = 0; k < NV; ++k) acc[k] = 0.0;
+        ldouble *xb = xbuf;
+        Raw A_[U], B_[U];
+        auto issue = [&](Raw (&X)[U], int j0) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                long long i = i0 + (long long)(2 * (j0 + u) + h) * CR_SLOTS;
+                i = i < s1 ? i : s1 - 1;
+                load(i, X[u]);
+            }
+        };
+        int buf = 0;
+        auto run = [&](const Raw (&X)[U], int j0) {
+            c64 mb[U];
+            batch(X, mb);
+            double f[U][NV];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+#pragma unroll
+                for (int k = 0; k < NV; ++k) f[u][k] = 0.0;
+                const int m = 2 * (j0 + u) + h;
+                if (m < M) accum(i0 + (long long)m * CR_SLOTS, X[u], mb[u], f[u]);
+            }
+            ldouble *q = xb + buf * (U * NV * EXACT_WG);
+            if (h == 1) {
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int k = 0; k < NV; ++k) q[(u * NV + k) * EXACT_WG + t] = f[u][k];
+            }
+            __syncthreads();  // (double-buffered: the next writes go to the other buffer)
+            if (h == 0) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+#pragma unroll
+                    for (int k = 0; k < NV; ++k) acc[k] += f[u][k];
+#pragma unroll
+                    for (int k = 0; k < NV; ++k) acc[k] += q[(u * NV + k) * EXACT_WG + t];
+                }
+            }
+            buf ^= 1;
+        };
+        if (J == 0) return;
+        issue(A_, 0);
+        int j0 = 0;
+        for (; j0 + U < J; j0 += 2 * U) {
+            issue(B_, j0 + U);
+            run(A_, j0);
+            if (j0 + 2 * U < J) issue(A_, j0 + 2 * U);
+            run(B_, j0 + U);
+        }
+        if (j0 < J) run(A_, j0);
+    }
+    template <int NV, int U, class L, class B, class A>
+    __device__ __forceinline__ void cr_sum2m_split(L &&load, B &&batch, A &&accum, double (&tot)[NV]) {
+        ldouble *lp = (ldouble *)lds;
+        if (sync_fail) {
+#pragma unroll
+            for (int k = 0; k < NV; ++k) tot[k] = __builtin_nan("");
+            return;
+        }
+        double acc[NV];
+        cr_split_chain<NV, U>(load, batch, accum, acc);
+        // block_sum<256> over waves 0-3 (the chains' owners); waves 4-7 join the barriers
+        const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
+        if (wave < EXACT_WG / 64) {
+            wave_sum<NV>(acc);
+            if (lane == 0) {
+#pragma unroll
+                for (int k = 0; k < NV; ++k) lp[wave * NV + k] = acc[k];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            double sv = lp[k];
+#pragma unroll
+            for (int w = 1; w < EXACT_WG / 64; ++w) sv = sv + lp[w * NV + k];
+            acc[k] = sv;
+        }
+        __syncthreads();
+        xpublish<NV>(g, acc);
+        xfinish<NV>(tot);
     }
 
     __device__ double operator()(const double (&xx)[2]) {
@@ -3309,6 +3438,7 @@ __device__ __forceinline__ void setup_exact(F &f, const Problem &pb, long long k
     f.mc = nullptr;
     f.lmc = nullptr;
     f.lml = 0;
+    f.xbuf = nullptr;
     f.s0 = sp.s0;
     f.s1 = sp.s1;
     f.G = G;
@@ -3358,7 +3488,7 @@ __global__ __launch_bounds__(WGT, MINB) void k_fit_exact(Problem pb, const Info 
                                                         double *__restrict__ xtot = nullptr,
                                                         unsigned *__restrict__ xcnt = nullptr,
                                                         int lml = 0)
-#if GPD_OWNS(GPD_U_EXACT | GPD_U_EXACT64)
+#if GPD_OWNS(GPD_U_EXACT | GPD_U_EXACT64 | GPD_U_EXACT512)
 {
     __shared__ double lds[EXACT_LDS];
     // G = 8 with lml > 0: the head of every chain's model cache in dynamic LDS (lml·WGT c64)
@@ -3367,7 +3497,8 @@ __global__ __launch_bounds__(WGT, MINB) void k_fit_exact(Problem pb, const Info 
     // read/write the same addresses), instead of replicated in every thread's registers
     __shared__ Newuoa<2, 5, true> nwx[WGT / 64];
     const double nvalid = (double)info->nvalid;
-    if (WGT == EXACT_WG && G > 1) {  // one series per G workgroups (whole exposures, no list)
+    // WGT = 512: the split form (two threads per canonical chain), always G = 8 parts
+    if ((WGT == EXACT_WG && G > 1) || WGT == 2 * EXACT_WG) {  // one series per G workgroups
       // persistent over rounds of gridDim.x / G series (r4, large batches: gridDim.x = the
       // resident workgroups, a multiple of 8·G, so a series' G parts are in one round and move
       // on together; the series in flight — their samples and model cache slots — stay within
@@ -3382,10 +3513,11 @@ __global__ __launch_bounds__(WGT, MINB) void k_fit_exact(Problem pb, const Info 
         setup_exact(f, pb, k, PHBUF ? phbuf : nullptr, lds, nvalid, G, g,
                     Xchg{xtot + k * (2 * CR_BLOCKS * CR_NV), xcnt + k});
         if (mcache) f.mc = mcache + (k % per_round) * mstride;
-        if (G == CR_BLOCKS && lml > 0) {  // one chain per thread (one canonical block per part)
+        if (WGT == EXACT_WG && G == CR_BLOCKS && lml > 0) {  // one chain per thread
             f.lmc = (__attribute__((address_space(3))) c64 *)xlds_dyn;
             f.lml = lml;
         }
+        if (WGT == 2 * EXACT_WG) f.xbuf = (__attribute__((address_space(3))) double *)xlds_dyn;
         if (FAINT) {
 #pragma unroll
             for (int q = 0; q < 5; ++q) {

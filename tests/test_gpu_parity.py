@@ -426,17 +426,20 @@ def test_one_exposure_exact_every_split(gpu, oracle, monkeypatch, fitoffsets):
     B = _exposure(100_000, seed=42, offsets=fitoffsets)
     ref = oracle_fit(oracle, B, fitoffsets=fitoffsets)
     recs = {}
-    # "8-lds": G = 8 with the head of every chain's model cache in LDS (GPD_EXACT_LMC=1, opt-in)
-    # instead of the whole cache in global memory
-    for G in ("1", "2", "4", "8", "8-lds", None):
+    # G = 8 runs in the split form by default (512-thread parts, two threads per canonical
+    # chain); "8-unsplit": 256-thread parts (GPD_EXACT_SPLIT=0); "8-lds": those with the head of
+    # every chain's model cache in LDS (GPD_EXACT_LMC=1, opt-in)
+    for G in ("1", "2", "4", "8", "8-unsplit", "8-lds", None):
         if G is None:
             monkeypatch.delenv("GPD_EXACT_G", raising=False)
         else:
             monkeypatch.setenv("GPD_EXACT_G", G[:1])
+        monkeypatch.delenv("GPD_EXACT_LMC", raising=False)
+        monkeypatch.delenv("GPD_EXACT_SPLIT", raising=False)
+        if G in ("8-unsplit", "8-lds"):
+            monkeypatch.setenv("GPD_EXACT_SPLIT", "0")
         if G == "8-lds":
             monkeypatch.setenv("GPD_EXACT_LMC", "1")
-        else:
-            monkeypatch.delenv("GPD_EXACT_LMC", raising=False)
         fit(gpu, B, fitoffsets=fitoffsets, method="exact")  # warm (workspace)
         t0 = time.perf_counter()
         recs[G] = fit(gpu, B, fitoffsets=fitoffsets, method="exact")
@@ -466,10 +469,15 @@ def test_exact_cohort_form_records_bitwise(gpu, oracle, monkeypatch, faint, fito
     monkeypatch.setenv("GPD_EXACT_COHORT", "1")
     coh = fit(gpu, B, method="exact", state=st, fitoffsets=fitoffsets)
     assert coh.tobytes() == base.tobytes()
-    # the cohort form with the chains' heads of the model cache in LDS (one workgroup per CU)
+    # the cohort form in 256-thread parts (two per CU), and with the chains' heads of the model
+    # cache in LDS (one per CU); the default above is the split form (512-thread parts)
+    monkeypatch.setenv("GPD_EXACT_SPLIT", "0")
+    cog = fit(gpu, B, method="exact", state=st, fitoffsets=fitoffsets)
+    assert cog.tobytes() == base.tobytes()
     monkeypatch.setenv("GPD_EXACT_LMC", "1")
     cog = fit(gpu, B, method="exact", state=st, fitoffsets=fitoffsets)
     monkeypatch.delenv("GPD_EXACT_LMC")
+    monkeypatch.delenv("GPD_EXACT_SPLIT")
     assert cog.tobytes() == base.tobytes()
     ref = oracle_fit(oracle, B, state=st, fitoffsets=fitoffsets)
     print(assert_exact_bitwise(coh, ref, label=f"exact cohort faint={faint} offsets={fitoffsets}"))
