@@ -79,7 +79,21 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, jobs: 
     objdir = os.path.join(HERE, "build", variant or ("diag" if diag else "release"))
     os.makedirs(objdir, exist_ok=True)
     extra = (["-DGPD_DIAG"] if diag else []) + [f"-D{d}" for d in defines] + list(flags)
-    extra.append(f'-DGPD_BUILD_ID="{tree_id()}"')
+    # the build id is compiled into unit 0 only (gpd_build_id); an object whose inputs (the
+    # headers, its unit, the flags) are unchanged since its last compile is reused (.key file)
+    bid = f'-DGPD_BUILD_ID="{tree_id()}"'
+
+    def unit_key(src: str) -> str:
+        import hashlib
+
+        h = hashlib.sha256()
+        for f in [src] + HEADERS + ["gpd_part3.hip", "gpd_part16.hip", "gpd_part20.hip"]:
+            with open(os.path.join(CSRC, f), "rb") as fh:
+                h.update(f.encode() + b"\0" + fh.read())
+        with open(os.path.join(HERE, "..", "include", "gpdemod.h"), "rb") as fh:
+            h.update(fh.read())
+        h.update(" ".join([HIPCC, *FLAGS, *extra, bid if src == "gpd_engine.hip" else ""]).encode())
+        return h.hexdigest()
     jobs = jobs or max(1, min(len(SOURCES), os.cpu_count() or 1))
     procs, objs, errs = [], [], []
     pending = [u for u in SOURCES if not only or u in only]
@@ -96,14 +110,25 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, jobs: 
             raise RuntimeError("--only: release objects older than the headers (rebuild the "
                                "release library first): " + ", ".join(map(os.path.basename, stale)))
         objs += reuse
+    keys = {}
     while pending or procs:
         while pending and len(procs) < jobs:
             src = pending.pop(0)
             obj = os.path.join(objdir, src.replace(".hip", ".o"))
             objs.append(obj)
-            cmd = [HIPCC, *FLAGS, *extra, "-c", "-o", obj + ".tmp", os.path.join(CSRC, src)]
+            keys[src] = unit_key(src)
+            try:
+                with open(obj + ".key") as fh:
+                    if fh.read() == keys[src] and os.path.exists(obj):
+                        continue  # unchanged inputs: reuse the object
+            except OSError:
+                pass
+            ex = extra + ([bid] if src == "gpd_engine.hip" else [])
+            cmd = [HIPCC, *FLAGS, *ex, "-c", "-o", obj + ".tmp", os.path.join(CSRC, src)]
             procs.append((src, obj, subprocess.Popen(cmd, stdout=subprocess.PIPE,
                                                      stderr=subprocess.PIPE, text=True)))
+        if not procs:
+            continue
         src, obj, p = procs.pop(0)
         _, err = p.communicate()
         if p.returncode != 0:
@@ -112,6 +137,8 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, jobs: 
             if verbose and err:
                 print(err)
             os.replace(obj + ".tmp", obj)
+            with open(obj + ".key", "w") as fh:
+                fh.write(keys[src])
     if errs:
         raise RuntimeError("\n".join(errs))
     cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out + ".tmp", *objs]

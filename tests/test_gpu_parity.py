@@ -426,18 +426,18 @@ def test_one_exposure_exact_every_split(gpu, oracle, monkeypatch, fitoffsets):
     B = _exposure(100_000, seed=42, offsets=fitoffsets)
     ref = oracle_fit(oracle, B, fitoffsets=fitoffsets)
     recs = {}
-    # G = 8 runs in the split form by default (512-thread parts, two threads per canonical
-    # chain); "8-unsplit": 256-thread parts (GPD_EXACT_SPLIT=0); "8-lds": those with the head of
-    # every chain's model cache in LDS (GPD_EXACT_LMC=1, opt-in)
-    for G in ("1", "2", "4", "8", "8-unsplit", "8-lds", None):
+    # G = 8 in 256-thread parts by default; "8-split": the split form (GPD_EXACT_SPLIT=1,
+    # 512-thread parts, two threads per canonical chain); "8-lds": 256-thread parts with the
+    # head of every chain's model cache in LDS (GPD_EXACT_LMC=1) — both opt-in
+    for G in ("1", "2", "4", "8", "8-split", "8-lds", None):
         if G is None:
             monkeypatch.delenv("GPD_EXACT_G", raising=False)
         else:
             monkeypatch.setenv("GPD_EXACT_G", G[:1])
         monkeypatch.delenv("GPD_EXACT_LMC", raising=False)
         monkeypatch.delenv("GPD_EXACT_SPLIT", raising=False)
-        if G in ("8-unsplit", "8-lds"):
-            monkeypatch.setenv("GPD_EXACT_SPLIT", "0")
+        if G == "8-split":
+            monkeypatch.setenv("GPD_EXACT_SPLIT", "1")
         if G == "8-lds":
             monkeypatch.setenv("GPD_EXACT_LMC", "1")
         fit(gpu, B, fitoffsets=fitoffsets, method="exact")  # warm (workspace)
@@ -469,15 +469,16 @@ def test_exact_cohort_form_records_bitwise(gpu, oracle, monkeypatch, faint, fito
     monkeypatch.setenv("GPD_EXACT_COHORT", "1")
     coh = fit(gpu, B, method="exact", state=st, fitoffsets=fitoffsets)
     assert coh.tobytes() == base.tobytes()
-    # the cohort form in 256-thread parts (two per CU), and with the chains' heads of the model
-    # cache in LDS (one per CU); the default above is the split form (512-thread parts)
-    monkeypatch.setenv("GPD_EXACT_SPLIT", "0")
+    # the cohort form in the split form (512-thread parts, one per CU), and with the chains'
+    # heads of the model cache in LDS (256-thread parts, one per CU); the default above runs
+    # 256-thread parts, two per CU
+    monkeypatch.setenv("GPD_EXACT_SPLIT", "1")
     cog = fit(gpu, B, method="exact", state=st, fitoffsets=fitoffsets)
+    monkeypatch.delenv("GPD_EXACT_SPLIT")
     assert cog.tobytes() == base.tobytes()
     monkeypatch.setenv("GPD_EXACT_LMC", "1")
     cog = fit(gpu, B, method="exact", state=st, fitoffsets=fitoffsets)
     monkeypatch.delenv("GPD_EXACT_LMC")
-    monkeypatch.delenv("GPD_EXACT_SPLIT")
     assert cog.tobytes() == base.tobytes()
     ref = oracle_fit(oracle, B, state=st, fitoffsets=fitoffsets)
     print(assert_exact_bitwise(coh, ref, label=f"exact cohort faint={faint} offsets={fitoffsets}"))
