@@ -182,7 +182,7 @@ void moment_grid(long long N, long long P, int n_cu, bool harmonic, bool mfma, i
 
 Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic, bool phbuf,
             bool mfma, int n_cu, bool harm_offs, bool windowed = false, int exact_g = 1,
-            bool fp32 = false, long long xround = 0, bool xlock = false) {
+            bool fp32 = false, long long xround = 0) {
     Layout L{};
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -231,7 +231,7 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     // (min(P, 1024) workgroups), or per series with the multi-workgroup split (per series of a
     // round, xround, for the persistent cohort form), when that stays below 8 GB
     const long long mc_slots = exact_g > 1 ? (xround > 0 ? std::min(P, xround) : P)
-                               : xlock ? P : std::min<long long>(P, 1024);
+                                           : std::min<long long>(P, 1024);
     const size_t mc_bytes = (size_t)mc_slots * (size_t)N * sizeof(c64);
     L.mstride = (!harmonic && mc_bytes <= (size_t(8) << 30)) ? N : 0;
     L.mcache = take(L.mstride ? mc_bytes : 0);
@@ -478,15 +478,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         xlml = (int)std::max<long long>(0, std::min<long long>(room, chain));
         xlds_bytes = (size_t)xlml * EXACT_WG * sizeof(c64);
     }
-    // Lock-step parts (r4, GPD_EXACT_LOCK=1): whole-exposure batches at G = 1 fitted four
-    // series per 256-thread part, one wave each, their passes kept at the same samples so that
-    // the four series of an FC group read its phasor column once (ExactChi2::lock); needs a
-    // model-cache slot per series.
-    const bool xlock = want_exact && !bphi && window == 0 && exact_g == 1 && !fp32 && xgrid == 0 &&
-                       N > (long long)CR_SLOTS && (double)P * (double)N * 16.0 <= 8589934592.0 &&
-                       getenv("GPD_EXACT_LOCK") && atoi(getenv("GPD_EXACT_LOCK")) == 1;
     const Layout L = plan(N, P, n_fc, faint, harmonic, phbuf, use_mfma, cx->n_cu, harm_offs,
-                          window > 0, exact_g, fp32, xround, xlock);
+                          window > 0, exact_g, fp32, xround);
     if (xlml > 0 && L.mstride == 0 && (long long)xlml * CR_SLOTS < N) {  // no global tail slot
         xlml = 0;
         xlds_bytes = 0;
@@ -1013,10 +1006,6 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         if (bphi)                                                                               \
             k_chi2_exact<FA, OF, PH><<<(unsigned)P, EXACT_WG, 0, stream>>>(pb, info, ph, fstat, \
                                                                            bphi, outp);         \
-        else if (xlock && L.mstride)                                                            \
-            k_fit_exact<FA, OF, PH, 2, 64, true><<<(unsigned)((P + 3) / 4), 256, 0, stream>>>(  \
-                pb, info, ph, fstat, nullptr, nullptr, outp, raw, 0, (c64 *)(ws + L.mcache),    \
-                L.mstride, 1, nullptr, nullptr, 0);                                              \
         else if (one_wave)                                                                      \
             k_fit_exact<FA, OF, PH, 2, 64><<<grid64, 64, 0, stream>>>(                         \
                 pb, info, ph, fstat, nullptr, nullptr, outp, raw, 0, nullptr, 0, 1, nullptr,    \

@@ -2612,12 +2612,6 @@ struct ExactChi2 {
     int lml;
     // the split form's (WGT = 512) term hand-over buffers in LDS: 2 × U × NV × 256 doubles
     __attribute__((address_space(3))) double *xbuf;
-    // lock-step parts (r4, WGT = 64 in 256-thread parts of four series, GPD_EXACT_LOCK): every
-    // chain's batches end at a barrier of the part every LOCK_SAMPLES samples, the same number
-    // in every pass and every wave, so the part's four series walk their samples together and
-    // the phasor column an FC group shares is fetched once from HBM
-    bool lock;
-    static constexpr int LOCK_SAMPLES = 8;
     // multi-workgroup split: G workgroups per series, this one is g; x: the series' exchange
     int G, g;
     Xchg x;
@@ -3030,7 +3024,7 @@ struct ExactChi2 {
             // one wave per series (G = 1): block blk's 256 slots in four quarters of 64 lanes,
             // each quarter butterflied as block_sum's wave stage, the quarter totals added left
             // to right as its LDS stage — block_sum<256>'s tree, bit for bit
-            const int lane = (int)threadIdx.x & 63;
+            const int lane = (int)threadIdx.x;
             for (int blk = 0; blk < CR_BLOCKS; ++blk) {
                 if (blk > 0 && s0 + (long long)blk * EXACT_WG >= s1) {  // empty blocks: as below
 #pragma unroll
@@ -3135,12 +3129,6 @@ struct ExactChi2 {
         }
         cr_sum_blocks<NV>(
             [&](long long i0, double (&acc)[NV]) {
-                if constexpr (WGT == 64) {
-                    if (lock) {
-                        lock_chain<NV, U>(i0, load, batch, accum, acc);
-                        return;
-                    }
-                }
                 const int M = i0 < s1 ? (int)((s1 - 1 - i0) / CR_SLOTS + 1) : 0;
                 if (M == 0) return;
                 Raw A_[U], B_[U];
@@ -3171,67 +3159,6 @@ struct ExactChi2 {
                 if (m0 < M) run(A_, m0);
             },
             tot);
-        if constexpr (WGT == 64) {
-            if (lock) {  // the pass's two closing barriers (lock_drain reads its flag between them)
-                __syncthreads();
-                __syncthreads();
-            }
-        }
-    }
-    // Lock-step chain (WGT = 64, lock): the quarter's chains run ⌈Mq / U⌉ batches, Mq the
-    // quarter's longest chain (uniform in the wave, and the same in every wave of the part: the
-    // four series share the span), loads past a chain's end clamped to the span's last sample
-    // and their terms skipped; a barrier closes every LOCK_SAMPLES samples.  The sums are the
-    // free-running chain's (the same terms added in the same order).
-    template <int NV, int U, class L, class B, class A>
-    __device__ __forceinline__ void lock_chain(long long i0, L &&load, B &&batch, A &&accum,
-                                               double (&acc)[NV]) {
-        static_assert(LOCK_SAMPLES % U == 0, "batches must tile the lock stride");
-        const long long q0 = i0 - ((int)threadIdx.x & 63);
-        const int M = i0 < s1 ? (int)((s1 - 1 - i0) / CR_SLOTS + 1) : 0;
-        const int Mq = q0 < s1 ? (int)((s1 - 1 - q0) / CR_SLOTS + 1) : 0;
-        if (Mq == 0) return;
-        Raw A_[U], B_[U];
-        auto issue = [&](Raw (&X)[U], int m0) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                long long i = i0 + (long long)(m0 + u) * CR_SLOTS;
-                i = i < s1 ? i : s1 - 1;
-                load(i, X[u]);
-            }
-        };
-        auto run = [&](const Raw (&X)[U], int m0) {
-            c64 mb[U];
-            batch(X, mb);
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (m0 + u < M) accum(i0 + (long long)(m0 + u) * CR_SLOTS, X[u], mb[u], acc);
-            if ((m0 + U) % LOCK_SAMPLES == 0 || m0 + U >= Mq) __syncthreads();
-        };
-        issue(A_, 0);
-        int m0 = 0;
-        for (; m0 + U < Mq; m0 += 2 * U) {
-            issue(B_, m0 + U);
-            run(A_, m0);
-            if (m0 + 2 * U < Mq) issue(A_, m0 + 2 * U);
-            run(B_, m0 + U);
-        }
-        if (m0 < Mq) run(A_, m0);
-    }
-    // A pass's barriers without its work (a lock-step part's wave whose series is done, or that
-    // has none): the blocks, quarters and ⌈Mq / LOCK_SAMPLES⌉ barriers per chain of a pass, then
-    // the first closing barrier; the caller reads the part's count of finished waves and takes
-    // the second.
-    __device__ __forceinline__ void lock_idle_pass() const {
-        for (int blk = 0; blk < CR_BLOCKS; ++blk) {
-            if (blk > 0 && s0 + (long long)blk * EXACT_WG >= s1) break;
-            for (int q = 0; q < EXACT_WG / 64; ++q) {
-                const long long q0 = s0 + blk * EXACT_WG + q * 64;
-                const int Mq = q0 < s1 ? (int)((s1 - 1 - q0) / CR_SLOTS + 1) : 0;
-                for (int b = 0; b < (Mq + LOCK_SAMPLES - 1) / LOCK_SAMPLES; ++b) __syncthreads();
-            }
-        }
-        __syncthreads();
     }
     // The split form (r4, WGT = 512 threads per part, G = 8): canonical chain c = g·256 + t of
     // the part (t = thread mod 256) is shared by thread t (h = 0: the chain's samples m = 0, 2,
@@ -3512,7 +3439,6 @@ __device__ __forceinline__ void setup_exact(F &f, const Problem &pb, long long k
     f.lmc = nullptr;
     f.lml = 0;
     f.xbuf = nullptr;
-    f.lock = false;
     f.s0 = sp.s0;
     f.s1 = sp.s1;
     f.G = G;
@@ -3549,11 +3475,8 @@ __device__ __forceinline__ int xpart(long long b, int G) { return (int)((b >> 3)
 // WGT = 64 (units 16-19): one wave per series for short spans (windows of < 256 samples, where a
 // 256-thread workgroup leaves most threads without a sample): four times the series in flight,
 // NEWUOA run once per series instead of once per wave; the same records (ExactChi2 WGT).
-// LOCK (r4, with WGT = 64): parts of four series, one wave each, in lock step (ExactChi2::lock):
-// series 4·blockIdx.x + wave, each with its model-cache slot; a wave whose series is done (or
-// that has none) keeps taking the passes' barriers until the part's four are done.
-template <bool FAINT, bool OFFS, bool PHBUF, int MINB = 1, int WGT = EXACT_WG, bool LOCK = false>
-__global__ __launch_bounds__(LOCK ? 4 * WGT : WGT, MINB) void k_fit_exact(Problem pb, const Info *__restrict__ info,
+template <bool FAINT, bool OFFS, bool PHBUF, int MINB = 1, int WGT = EXACT_WG>
+__global__ __launch_bounds__(WGT, MINB) void k_fit_exact(Problem pb, const Info *__restrict__ info,
                                                         const c64 *__restrict__ phbuf,
                                                         const double *__restrict__ fstat,
                                                         const int *__restrict__ list,
@@ -3572,46 +3495,8 @@ __global__ __launch_bounds__(LOCK ? 4 * WGT : WGT, MINB) void k_fit_exact(Proble
     extern __shared__ __attribute__((aligned(16))) double xlds_dyn[];
     // NEWUOA state: one copy per wave in LDS (all lanes of a wave run the same iteration and
     // read/write the same addresses), instead of replicated in every thread's registers
-    __shared__ Newuoa<2, 5, true> nwx[(LOCK ? 4 * WGT : WGT) / 64];
+    __shared__ Newuoa<2, 5, true> nwx[WGT / 64];
     const double nvalid = (double)info->nvalid;
-    if constexpr (LOCK) {
-        static_assert(WGT == 64, "lock-step parts are four one-wave series");
-        __shared__ int ldone;  // waves of the part whose series is done
-        if (threadIdx.x == 0) ldone = 0;
-        __syncthreads();
-        const int w = (int)threadIdx.x >> 6;
-        const long long k = (long long)blockIdx.x * 4 + w;
-        ExactChi2<FAINT, OFFS, PHBUF, (MINB == 2 ? 8 : CR_UR), WGT> f;
-        setup_exact(f, pb, k < pb.P ? k : pb.P - 1, PHBUF ? phbuf : nullptr, lds, nvalid);
-        if (k < pb.P && mcache != nullptr) {  // (the engine always passes the model cache)
-            f.lock = true;
-            f.mc = mcache + k * mstride;
-            if (FAINT) {
-#pragma unroll
-                for (int q = 0; q < 5; ++q) {
-                    f.m5[q] = fstat[k * 16 + q];
-                    f.w5[q] = fstat[k * 16 + 5 + q];
-                }
-            }
-            f.a_re = f.a_im = f.c_re = f.c_im = 0.0;
-            f.nfev = 0;
-            double x[2];
-            int status = ST_EXACT | extra_status;
-            drive_fit(f, pb, x, status, nwx[w]);
-            const double chi2 = f(x);
-            if ((threadIdx.x & 63) == 0)
-                store_param(out, raw, k, f.c_re, f.c_im, f.a_re, f.a_im, x[0], x[1], chi2, f.nfev,
-                            status);
-        }
-        if ((threadIdx.x & 63) == 0) atomicAdd(&ldone, 1);
-        for (;;) {  // the part's other series' passes: the same barriers, no work
-            f.lock_idle_pass();
-            const int c = ldone;
-            __syncthreads();
-            if (c == 4) break;
-        }
-        return;
-    }
     // WGT = 512: the split form (two threads per canonical chain), always G = 8 parts
     if ((WGT == EXACT_WG && G > 1) || WGT == 2 * EXACT_WG) {  // one series per G workgroups
       // persistent over rounds of gridDim.x / G series (r4, large batches: gridDim.x = the

@@ -23,10 +23,7 @@ namespace gpd {
 #endif
 __attribute__((used)) void *const k_fit_exact64_units[] = {
     (void *)&k_fit_exact<GPD_FA, GPD_OF, false, 2, 64>,
-    (void *)&k_fit_exact<GPD_FA, GPD_OF, true, 2, 64>,
-    // lock-step parts of four series (r4, GPD_EXACT_LOCK)
-    (void *)&k_fit_exact<GPD_FA, GPD_OF, false, 2, 64, true>,
-    (void *)&k_fit_exact<GPD_FA, GPD_OF, true, 2, 64, true>};
+    (void *)&k_fit_exact<GPD_FA, GPD_OF, true, 2, 64>};
 #undef GPD_FA
 #undef GPD_OF
 }  // namespace gpd

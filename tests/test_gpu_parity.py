@@ -484,31 +484,6 @@ def test_exact_cohort_form_records_bitwise(gpu, oracle, monkeypatch, faint, fito
     print(assert_exact_bitwise(coh, ref, label=f"exact cohort faint={faint} offsets={fitoffsets}"))
 
 
-@pytest.mark.parametrize("faint,fitoffsets,P", [(False, False, 64), (True, False, 62), (False, True, 33)])
-def test_exact_lock_step_parts_records_bitwise(gpu, oracle, monkeypatch, faint, fitoffsets, P):
-    """Lock-step parts (GPD_EXACT_LOCK=1: four series per 256-thread part, one wave each, their
-    passes held at the same samples by the part's barriers; a wave whose series is done — or,
-    with P not a multiple of four, that has none — keeps taking the barriers): records
-    byte-identical to the default batch path and the oracle's bits."""
-    N = 9000
-    B = synth.make_batch(N, P, seed=93, offsets=fitoffsets)
-    st = None
-    if faint:
-        st = np.full(N, 2, dtype=np.int8)
-        st[700:2100] = 3
-        st[5000:6100] = 1
-        st[2095:2110] = -1
-        B["d"] = B["d"] * np.where(st == 3, 1.1, np.where(st == 1, 0.3, 0.6))[None, :]
-    monkeypatch.delenv("GPD_EXACT_LOCK", raising=False)
-    base = fit(gpu, B, method="exact", state=st, fitoffsets=fitoffsets)
-    monkeypatch.setenv("GPD_EXACT_LOCK", "1")
-    got = fit(gpu, B, method="exact", state=st, fitoffsets=fitoffsets)
-    monkeypatch.delenv("GPD_EXACT_LOCK")
-    assert got.tobytes() == base.tobytes()
-    ref = oracle_fit(oracle, B, state=st, fitoffsets=fitoffsets)
-    print(assert_exact_bitwise(got, ref, label=f"exact lock faint={faint} offsets={fitoffsets}"))
-
-
 @pytest.mark.parametrize("faint,fitoffsets", [(False, False), (True, False), (False, True)])
 def test_exact_fast_loads_equal_the_general_path(gpu, oracle, monkeypatch, faint, fitoffsets):
     """The exact evaluator's FAST form (ComplexF64 storage, Float64 arithmetic: every sample's
