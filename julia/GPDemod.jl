@@ -49,6 +49,8 @@ end
 
 gpd_version() = ccall((:gpd_version, libgpdemod), Cint, ())
 gpd_device_count() = ccall((:gpd_device_count, libgpdemod), Cint, ())
+# id of the sources the loaded library was built from (build.py's tree id; provenance checks)
+gpd_build_id() = unsafe_string(ccall((:gpd_build_id, libgpdemod), Cstring, ()))
 gpd_release(device::Integer=0) = ccall((:gpd_release, libgpdemod), Cint, (Cint,), device)
 
 method_flags(method::Symbol) =
