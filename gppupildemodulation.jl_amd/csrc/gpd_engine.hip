@@ -484,11 +484,11 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         xlml = 0;
         xlds_bytes = 0;
     }
-    // the split form needs the model cache (its sums run through cr_sum2m only) and hands its
-    // terms over in 2 × CR_U × NV × 256 doubles of LDS (NV = 8 with offsets, 4 without)
+    // the split form needs the model cache (its sums run through cr_sum2m only) and 256 × NV
+    // doubles of LDS for its first butterfly step (NV = 8 with offsets, 4 without)
     const bool split = split_on && want_exact && !bphi && window == 0 && exact_g == CR_BLOCKS &&
                        L.mstride != 0 && xlml == 0;
-    const size_t split_lds = split ? (size_t)2 * CR_U * (offs ? 8 : 4) * EXACT_WG * sizeof(double) : 0;
+    const size_t split_lds = split ? (size_t)(offs ? 8 : 4) * EXACT_WG * sizeof(double) : 0;
     if (cx->ws_cap < L.total) {
         if (cx->ws) {
             HIP_TRY(hipDeviceSynchronize());

@@ -2610,7 +2610,7 @@ struct ExactChi2 {
     // the chain's later samples stay in the global slot mc).  lml = 0: all in mc.
     __attribute__((address_space(3))) c64 *lmc;
     int lml;
-    // the split form's (WGT = 512) term hand-over buffers in LDS: 2 × U × NV × 256 doubles
+    // the split form's (WGT = 512) LDS for the first butterfly step: 256 × NV doubles
     __attribute__((address_space(3))) double *xbuf;
     // multi-workgroup split: G workgroups per series, this one is g; x: the series' exchange
     int G, g;
@@ -3160,70 +3160,57 @@ struct ExactChi2 {
             },
             tot);
     }
-    // The split form (r4, WGT = 512 threads per part, G = 8): canonical chain c = g·256 + t of
-    // the part (t = thread mod 256) is shared by thread t (h = 0: the chain's samples m = 0, 2,
-    // 4, …) and thread t + 256 (h = 1: m = 1, 3, 5, …).  Each evaluates its own samples' terms
-    // (accum into zeroed temporaries: a term x becomes 0.0 + x, which differs from x only for
-    // x = −0.0, and a chain sum is never −0.0, so adding either gives the same bits); thread
-    // t + 256 hands its terms over through LDS and thread t adds both in chain order.  Then the
-    // chains of waves 0-3 are reduced as block_sum<256> does (butterfly, then the four wave
-    // totals left to right) and exchanged with the other parts as in cr_sum_blocks — the G = 8
-    // sums, bit for bit, with two waves per SIMD instead of one.  Every thread runs the same
-    // number of iterations (bounded by the part's longest chain; loads of samples past a
-    // chain's end are clamped to the span's last sample and their terms discarded).
+    // The split form (r4, WGT = 512 threads per part, G = 8): wave w (0-7) of the part holds
+    // the block's canonical chains c = 32·w + (lane mod 32), lanes l and l + 32 sharing chain c —
+    // lane l (h = 0) evaluates its samples m = 0, 2, 4, …, lane l + 32 (h = 1) the odd ones.
+    // Each evaluates its sample's terms (accum into zeroed temporaries: a term x becomes 0.0 + x,
+    // which differs from x only for x = −0.0, and a chain sum is never −0.0, so adding either gives
+    // the same bits); the odd term crosses to lane l (lane_xor<32>) and lane l adds both in chain
+    // order.  Both lanes of a pair run the same ⌈M/2⌉ steps.  Then block_sum<256>'s tree over the
+    // block's 256 chains (its butterfly's first step pairs chains c and c ± 32, which sit in waves
+    // 2q and 2q + 1: through LDS) and the parts' exchange as in cr_sum_blocks — the G = 8 sums,
+    // bit for bit, with two waves per SIMD instead of one.
     template <int NV, int U, class L, class B, class A>
     __device__ __forceinline__ void cr_split_chain(L &&load, B &&batch, A &&accum,
                                                    double (&acc)[NV]) {
-        const int t = (int)threadIdx.x & (EXACT_WG - 1), h = (int)threadIdx.x / EXACT_WG;
-        const long long c0 = s0 + (long long)g * EXACT_WG;  // the part's first chain
-        const long long i0 = c0 + t;
+        const int lane = (int)threadIdx.x & 63, w = (int)threadIdx.x >> 6, h = lane >> 5;
+        const long long i0 = s0 + (long long)g * EXACT_WG + 32 * w + (lane & 31);
         const int M = i0 < s1 ? (int)((s1 - 1 - i0) / CR_SLOTS + 1) : 0;
-        const int Mmax = c0 < s1 ? (int)((s1 - 1 - c0) / CR_SLOTS + 1) : 0;
-        const int J = (Mmax + 1) >> 1;  // sample pairs of the longest chain
+        const int J = (M + 1) >> 1;  // the pair's steps (the same in both lanes)
 #pragma unroll
         for (int k = 0; k < NV; ++k) acc[k] = 0.0;
-        ldouble *xb = xbuf;
+        if (J == 0) return;
         Raw A_[U], B_[U];
         auto issue = [&](Raw (&X)[U], int j0) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                long long i = i0 + (long long)(2 * (j0 + u) + h) * CR_SLOTS;
-                i = i < s1 ? i : s1 - 1;
-                load(i, X[u]);
+                int m = 2 * (j0 + u < J ? j0 + u : J - 1) + h;
+                m = m < M ? m : M - 1;
+                load(i0 + (long long)m * CR_SLOTS, X[u]);
             }
         };
-        int buf = 0;
         auto run = [&](const Raw (&X)[U], int j0) {
             c64 mb[U];
             batch(X, mb);
-            double f[U][NV];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
+                if (j0 + u >= J) break;
+                double t[NV];
 #pragma unroll
-                for (int k = 0; k < NV; ++k) f[u][k] = 0.0;
+                for (int k = 0; k < NV; ++k) t[k] = 0.0;
                 const int m = 2 * (j0 + u) + h;
-                if (m < M) accum(i0 + (long long)m * CR_SLOTS, X[u], mb[u], f[u]);
-            }
-            ldouble *q = xb + buf * (U * NV * EXACT_WG);
-            if (h == 1) {
+                if (m < M) accum(i0 + (long long)m * CR_SLOTS, X[u], mb[u], t);
+                double p[NV];
 #pragma unroll
-                for (int u = 0; u < U; ++u)
+                for (int k = 0; k < NV; ++k) p[k] = lane_xor<32>(t[k]);  // lane l: the odd term
+                if (h == 0) {
 #pragma unroll
-                    for (int k = 0; k < NV; ++k) q[(u * NV + k) * EXACT_WG + t] = f[u][k];
-            }
-            __syncthreads();  // (double-buffered: the next writes go to the other buffer)
-            if (h == 0) {
+                    for (int k = 0; k < NV; ++k) acc[k] += t[k];
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-#pragma unroll
-                    for (int k = 0; k < NV; ++k) acc[k] += f[u][k];
-#pragma unroll
-                    for (int k = 0; k < NV; ++k) acc[k] += q[(u * NV + k) * EXACT_WG + t];
+                    for (int k = 0; k < NV; ++k) acc[k] += p[k];
                 }
             }
-            buf ^= 1;
         };
-        if (J == 0) return;
         issue(A_, 0);
         int j0 = 0;
         for (; j0 + U < J; j0 += 2 * U) {
@@ -3244,21 +3231,40 @@ struct ExactChi2 {
         }
         double acc[NV];
         cr_split_chain<NV, U>(load, batch, accum, acc);
-        // block_sum<256> over waves 0-3 (the chains' owners); waves 4-7 join the barriers
-        const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
-        if (wave < EXACT_WG / 64) {
-            wave_sum<NV>(acc);
-            if (lane == 0) {
+        const int lane = (int)threadIdx.x & 63, w = (int)threadIdx.x >> 6;
+        // block_sum<256>'s butterfly: partner 32 (chains c, c ± 32: waves w and w ^ 1) via LDS
+        ldouble *xb = xbuf;
+        if (lane < 32) {
 #pragma unroll
-                for (int k = 0; k < NV; ++k) lp[wave * NV + k] = acc[k];
-            }
+            for (int k = 0; k < NV; ++k) xb[(w * 32 + lane) * NV + k] = acc[k];
+        }
+        __syncthreads();
+        if (lane < 32) {
+#pragma unroll
+            for (int k = 0; k < NV; ++k) acc[k] = acc[k] + xb[((w ^ 1) * 32 + lane) * NV + k];
+        }
+        // partners 16 … 1 within the 32 chains of each wave (lanes 0-31)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) acc[k] = acc[k] + lane_xor<16>(acc[k]);
+#pragma unroll
+        for (int k = 0; k < NV; ++k) acc[k] = acc[k] + lane_xor<8>(acc[k]);
+#pragma unroll
+        for (int k = 0; k < NV; ++k) acc[k] = acc[k] + lane_xor<4>(acc[k]);
+#pragma unroll
+        for (int k = 0; k < NV; ++k) acc[k] = acc[k] + lane_xor<2>(acc[k]);
+#pragma unroll
+        for (int k = 0; k < NV; ++k) acc[k] = acc[k] + lane_xor<1>(acc[k]);
+        // the LDS stage: canonical wave q's total (lane 0 of wave 2q), left to right
+        if (lane == 0 && (w & 1) == 0) {
+#pragma unroll
+            for (int k = 0; k < NV; ++k) lp[(w >> 1) * NV + k] = acc[k];
         }
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
             double sv = lp[k];
 #pragma unroll
-            for (int w = 1; w < EXACT_WG / 64; ++w) sv = sv + lp[w * NV + k];
+            for (int q = 1; q < EXACT_WG / 64; ++q) sv = sv + lp[q * NV + k];
             acc[k] = sv;
         }
         __syncthreads();

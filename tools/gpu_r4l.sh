@@ -14,7 +14,7 @@ for sp in 1 0; do
   echo "C2 split=$sp"; grep exact $O/c2_split$sp$r.jsonl
 done
 done
-GPD_FIT_PROF=1 timeout -k 10 120 python tools/c2_offsets_timing.py --g8 > /dev/null 2> $O/c2_prof.err || exit 1
+GPD_EXACT_SPLIT=1 GPD_FIT_PROF=1 timeout -k 10 120 python tools/c2_offsets_timing.py --g8 > /dev/null 2> $O/c2_prof.err || exit 1
 grep "exact fit_prof" $O/c2_prof.err
-GPD_EXACT_COHORT=1 timeout -k 10 150 python tools/faint_time.py --method exact --reps 2 > $O/c5_coh_split.json 2>$O/c5_coh_split.err || { tail -20 $O/c5_coh_split.err; exit 1; }
+GPD_EXACT_SPLIT=1 GPD_EXACT_COHORT=1 timeout -k 10 150 python tools/faint_time.py --method exact --reps 2 > $O/c5_coh_split.json 2>$O/c5_coh_split.err || { tail -20 $O/c5_coh_split.err; exit 1; }
 echo "C5 cohort split"; cat $O/c5_coh_split.json
