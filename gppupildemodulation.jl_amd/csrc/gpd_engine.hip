@@ -445,9 +445,9 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     bool lmc_on = getenv("GPD_EXACT_LMC") && atoi(getenv("GPD_EXACT_LMC")) == 1;
     // Split form (r4): at G = 8 every canonical chain shared by two threads of a 512-thread part
     // (k_fit_exact WGT = 512, ExactChi2::cr_split_chain): two waves per SIMD where the G = 8
-    // form has one; the same records.  Measured slower (C2 exact 2.96-3.04 → 3.53-3.63 ms,
-    // fitoffsets 3.80-3.90 → 4.75-4.78 ms: 256 registers per lane spill, a barrier per batch;
-    // profiles/r4/exact_split/), so opt-in: GPD_EXACT_SPLIT=1.
+    // form has one; the same records.  Measured slower (C2 exact 2.95-3.01 → 3.47 ms, fitoffsets
+    // 3.78-3.80 → 4.52-4.56 ms: the part's first pass takes as many cycles with twice the waves;
+    // profiles/r4/exact_split_pair/), so opt-in: GPD_EXACT_SPLIT=1.
     const bool split_on = getenv("GPD_EXACT_SPLIT") && atoi(getenv("GPD_EXACT_SPLIT")) == 1 &&
                           !fp32;
     if (split_on) lmc_on = false;
