@@ -233,9 +233,7 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     const long long mc_slots = exact_g > 1 ? (xround > 0 ? std::min(P, xround) : P)
                                            : std::min<long long>(P, 1024);
     const size_t mc_bytes = (size_t)mc_slots * (size_t)N * sizeof(c64);
-    // GPD_EXACT_MCACHE=0 (A/B): no model cache — the residual pass evaluates the model again
-    const bool mc_on = !(getenv("GPD_EXACT_MCACHE") && atoi(getenv("GPD_EXACT_MCACHE")) == 0);
-    L.mstride = (!harmonic && mc_on && mc_bytes <= (size_t(8) << 30)) ? N : 0;
+    L.mstride = (!harmonic && mc_bytes <= (size_t(8) << 30)) ? N : 0;
     L.mcache = take(L.mstride ? mc_bytes : 0);
     // multi-workgroup exact fit: per-series block totals (2 slots × 8 blocks × 8 values) and
     // arrival counters (zeroed per launch)

@@ -3416,14 +3416,6 @@ struct ExactChi2 {
                            resid(r.f, r.d, weight_of(V, r.st), a);
                        },
                        s);
-        } else if (FAST) {  // no model cache: the first pass's batched model again (same bits)
-            cr_sum2m<1>([&](long long i, Raw &r) { load_raw<FAST>(V, i, r); },
-                        [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch(V, X, b, phi, mb); },
-                        [&](long long i, const Raw &r, const c64 &m, double (&a)[1]) {
-                            if (!valid_st<FAST>(V, r.st)) return;
-                            resid(m, r.d, weight_of(V, r.st), a);
-                        },
-                        s);
         } else {
             cr_sum<1>(
                 [&](long long i, double (&a)[1]) {
