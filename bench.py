@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--no-ceiling", action="store_true",
                     help="skip the reference-ceiling oracle runs (alternative summation orders, "
                          "1-ulp χ²) of the C3 CPU sample")
+    ap.add_argument("--no-c2", action="store_true",
+                    help="skip the C2 block (one exposure through the host-buffer drop-in call)")
     ap.add_argument("--no-c4", action="store_true",
                     help="skip the C4-rank rehearsal block (profiling runs: one kernel shape)")
     ap.add_argument("--dist-always", action="store_true",
@@ -166,16 +168,31 @@ def main():
     err = ctypes.create_string_buffer(512)
 
     fit_dev = L.gpd_fit_batch_c32_dev if c32 else L.gpd_fit_batch_dev
+    # per-step time of the record gather on this rank (ms): HIP events on the launch stream
+    # around the RCCL gather (the current stream waits for the collective), host clock around
+    # the gloo gather (after the records' device-to-host copy, which waits for the fit)
+    gather_ms = []
 
-    def step():
+    def step(timed=False):
         r = fit_dev(N, P, t.data_ptr(), d.data_ptr(), N, fc.data_ptr(), G, N,
                     fcop.data_ptr(), None, gpd.M_2PI, None, flags, 60,
                     params.data_ptr(), None, N, local, sptr, err, len(err))
         gpd._lib.check(r, err)
         if backend != "nccl" and use_dist:
-            g = shard.gather_records(params.cpu(), world, rank, counts=counts, force=use_dist)
+            host = params.cpu()
+            tg = time.perf_counter()
+            g = shard.gather_records(host, world, rank, counts=counts, force=use_dist)
+            if timed:
+                gather_ms.append(1e3 * (time.perf_counter() - tg))
             return None if g is None else g.to(dev)
-        return shard.gather_records(params, world, rank, counts=counts, force=use_dist)
+        if timed and use_dist:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        g = shard.gather_records(params, world, rank, counts=counts, force=use_dist)
+        if timed and use_dist:
+            e1.record(stream)
+            gather_ms.append((e0, e1))
+        return g
 
     log = (lambda msg: print(f"[bench] rank {rank}: {msg}", file=sys.stderr, flush=True))
     log(f"{P} series x {N} samples resident; {args.warmup} warmup + {args.steps} timed steps")
@@ -188,7 +205,7 @@ def main():
     kern = {}
     t_start = time.perf_counter()
     for _ in range(args.steps):
-        gathered = step()
+        gathered = step(timed=True)
         for name, ms in gpd.timings(local).items():  # HIP events on the launch stream
             kern.setdefault(name, []).append(ms)
     torch.cuda.synchronize(dev)
@@ -196,11 +213,24 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
+    own_elapsed = elapsed
     if dist:
         e = torch.tensor([elapsed], dtype=torch.float64,
                          device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
+    # every rank's own numbers, gathered to all (untimed): a shortfall from linear scaling then
+    # shows whether it came from shard imbalance, a slow kernel on one GPU or the gather
+    ranks = None
+    if dist:
+        g_ms = [x if isinstance(x, float) else x[0].elapsed_time(x[1]) for x in gather_ms]
+        mine = {"rank": rank, "local_rank": local, "device": torch.cuda.get_device_name(dev),
+                "series": P, "series_range": [p0, p1],
+                "step_ms": round(1e3 * own_elapsed / args.steps, 3),
+                "gather_ms": round(float(np.mean(g_ms)), 3) if g_ms else None,
+                "kernels_ms": {k: round(float(np.mean(v)), 3) for k, v in kern.items()}}
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
 
     samples_total = float(P_total) * N * args.steps
     value = samples_total / elapsed
@@ -330,6 +360,12 @@ def main():
                      "value_mean": float(P_total) * N / (float(np.mean(chunks)) * 1e-3),
                      "note": "chunks of 10 steps after the timed region; not the headline"}
 
+    # BASELINE configs[1] (C2): one exposure through the drop-in call as the reference makes it
+    # (host arrays in, output = copy(data) back), PCIe included
+    c2 = None
+    if world == 1 and not args.no_c2 and P >= 32 and not c32:
+        c2 = c2_block(gpd, t, d, fc, args, log)
+
     cpu = None
     if not args.no_cpu and args.cpu_pixels > 0 and world == 1:  # rank 0 at N=1 only
         cpu = cpu_baseline(gpd, t, d, fc, fcop, par, args, N,
@@ -361,12 +397,92 @@ def main():
                               if backend == "nccl" else f"{backend} gather (multi-rank rehearsal)")},
         "roofline": roofline, "cpu_baseline": cpu, "kernels_ms": kernels, "fits": fits,
         "all_f64_moments": f64_all, "c4_rank_rehearsal": c4, "sustained": sustained,
+        "c2_exposure": c2,
         "c5_faint": c5,
+        "distributed": None if not dist else {
+            "world_size": dist.get_world_size(), "backend": backend,
+            "per_rank": ranks,
+            "step_ms_max_over_min": round(max(r["step_ms"] for r in ranks) /
+                                          max(1e-9, min(r["step_ms"] for r in ranks)), 4),
+            "note": "per rank: its own timed-loop time per step (before the MAX over ranks), "
+                    "its kernels (HIP events, mean of the timed steps) and its record gather "
+                    "(events around the RCCL gather on the launch stream; host clock for gloo)"},
         "build_id": gpd.build_id(),
     }
     print(json.dumps(out))
     if dist:
         dist.destroy_process_group()
+
+
+def c2_block(gpd, t, d, fc, args, log, reps=5):
+    """BASELINE configs[1] (C2): one GRAVITY exposure — 32 diodes + 8 FC columns x N samples, the
+    first 32 series and 8 FC columns of the resident batch — through the drop-in boundary as the
+    reference is called (src/GPPupilDemodulation.jl:161,205 → demodulateall, src/Modulation.jl:
+    344-435): host arrays in, the demodulated `output = copy(data)` and the records back, PCIe
+    included (gpd_fit_batch / gpd_fit_windows from pageable host memory).  `data` is the N x 40
+    column-major matrix a Julia caller hands over (np.asfortranarray).  Median of `reps` calls
+    each: the fit alone (records only), demodulateall with its output, demodulateall with
+    fitoffsets (the reference's --center fit: the exact evaluator), and the 1-s windows of
+    processmetrology (500 samples, gpd_fit_windows with the output)."""
+    import numpy as np
+    import torch
+
+    N = t.shape[0]
+    log(f"C2 exposure: 32 x {N} through the host-buffer drop-in ({reps} calls per case)")
+    th = t.cpu().numpy()
+    dd = d[:32].cpu().numpy().view(np.complex128).reshape(32, N)
+    ff = fc[:8].cpu().numpy().view(np.complex128).reshape(8, N)
+    data = np.empty((N, 40), dtype=np.complex128, order="F")
+    fop = np.array([gpd.fc_column_of(c) - 1 for c in range(1, 33)], dtype=np.int32)
+    for c in range(32):
+        data[:, c] = dd[c]
+    for g in range(8):  # diodes 4g..4g+3 share FC row g (the synthetic batch's groups of 4)
+        data[:, fop[4 * g]] = ff[g]
+    cols = data.T  # (40, N) C-contiguous view: no copy
+
+    def med(fn):
+        fn()
+        ts = []
+        for _ in range(reps):
+            t1 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t1)
+        return round(1e3 * float(np.median(ts)), 3), gpd.timings(0)
+
+    cases = {}
+    ms, k = med(lambda: gpd.fit_batch(th, cols[:32], cols, fop))
+    cases["fit_only"] = {"host_call_ms": ms, "what": "gpd_fit_batch, records only"}
+    kern = k
+    ms, k = med(lambda: gpd.demodulateall(th, data))
+    cases["demodulateall"] = {"host_call_ms": ms,
+                              "what": "output = copy(data) with the 32 demodulated columns "
+                                      "written in place, records, likelihood"}
+    ms, k = med(lambda: gpd.demodulateall(th, data, fitoffsets=True))
+    cases["demodulateall_fitoffsets"] = {
+        "host_call_ms": ms, "kernels_ms": {a: round(b, 3) for a, b in k.items()},
+        "what": "--center fit (ModulationWithOffsets): the exact evaluator by default"}
+    nwin = gpd.window_length(th, 1.0)
+    out = cols.copy()
+
+    def windows():
+        gpd.fit_windows(th, cols[:32], cols, fop, nwin, want_output=True, out=out[:32])
+    ms, k = med(windows)
+    cases["windows_1s"] = {"host_call_ms": ms, "window_samples": nwin,
+                           "series": 32 * (-(-N // nwin)),
+                           "kernels_ms": {a: round(b, 3) for a, b in k.items()},
+                           "what": "processmetrology's window mode: every 1-s window fitted "
+                                   "(gpd_fit_windows), demodulated output in place"}
+    # the same calls' records against the fit-only call: the output path changes nothing
+    p_fit = gpd.fit_batch(th, cols[:32], cols, fop)
+    _, par, _ = gpd.demodulateall(th, data)
+    same = bool(np.array_equal(np.array([p.b for p in par]), p_fit["b"]))
+    return {"series": 32, "samples": N, "fc_columns": 8,
+            "host_bytes_in": int(dd.nbytes + ff.nbytes + th.nbytes),
+            "host_bytes_out": int(dd.nbytes), "cases": cases,
+            "kernels_ms_fit_only": {a: round(b, 3) for a, b in kern.items()},
+            "records_equal_fit_only": same,
+            "host_memory": "pageable numpy arrays (column-major, as a Julia Matrix)",
+            "note": "PCIe-inclusive host-buffer calls; not the headline (which is HBM-resident)"}
 
 
 def c5_block(gpd, L, dev, sptr, args, log):

@@ -47,6 +47,38 @@ def tree_id() -> str:
 ID_MARKER = b"GPD_BUILD_ID="
 
 
+def unit_deps(src: str) -> list:
+    """`src` and every unit it #includes, transitively (gpd_part6.hip includes gpd_part2.hip,
+    gpd_part9-11.hip gpd_part5.hip, …): an edit to an included unit must change the key of
+    every unit that compiles it."""
+    import re
+
+    seen, todo = [], [src]
+    while todo:
+        f = todo.pop(0)
+        if f in seen:
+            continue
+        seen.append(f)
+        with open(os.path.join(CSRC, f)) as fh:
+            todo += re.findall(r'^\s*#\s*include\s+"(gpd_part\d+\.hip)"', fh.read(), re.M)
+    return seen
+
+
+def unit_key(src: str, extra=(), bid: str = "") -> str:
+    """Content key of one translation unit's object: its source and every unit it includes, the
+    headers, include/gpdemod.h, the compiler and its flags (and the build id for unit 0)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in unit_deps(src) + HEADERS:
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    with open(os.path.join(HERE, "..", "include", "gpdemod.h"), "rb") as fh:
+        h.update(fh.read())
+    h.update(" ".join([HIPCC, *FLAGS, *extra, bid if src == "gpd_engine.hip" else ""]).encode())
+    return h.hexdigest()
+
+
 def lib_id(path: str) -> str | None:
     """The build id embedded in a built library (read from its bytes, without loading it)."""
     try:
@@ -82,41 +114,38 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, jobs: 
     # the build id is compiled into unit 0 only (gpd_build_id); an object whose inputs (the
     # headers, its unit, the flags) are unchanged since its last compile is reused (.key file)
     bid = f'-DGPD_BUILD_ID="{tree_id()}"'
-
-    def unit_key(src: str) -> str:
-        import hashlib
-
-        h = hashlib.sha256()
-        for f in [src] + HEADERS + ["gpd_part3.hip", "gpd_part16.hip", "gpd_part20.hip"]:
-            with open(os.path.join(CSRC, f), "rb") as fh:
-                h.update(f.encode() + b"\0" + fh.read())
-        with open(os.path.join(HERE, "..", "include", "gpdemod.h"), "rb") as fh:
-            h.update(fh.read())
-        h.update(" ".join([HIPCC, *FLAGS, *extra, bid if src == "gpd_engine.hip" else ""]).encode())
-        return h.hexdigest()
     jobs = jobs or max(1, min(len(SOURCES), os.cpu_count() or 1))
     procs, objs, errs = [], [], []
     pending = [u for u in SOURCES if not only or u in only]
     if only:  # the other units from the release build
         rel = os.path.join(HERE, "build", "release")
-        reuse = [os.path.join(rel, u.replace(".hip", ".o")) for u in SOURCES if u not in only]
-        # every kernel takes Problem & co. by value: a release object older than a shared header
-        # would link silently against another struct layout (advisor r3) — refuse it
-        deps = [os.path.join(CSRC, h) for h in HEADERS] + \
-            [os.path.join(HERE, "..", "include", "gpdemod.h")]
-        newest = max(os.path.getmtime(p) for p in deps)
-        stale = [o for o in reuse if not os.path.exists(o) or os.path.getmtime(o) < newest]
+        reuse = [u for u in SOURCES if u not in only]
+        # every kernel takes Problem & co. by value: a release object built from other sources
+        # or headers would link silently against another struct layout (advisor r3) — refuse
+        # any whose content key is not the current release key of its unit (advisor r4: keys,
+        # not mtimes, so a touched but unchanged header does not refuse valid objects)
+        rbid = f'-DGPD_BUILD_ID="{tree_id()}"'
+        stale = []
+        for u in reuse:
+            o = os.path.join(rel, u.replace(".hip", ".o"))
+            try:
+                with open(o + ".key") as fh:
+                    ok = os.path.exists(o) and fh.read() == unit_key(u, [], rbid)
+            except OSError:
+                ok = False
+            if not ok:
+                stale.append(os.path.basename(o))
         if stale:
-            raise RuntimeError("--only: release objects older than the headers (rebuild the "
-                               "release library first): " + ", ".join(map(os.path.basename, stale)))
-        objs += reuse
+            raise RuntimeError("--only: release objects not built from this tree (rebuild the "
+                               "release library first): " + ", ".join(stale))
+        objs += [os.path.join(rel, u.replace(".hip", ".o")) for u in reuse]
     keys = {}
     while pending or procs:
         while pending and len(procs) < jobs:
             src = pending.pop(0)
             obj = os.path.join(objdir, src.replace(".hip", ".o"))
             objs.append(obj)
-            keys[src] = unit_key(src)
+            keys[src] = unit_key(src, extra, bid)
             try:
                 with open(obj + ".key") as fh:
                     if fh.read() == keys[src] and os.path.exists(obj):

@@ -313,6 +313,8 @@ int gpd_release(int device) {
     (void)hipFree(cx->harena);
     cx->ws = cx->harena = nullptr;
     cx->ws_cap = cx->harena_cap = 0;
+    cx->last_fstat = nullptr;  // pointed into the freed workspace (advisor r4)
+    cx->last_fstat_P = 0;
     return GPD_OK;
 }
 
@@ -491,6 +493,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     const size_t split_lds = split ? (size_t)(offs ? 8 : 4) * EXACT_WG * sizeof(double) : 0;
     if (cx->ws_cap < L.total) {
         if (cx->ws) {
+            cx->last_fstat = nullptr;  // points into the workspace being freed (advisor r4)
+            cx->last_fstat_P = 0;
             HIP_TRY(hipDeviceSynchronize());
             HIP_TRY(hipFree(cx->ws));
             cx->ws = nullptr;

@@ -191,13 +191,14 @@ def _storage(d, fc):
 
 def fit_batch(t, d, fc, fc_of_pixel, *, state=None, omega=M_2PI, xinit=None, recenter=True,
               fitoffsets=False, onlyhigh=False, maxfun=60, want_output=False, method="auto",
-              n_gpus=1):
+              n_gpus=1, out=None):
     """Batch fit of P series on the GPU.
 
     t: (N,) float64; d: (P, N) complex (row k = series k); fc: (G, N) complex raw FC
     columns; fc_of_pixel: (P,) int (0-based row of fc).  complex64 d and fc are kept in Float32
     in device memory (gpd_fit_batch_c32), anything else is taken as complex128.  Returns a
-    PARAM_DTYPE record array (and the (P, N) complex128 demodulated series when want_output).
+    PARAM_DTYPE record array (and the (P, N) complex128 demodulated series when want_output;
+    `out`, a caller-owned (P, N) complex128 array with contiguous rows, receives them in place).
     """
     L = load()
     t = np.ascontiguousarray(t, dtype=np.float64)
@@ -226,11 +227,19 @@ def fit_batch(t, d, fc, fc_of_pixel, *, state=None, omega=M_2PI, xinit=None, rec
     if onlyhigh:
         flags |= GPD_ONLY_HIGH
     params = np.zeros(P, dtype=PARAM_DTYPE)
-    out = np.zeros((P, N), dtype=np.complex128) if want_output else None
+    ldo = N
+    if out is not None:
+        want_output = True
+        if (out.dtype != np.complex128 or out.ndim != 2 or out.shape != (P, N)
+                or out.strides[1] != 16 or out.strides[0] % 16 or out.strides[0] < 16 * N):
+            raise ValueError("out must be a (P, N) complex128 array with contiguous rows")
+        ldo = out.strides[0] // 16
+    elif want_output:
+        out = np.zeros((P, N), dtype=np.complex128)
     err = ctypes.create_string_buffer(512)
     fn = L.gpd_fit_batch_c32 if c32 else L.gpd_fit_batch
     rc = fn(N, P, ptr(t), ptr(d), N, ptr(fc), fc.shape[0], N, ptr(fop), ptr(st), float(omega),
-            ptr(xi), flags, int(maxfun), ptr(params), ptr(out), N, int(n_gpus), err, len(err))
+            ptr(xi), flags, int(maxfun), ptr(params), ptr(out), ldo, int(n_gpus), err, len(err))
     check(rc, err)
     return (params, out) if want_output else params
 
@@ -281,7 +290,9 @@ def demodulateall(timestamp, data, *, init="auto", recenter=True, faintparam=Non
     N = data.shape[0]
     if t.shape != (N,):
         raise ValueError("voltage and time must have the same number of lines")
-    cols = np.ascontiguousarray(data.T)  # (40, N): column k contiguous, like Julia's Matrix
+    # (40, N): column k contiguous, like Julia's Matrix (no copy when `data` is column-major,
+    # np.asfortranarray — the layout a Julia caller hands over)
+    cols = np.ascontiguousarray(data.T)
     state = None
     if faintparam is not None:
         if isinstance(faintparam, FaintStates):
@@ -295,12 +306,19 @@ def demodulateall(timestamp, data, *, init="auto", recenter=True, faintparam=Non
     if not (isinstance(init, str) and init == "auto"):
         xinit = np.asarray(init, dtype=np.float64)
     fop = np.array([fc_column_of(c) - 1 for c in range(1, 33)], dtype=np.int32)
+    # output = copy(data): FC columns pass through, eltype of data (src/Modulation.jl:353).  For
+    # complex128 data the library writes the demodulated diodes into its columns 1..32 in place
+    # (one device-to-host copy into memory the copy has touched); complex64 data takes the
+    # Float64 result through a separate array, converted to the data's element type
+    out_cols = cols.copy()
+    inplace = out_cols.dtype == np.complex128
     params, out = fit_batch(t, cols[:32], cols, fop, state=state, xinit=xinit, recenter=recenter,
                             fitoffsets=fitoffsets, onlyhigh=onlyhigh, want_output=True,
-                            method=method, n_gpus=n_gpus)
-    # output = copy(data): FC columns pass through, eltype of data (src/Modulation.jl:353)
-    output = data.copy()
-    output[:, :32] = out.T
+                            method=method, n_gpus=n_gpus,
+                            out=out_cols[:32] if inplace else None)
+    if not inplace:
+        out_cols[:32] = out
+    output = out_cols.T  # (N, 40), column-major like the Julia Matrix
     param = []
     for p in params:
         if fitoffsets:
@@ -314,7 +332,7 @@ def demodulateall(timestamp, data, *, init="auto", recenter=True, faintparam=Non
 
 def fit_windows(t, d, fc, fc_of_col, nwindow, *, state=None, omega=M_2PI, xinit=None,
                 recenter=True, fitoffsets=False, onlyhigh=False, maxfun=60, want_output=False,
-                method="auto", n_gpus=1):
+                method="auto", n_gpus=1, out=None):
     """Every window of `nwindow` samples (Iterators.partition, the last one shorter) fitted as its
     own demodulateall call (src/GPPupilDemodulation.jl:204-205), all windows in one GPU call.
 
@@ -342,11 +360,19 @@ def fit_windows(t, d, fc, fc_of_col, nwindow, *, state=None, omega=M_2PI, xinit=
         (GPD_FIT_OFFSETS if fitoffsets else 0) | (GPD_ONLY_HIGH if onlyhigh else 0)
     nwin = -(-N // nwindow)
     params = np.zeros(nwin * C, dtype=PARAM_DTYPE)
-    out = np.zeros((C, N), dtype=np.complex128) if want_output else None
+    ldo = N
+    if out is not None:  # caller-owned (C, N) complex128 rows, written in place
+        want_output = True
+        if (out.dtype != np.complex128 or out.ndim != 2 or out.shape != (C, N)
+                or out.strides[1] != 16 or out.strides[0] % 16 or out.strides[0] < 16 * N):
+            raise ValueError("out must be a (C, N) complex128 array with contiguous rows")
+        ldo = out.strides[0] // 16
+    elif want_output:
+        out = np.zeros((C, N), dtype=np.complex128)
     err = ctypes.create_string_buffer(512)
     fn = L.gpd_fit_windows_c32 if c32 else L.gpd_fit_windows
     rc = fn(N, nwindow, C, ptr(t), ptr(d), N, ptr(fc), fc.shape[0], N, ptr(fop), ptr(st),
-            float(omega), ptr(xi), flags, int(maxfun), ptr(params), ptr(out), N, int(n_gpus), err,
+            float(omega), ptr(xi), flags, int(maxfun), ptr(params), ptr(out), ldo, int(n_gpus), err,
             len(err))
     check(rc, err)
     params = params.reshape(nwin, C)
@@ -385,10 +411,14 @@ def demodulate_windows(timestamp, data, window, *, faintparam=None, onlyhigh=Fal
             if isinstance(faintparam, FaintStates) else np.asarray(faintparam, dtype=np.int8)
     cols = np.ascontiguousarray(data.T)
     fop = np.array([fc_column_of(c) - 1 for c in range(1, 33)], dtype=np.int32)
+    out_cols = cols.copy()  # output = copy(data), written in place as in demodulateall
+    inplace = out_cols.dtype == np.complex128
     params, out = fit_windows(t, cols[:32], cols, fop, nwindow, state=state, fitoffsets=fitoffsets,
-                              onlyhigh=onlyhigh, want_output=True, method=method, n_gpus=n_gpus)
-    output = data.copy()
-    output[:, :32] = out.T
+                              onlyhigh=onlyhigh, want_output=True, method=method, n_gpus=n_gpus,
+                              out=out_cols[:32] if inplace else None)
+    if not inplace:
+        out_cols[:32] = out
+    output = out_cols.T
     return output, params, window_tables(params, N, nwindow, fitoffsets=fitoffsets)
 
 

@@ -266,7 +266,13 @@ int gpd_buildstates_dev(int64_t n_samples, const double *t, int64_t n1, const do
  * (src/Modulation.jl:373-396): per series k (column k of d, host buffers) and MetState, over the
  * valid samples (TRANSIENT dropped; GPD_ONLY_HIGH in flags keeps HIGH ∪ NORMAL),
  *   m = mean(abs, d[state .== s]),   w = 1 / var(abs.(d[state .== s]); mean = m)
- * — the faint power and weight the fit uses, computed by the same kernel, bit for bit.
+ * — computed by the kernels of the exact evaluator (method EXACT, and the harmonic path with
+ * GPD_FAINT_STATS=1|2), bit for bit the oracle's two-pass restatement.  The default
+ * whole-exposure harmonic path forms these statistics inside its moment pass (one pass,
+ * shifted sums per state: m within 1e-14, w within 1e-13 relative of these values) and its
+ * exact re-fit of FALLBACK series uses those, so faint GPD_ST_FALLBACK records are within that
+ * tolerance of the oracle rather than its bits (tests/test_gpu_parity.py
+ * ::test_faint_large_b_fallback_statistics).
  * out[10k + c] = m and out[10k + 5 + c] = w of MetState code c − 1 (c = 0 TRANSIENT … 4 HIGH;
  * NaN for a state without samples, w NaN for a 1-sample state, as Julia's 0/0).  Synchronous.
  */

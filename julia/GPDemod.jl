@@ -103,14 +103,24 @@ function demodulateall_gpu(timestamp::AbstractVector, data::AbstractMatrix{Compl
     length(timestamp) == N || error("voltage and time must have the same number of lines")
     t = Vector{Float64}(timestamp)
     c32 = T === Float32
-    d = c32 ? Matrix{ComplexF32}(data) : Matrix{ComplexF64}(data)  # column k = diode k
+    # column k = diode k; a Matrix already in the library's element type is passed as it is
+    # (no conversion copy of the 64 MB exposure)
+    d = c32 ? (data isa Matrix{ComplexF32} ? data : Matrix{ComplexF32}(data)) :
+              (data isa Matrix{ComplexF64} ? data : Matrix{ComplexF64}(data))
     state = faint_state_vector(faintparam, t, preswitchdelay, postwitchdelay)
     fcop = fc_columns()
     flags = UInt32((recenter ? GPD_RECENTER : 0) | (fitoffsets ? GPD_FIT_OFFSETS : 0) |
                    (onlyhigh ? GPD_ONLY_HIGH : 0) | method_flags(method))
     xinit = init isa Symbol ? C_NULL : Vector{Float64}(init)
     params = Vector{GpdParam}(undef, 32)
-    demod = Matrix{ComplexF64}(undef, N, 32)
+    # the reference's output = copy(data) (src/Modulation.jl:353): FC columns 33..40 pass
+    # through.  For ComplexF64 data the library writes the demodulated diodes straight into its
+    # columns 1..32 (out_demod = output, ldo = N): one copy of the exposure into memory that
+    # copy() has already touched, instead of a fresh matrix (page faults on the device-to-host
+    # copy) plus a second copy; ComplexF32 data takes the Float64 result through `demod`.
+    output = copy(data)
+    inplace = !c32 && output isa Matrix{ComplexF64}
+    demod = inplace ? output : Matrix{ComplexF64}(undef, N, 32)
     err = zeros(UInt8, 512)
     GC.@preserve t d state xinit params demod err begin
         if c32
@@ -130,11 +140,10 @@ function demodulateall_gpu(timestamp::AbstractVector, data::AbstractMatrix{Compl
         end
         gpd_assert_ok(rc, err)
     end
-    # the reference's return types (src/Modulation.jl:353-359, 434): output = copy(data) keeps
-    # Matrix{Complex{T}} (FC columns 33..40 pass through), param::Vector{Modulation…{T}},
-    # likelihood::Vector{T}; the library's Float64 results are converted to T
-    output = copy(data)
-    output[:, 1:32] .= Complex{T}.(demod)
+    # the reference's return types (src/Modulation.jl:353-359, 434): output keeps
+    # Matrix{Complex{T}}, param::Vector{Modulation…{T}}, likelihood::Vector{T}; the library's
+    # Float64 results are converted to T
+    inplace || (output[:, 1:32] .= Complex{T}.(demod))
     param = fitoffsets ?
         ModulationWithOffsets{T}[ModulationWithOffsets{T}(p.c, p.a, p.b, p.ϕ, M_2PI) for p in params] :
         ModulationNoOffsets{T}[ModulationNoOffsets{T}(p.a, p.b, p.ϕ, M_2PI) for p in params]

@@ -74,6 +74,18 @@ def test_bench_multi_rank_strong_scaling_bitwise(tmp_path, nproc):
     assert out["scaling"] == "strong" and out["value"] > 0
     assert one["config"]["total_series"] == 520 and len(r1) == 520 and len(rn) == 520
     assert r1.tobytes() == rn.tobytes(), "sharded records differ from the 1-rank run"
+    # the line diagnoses itself: every rank's shard, step time, kernels and gather time
+    di = out["distributed"]
+    assert di["world_size"] == nproc and di["backend"] == "gloo"
+    pr = di["per_rank"]
+    assert [r["rank"] for r in pr] == list(range(nproc))
+    assert sum(r["series"] for r in pr) == 520
+    assert [r["series_range"] for r in pr][0][0] == 0 and pr[-1]["series_range"][1] == 520
+    for r in pr:
+        assert r["step_ms"] > 0 and r["gather_ms"] is not None and r["gather_ms"] >= 0
+        assert {"moments", "fit_harmonic", "reduce"} <= set(r["kernels_ms"]), r["kernels_ms"]
+    assert di["step_ms_max_over_min"] >= 1.0
+    assert one["distributed"] is None
 
 
 def test_bench_weak_scaling_label(tmp_path):
@@ -93,3 +105,6 @@ def test_bench_rccl_branch_at_world_one(tmp_path):
     assert out["config"]["gather"].startswith("RCCL gather"), out["config"]
     assert out["n_gpus"] == 1 and out["value"] > 0
     assert len(rd) == 520 and r1.tobytes() == rd.tobytes(), "RCCL-gathered records differ"
+    di = out["distributed"]
+    assert di["world_size"] == 1 and di["backend"] == "nccl"
+    assert di["per_rank"][0]["series"] == 520 and di["per_rank"][0]["gather_ms"] > 0

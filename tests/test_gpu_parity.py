@@ -320,6 +320,32 @@ def test_large_b_falls_back_to_exact(gpu, oracle):
     print(assert_exact_bitwise(got, ref, label="fallback"))
 
 
+def test_faint_large_b_fallback_statistics(gpu, oracle, monkeypatch):
+    """Faint series whose harmonic fit falls back to the exact evaluator (advisor r4): the
+    re-fit takes the faint power/weight of the harmonic pass — by default the statistics fused
+    into the moment pass (one pass, shifted sums: m within 1e-14, w within 1e-13 of the
+    oracle's two-pass restatement, tests/test_gpu_faint_stats.py), so these records are the
+    oracle's within the χ² noise of that size, not bit for bit; with the separate statistics
+    kernels (GPD_FAINT_STATS=1) they are the oracle's bits, as method="exact" is."""
+    B, st = faint_batch(4000, 16, seed=41)
+    B2 = synth.make_batch(4000, 16, seed=41, b_range=(4.6, 5.5))
+    power = np.where(st == 3, 1.1, np.where(st == 1, 0.3, 0.6))
+    B["d"] = B2["d"] * power[None, :]
+    xinit = np.array([5.0, 0.3])
+    ref = oracle_fit(oracle, B, state=st, xinit=xinit)
+    got = fit(gpu, B, state=st, method="auto", xinit=xinit)
+    assert np.all(got["status"] & gpu.GPD_ST_FALLBACK) and np.all(got["status"] & gpu.GPD_ST_EXACT)
+    pert = perturbed_runs(oracle, B, ulps=512.0, state=st, xinit=xinit)
+    print(assert_fit_parity(got, ref, pert, label="faint fallback/fused statistics",
+                            min_match=0.5))
+    monkeypatch.setenv("GPD_FAINT_STATS", "1")
+    got1 = fit(gpu, B, state=st, method="auto", xinit=xinit)
+    assert np.all(got1["status"] & gpu.GPD_ST_FALLBACK)
+    print(assert_exact_bitwise(got1, ref, label="faint fallback/separate statistics"))
+    print(assert_exact_bitwise(fit(gpu, B, state=st, method="exact", xinit=xinit), ref,
+                               label="faint/exact/large b"))
+
+
 def test_demodulateall_one_exposure_full_size(gpu, oracle):
     """C2: one GRAVITY exposure, N×40 (32 diodes + 8 FC), N = 1e5, through the API mirror."""
     N = 100_000
