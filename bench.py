@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--dump-records", default=None,
                     help="rank 0 writes the gathered records (.npy, PARAM_DTYPE) here")
     ap.add_argument("--no-f64", action="store_true",
-                    help="skip the all-f64 moment-kernel (GPD_MIX=0) comparison steps")
+                    help="skip the all-f64 moment-kernel (option mix = 0) comparison steps")
     ap.add_argument("--samples", type=int, default=100_000)
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--t0", type=float, default=0.0)
@@ -254,8 +254,8 @@ def main():
         achieved = algo_bytes / (avg_ms * 1e-3) / 1e9
         # the same kernel against the dense fp64 MFMA peak: 4 real MACs per harmonic per
         # complex sample for the harmonics 1..16 on the f64 MFMAs (17..24 run on split-bf16
-        # MFMAs; GPD_MIX=0: all 24 on f64)
-        n_f64 = 24 if os.environ.get("GPD_MIX") == "0" else 16
+        # MFMAs; option mix = 0: all 24 on f64)
+        n_f64 = 24 if gpd.get_option("mix") == 0 else 16
         mfma_flops = 2.0 * 4 * n_f64 * P * N
         tflops = mfma_flops / (avg_ms * 1e-3) / 1e12
         roofline = {"bound": "hbm", "kernel": "k_moments", "achieved": round(achieved, 1),
@@ -279,12 +279,12 @@ def main():
     tr = truth.cpu().numpy().reshape(-1).view(rec)
     fits["median_abs_b_err_vs_truth"] = float(np.median(np.abs(par["b"] - tr["b"])))
 
-    # the same steps with every harmonic on the f64 MFMAs (GPD_MIX=0; the production kernel puts
+    # the same steps with every harmonic on the f64 MFMAs (option mix = 0; the production kernel puts
     # harmonics 17..24 on split-bf16 MFMAs), untimed by the headline
     f64_all = None
     if not args.no_f64 and world == 1:
-        log("all-f64 moment kernel comparison steps (GPD_MIX=0)")
-        os.environ["GPD_MIX"] = "0"
+        log("all-f64 moment kernel comparison steps (option mix = 0)")
+        gpd.set_option("mix", 0)
         try:
             step()
             torch.cuda.synchronize(dev)
@@ -296,14 +296,14 @@ def main():
             torch.cuda.synchronize(dev)
             el = time.perf_counter() - t1
         finally:
-            del os.environ["GPD_MIX"]
+            gpd.set_option("mix", 1)
         par64 = params.cpu().numpy().reshape(-1).view(rec).copy()
         step()  # leave the production records in `params`
         torch.cuda.synchronize(dev)
         f64_all = {"value": float(P_total) * N * args.steps / el,
                    "ms_per_step": 1e3 * el / args.steps,
                    "moments_ms": round(float(np.mean(km)), 3),
-                   "note": "GPD_MIX=0: all 24 harmonics on v_mfma_f64_16x16x4 (not the headline)",
+                   "note": "option mix = 0: all 24 harmonics on v_mfma_f64_16x16x4 (not the headline)",
                    "records": par64}
 
     # one C4 rank rehearsed on this GPU: the shard an 8-GPU node's rank fits (12 500 series of

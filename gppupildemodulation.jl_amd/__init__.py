@@ -14,8 +14,9 @@ The package directory name contains a dot, so load it by path, e.g.::
 """
 from ._lib import (GPD_FIT_OFFSETS, GPD_FP32, GPD_METHOD_EXACT, GPD_METHOD_HARMONIC, GPD_ONLY_HIGH,
                    GPD_RECENTER, GPD_ST_EXACT, GPD_ST_FALLBACK, GPD_ST_MAXFUN, GPD_ST_NAN,
-                   GPD_ST_REFIT, GPD_ST_SYNC, PARAM_DTYPE, GpdError, build_id, last_faint_stats,
-                   libm_eval, load, timings)
+                   GPD_ST_REFIT, GPD_ST_SYNC, PARAM_DTYPE, GpdError, build_id, get_option,
+                   last_faint_stats, libm_eval, load, option_names, options, options_from_env,
+                   reset_options, set_option, timings)
 from .demod import (DAY_TO_SEC, M_2PI, MJD_1970_1_1, Diode, FaintStates, MetState,
                     ModulationNoOffsets, ModulationWithOffsets, Side, buildfaintparameters,
                     buildstates, chi2_batch, compute_mean_var_power, demodulate_windows,
@@ -29,7 +30,8 @@ __all__ = [
     "GPD_FIT_OFFSETS", "GPD_FP32", "GPD_METHOD_EXACT", "GPD_METHOD_HARMONIC", "GPD_ONLY_HIGH", "GPD_RECENTER",
     "GPD_ST_EXACT", "GPD_ST_FALLBACK", "GPD_ST_MAXFUN", "GPD_ST_NAN", "GPD_ST_REFIT",
     "GPD_ST_SYNC",
-    "PARAM_DTYPE", "GpdError", "build_id", "last_faint_stats", "libm_eval", "load", "timings", "M_2PI", "Diode", "FaintStates", "MetState",
+    "PARAM_DTYPE", "GpdError", "build_id", "get_option", "last_faint_stats", "option_names",
+    "options", "options_from_env", "reset_options", "set_option", "libm_eval", "load", "timings", "M_2PI", "Diode", "FaintStates", "MetState",
     "ModulationNoOffsets", "ModulationWithOffsets", "Side", "buildstates", "chi2_batch",
     "demodulate_windows", "demodulateall", "fc_column_of", "fit_batch", "fit_windows", "idx",
     "window_length", "window_tables", "process_volt", "read_stefan_file", "DAY_TO_SEC",

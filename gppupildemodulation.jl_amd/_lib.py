@@ -49,7 +49,8 @@ EXPORTS = ("gpd_version", "gpd_strerror", "gpd_device_count", "gpd_fit_batch",
            "gpd_synth_fill_dev", "gpd_last_timings", "gpd_fit_windows", "gpd_fit_windows_dev",
            "gpd_process_volt", "gpd_fit_batch_c32", "gpd_fit_batch_c32_dev", "gpd_fit_windows_c32",
            "gpd_fit_windows_c32_dev", "gpd_buildstates_dev", "gpd_release", "gpd_libm_eval",
-           "gpd_mean_var_power", "gpd_build_id", "gpd_last_faint_stats")
+           "gpd_mean_var_power", "gpd_build_id", "gpd_last_faint_stats", "gpd_set_option",
+           "gpd_get_option", "gpd_reset_options", "gpd_option_name")
 
 
 class GpdError(RuntimeError):
@@ -124,6 +125,14 @@ def load():
     L.gpd_last_timings.restype = ctypes.c_int
     L.gpd_last_timings.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                    ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+    L.gpd_set_option.restype = ctypes.c_int
+    L.gpd_set_option.argtypes = [ctypes.c_char_p, I64]
+    L.gpd_get_option.restype = ctypes.c_int
+    L.gpd_get_option.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]
+    L.gpd_reset_options.restype = None
+    L.gpd_reset_options.argtypes = []
+    L.gpd_option_name.restype = ctypes.c_char_p
+    L.gpd_option_name.argtypes = [ctypes.c_int]
     if L.gpd_version() != GPD_ABI_VERSION:
         raise ImportError(f"libgpdemod ABI {L.gpd_version()} != {GPD_ABI_VERSION}")
     _lib = L
@@ -187,3 +196,60 @@ def timings(device: int = 0):
         k = names[i].decode()
         out[k] = out.get(k, 0.0) + ms[i]
     return out
+
+
+# ---- test and diagnostics controls (gpd_set_option; the library reads no environment) --------
+def set_option(name: str, value: int):
+    """Set one of the library's process-wide test/diagnostics options (include/gpdemod.h)."""
+    check(load().gpd_set_option(name.encode(), int(value)))
+
+
+def get_option(name: str) -> int:
+    v = ctypes.c_int64(0)
+    check(load().gpd_get_option(name.encode(), ctypes.byref(v)))
+    return v.value
+
+
+def reset_options():
+    """Every option back to its production default."""
+    load().gpd_reset_options()
+
+
+def option_names():
+    L, out, i = load(), [], 0
+    while (n := L.gpd_option_name(i)) is not None:
+        out.append(n.decode())
+        i += 1
+    return out
+
+
+class options:
+    """Context manager: `with options(mix=0, faint_stats=1): ...` sets the options for the block
+    and restores their previous values afterwards."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+        self.old = {}
+
+    def __enter__(self):
+        for k, v in self.kw.items():
+            self.old[k] = get_option(k)
+            set_option(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            set_option(k, v)
+        return False
+
+
+def options_from_env(var: str = "GPD_OPTS"):
+    """For the A/B tools only (never called by the package): apply "name=value,..." from the
+    environment variable `var` through set_option, and return the dict applied."""
+    spec = os.environ.get(var, "")
+    applied = {}
+    for item in filter(None, (x.strip() for x in spec.split(","))):
+        k, v = item.split("=", 1)
+        set_option(k.strip(), int(v))
+        applied[k.strip()] = int(v)
+    return applied

@@ -14,7 +14,7 @@ OUT_DIAG = os.path.join(HERE, "libgpdemod_diag.so")
 # translation units compiled in parallel and linked into one library (gpd_kernels.hpp GPD_OWNS:
 # unit 0 = host code + light kernels, the others = the heavy kernel instances)
 # the slowest units first (the exact path's instances), so the pool's tail is short
-SOURCES = ["gpd_part20.hip", "gpd_part21.hip", "gpd_part22.hip", "gpd_part23.hip", "gpd_part3.hip", "gpd_part4.hip", "gpd_part7.hip", "gpd_part8.hip", "gpd_part12.hip",
+SOURCES = ["gpd_part3.hip", "gpd_part4.hip", "gpd_part7.hip", "gpd_part8.hip", "gpd_part12.hip",
            "gpd_part13.hip", "gpd_part14.hip", "gpd_part15.hip", "gpd_part16.hip", "gpd_part17.hip",
            "gpd_part18.hip", "gpd_part19.hip", "gpd_part5.hip", "gpd_part9.hip",
            "gpd_part10.hip", "gpd_part11.hip", "gpd_part2.hip", "gpd_part6.hip", "gpd_part1.hip",

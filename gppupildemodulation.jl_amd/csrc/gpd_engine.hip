@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <climits>
 #include <cstdarg>
 #include <cstdio>
@@ -36,6 +37,52 @@ void set_err(char *buf, size_t len, const char *fmt, ...) {
     va_start(ap, fmt);
     vsnprintf(buf, len, fmt, ap);
     va_end(ap);
+}
+
+// Test and diagnostics controls (gpd_set_option, include/gpdemod.h).  The library reads no
+// environment variable: a process inheriting one cannot change the product path or the bits of
+// its records.  Every option defaults to the production behaviour; tests and the A/B tools set
+// them explicitly through the C-ABI and reset them afterwards.
+enum OptId {
+    O_MIX,           // 1: harmonics 17..24 on split-bf16 MFMAs; 0: all on f64 MFMAs (A/B)
+    O_FAINT_STATS,   // 0: faint statistics fused into the moment pass; 1: one-pass kernels; 2: two-pass
+    O_FAINT_SIDE,    // 1: separate faint statistics on the side stream (measured: no gain)
+    O_FAKE_GPUS,     // 1: keep n_gpus shards on fewer devices (shard g on device g mod ndev)
+    O_EXACT_G,       // 0: automatic workgroups per exact series; 1|2|4|8 forced
+    O_EXACT_WAVES,   // 0: automatic; 1|2 waves per SIMD of the exact fit
+    O_EXACT_WGT,     // 0: automatic; 64|256 threads per exact series
+    O_EXACT_FAST,    // 1: unconditional-load evaluator where it applies; 0: general form
+    O_EXACT_MCACHE,  // 1: model cache of the exact evaluator; 0: residual pass re-evaluates it
+    O_XSPIN_TEST,    // 1: the multi-workgroup barrier gives up at once (poison path, tests)
+    O_UNITS,         // 0: automatic sample units of the moment pass; n forced
+    O_UPW,           // 0: automatic units per moment workgroup; n forced
+    O_FIT_LANES,     // 0: automatic series per harmonic-fit wave; n forced
+    O_COHORTS,       // 1: one series cohort; n > 1: pipelined harmonic cohorts
+    O_HARM_MIN_SPAN, // shortest window fitted from harmonic moments (samples)
+    O_FS_COHORT_MB,  // |d| scratch per cohort of the one-pass faint statistics (MB)
+    O_MOMENTS,       // 0: automatic moment kernel; 1: VALU kernel; 2..7 diagnostics variants
+    O_FIT_PROF,      // 1: cycle split of the fit kernels on stderr (diagnostics)
+    O_SYNC_DEBUG,    // 1: synchronise after every stage and name the stage that faulted
+    O_COUNT
+};
+struct OptDef {
+    const char *name;
+    long long def;
+};
+constexpr OptDef kOpt[O_COUNT] = {
+    {"mix", 1},          {"faint_stats", 0},   {"faint_side", 0},    {"fake_gpus", 0},
+    {"exact_g", 0},      {"exact_waves", 0},   {"exact_wgt", 0},     {"exact_fast", 1},
+    {"exact_mcache", 1}, {"xspin_test", 0},    {"units", 0},         {"upw", 0},
+    {"fit_lanes", 0},    {"cohorts", 1},       {"harm_min_span", 256}, {"fs_cohort_mb", 4096},
+    {"moments", 0},      {"fit_prof", 0},      {"sync_debug", 0}};
+std::atomic<long long> g_opt[O_COUNT] = {
+    {1}, {0}, {0}, {0}, {0}, {0}, {0}, {1}, {1}, {0}, {0}, {0}, {0}, {1}, {256}, {4096}, {0}, {0}, {0}};
+inline long long opt(OptId o) { return g_opt[o].load(std::memory_order_relaxed); }
+int opt_find(const char *name) {
+    if (!name) return -1;
+    for (int i = 0; i < O_COUNT; ++i)
+        if (std::strcmp(kOpt[i].name, name) == 0) return i;
+    return -1;
 }
 
 #define HIP_TRY(expr)                                                                    \
@@ -142,7 +189,7 @@ struct Layout {
 int fit_lanes_for(long long P, int n_cu) {
     long long lanes = (P + std::max(1, n_cu) - 1) / std::max(1, n_cu);
     lanes = std::max<long long>(1, std::min<long long>(GPD_FIT_WAVE_LANES, lanes));
-    if (const char *e = getenv("GPD_FIT_LANES")) lanes = std::max(1, std::min(GPD_FIT_WAVE_LANES, atoi(e)));
+    if (opt(O_FIT_LANES) > 0) lanes = std::min<long long>(GPD_FIT_WAVE_LANES, opt(O_FIT_LANES));
     return (int)lanes;
 }
 
@@ -156,7 +203,7 @@ void moment_grid(long long N, long long P, int n_cu, bool harmonic, bool mfma, i
     // (32 groups: 4 waves; with 26, 3.25 → a quarter-filled last wave: moments 2.1 → 1.65 ms,
     // GPD_UNITS A/B, r3) and a faint 1e5 batch (97.75 waves).
     long long umax = faint ? 32 : 26;
-    if (const char *e = getenv("GPD_UNITS")) umax = std::max(1LL, atoll(e));  // A/B only
+    if (opt(O_UNITS) > 0) umax = opt(O_UNITS);  // A/B only
     long long U = std::min<long long>(umax, std::max<long long>(1, (N + 255) / 256));
     long long ulen = (N + U - 1) / U;
     ulen = (ulen + MM_TS - 1) / MM_TS * MM_TS;
@@ -173,7 +220,7 @@ void moment_grid(long long N, long long P, int n_cu, bool harmonic, bool mfma, i
             }
         }
     }
-    if (const char *e = getenv("GPD_UPW")) upw = std::min(U, std::max(1LL, atoll(e)));  // A/B only
+    if (opt(O_UPW) > 0) upw = std::min(U, opt(O_UPW));  // A/B only
     units = (int)U;
     unit_len = ulen;
     chunk = mfma ? upw * ulen : ulen;
@@ -182,7 +229,7 @@ void moment_grid(long long N, long long P, int n_cu, bool harmonic, bool mfma, i
 
 Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic, bool phbuf,
             bool mfma, int n_cu, bool harm_offs, bool windowed = false, int exact_g = 1,
-            bool fp32 = false, long long xround = 0) {
+            bool fp32 = false, bool mcache = true) {
     Layout L{};
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -228,12 +275,12 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     L.fcid = take(harm_offs ? (size_t)n_fc * sizeof(int32_t) : 0);
     L.d0 = take(harm_offs ? (size_t)2 * P * sizeof(double) : 0);
     // exact evaluator: one model-cache slot of N complex per workgroup of the fit grid
-    // (min(P, 1024) workgroups), or per series with the multi-workgroup split (per series of a
-    // round, xround, for the persistent cohort form), when that stays below 8 GB
-    const long long mc_slots = exact_g > 1 ? (xround > 0 ? std::min(P, xround) : P)
-                                           : std::min<long long>(P, 1024);
+    // (min(P, 1024) workgroups), or per series with the multi-workgroup split, when that stays
+    // below 8 GB; mcache = false (option exact_mcache = 0, A/B): none, the residual pass
+    // evaluates the model again
+    const long long mc_slots = exact_g > 1 ? P : std::min<long long>(P, 1024);
     const size_t mc_bytes = (size_t)mc_slots * (size_t)N * sizeof(c64);
-    L.mstride = (!harmonic && mc_bytes <= (size_t(8) << 30)) ? N : 0;
+    L.mstride = (!harmonic && mcache && mc_bytes <= (size_t(8) << 30)) ? N : 0;
     L.mcache = take(L.mstride ? mc_bytes : 0);
     // multi-workgroup exact fit: per-series block totals (2 slots × 8 blocks × 8 values) and
     // arrival counters (zeroed per launch)
@@ -243,8 +290,7 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     // of ~192 MB measured no faster: 3.54 vs 3.34 ms on C5), block totals of the cohort
     L.fs_mmax = (int)((N + 2047) / 2048);
     L.fs1 = faint && !windowed;
-    long long fs_mb = 4096;
-    if (const char *e = getenv("GPD_FS_COHORT_MB")) fs_mb = std::max(1LL, atoll(e));  // A/B only
+    const long long fs_mb = std::max(1LL, opt(O_FS_COHORT_MB));
     L.fs_pc = std::max<long long>(1, std::min<long long>(
         P, (fs_mb << 20) / ((long long)FS_G * L.fs_mmax * 256 * 8)));
     L.fs_pc = std::min<long long>(L.fs_pc, (1LL << 31) / FS_G - 1);
@@ -293,6 +339,28 @@ const char *gpd_build_id(void) { return kBuildIdMarker + 13; }
 const char *gpd_strerror(int code) {
     if (code > 0 || code < -5) return "unknown error";
     return kErrStr[-code];
+}
+
+int gpd_set_option(const char *name, int64_t value) {
+    const int i = opt_find(name);
+    if (i < 0) return GPD_E_ARG;
+    g_opt[i].store(value, std::memory_order_relaxed);
+    return GPD_OK;
+}
+
+int gpd_get_option(const char *name, int64_t *value) {
+    const int i = opt_find(name);
+    if (i < 0 || !value) return GPD_E_ARG;
+    *value = opt((OptId)i);
+    return GPD_OK;
+}
+
+void gpd_reset_options(void) {
+    for (int i = 0; i < O_COUNT; ++i) g_opt[i].store(kOpt[i].def, std::memory_order_relaxed);
+}
+
+const char *gpd_option_name(int index) {
+    return index >= 0 && index < O_COUNT ? kOpt[index].name : nullptr;
 }
 
 int gpd_device_count(void) {
@@ -370,18 +438,19 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     const bool offs = (flags & GPD_FIT_OFFSETS) != 0;
     // fp64 MFMA moment pass (producer/consumer kernel, non-temporal series loads); the VALU
     // kernel when a series row or the cos/sin table exceeds the buffer descriptors' 32-bit
-    // offsets (N ≳ 1e6 samples) — GPD_MOMENTS=valu forces it (tests of that fallback)
-    const char *mk = getenv("GPD_MOMENTS");
+    // offsets (N ≳ 1e6 samples) — option moments = 1 forces it (tests of that fallback);
+    // moments = 2..7: the diagnostics build's timing variants
+    const long long mk = opt(O_MOMENTS);
     // buffer descriptors of the MFMA kernels address 128 series rows / the cos-sin table
     // with 32-bit offsets
     const double esz = is_c32 ? 8.0 : 16.0;  // bytes per stored complex element
-    const bool use_mfma = !(mk && std::string(mk) == "valu") &&
+    const bool use_mfma = mk != 1 &&
                           (double)MM_PIX * (double)ldd * esz < 2147483648.0 &&
                           (double)(n_samples + MM_TS) * KH * 16.0 < 2147483648.0;
     // mixed-precision moment kernel (harmonics 17..24 on split-bf16 MFMAs);
-    // GPD_MIX=0 keeps all harmonics on the f64 MFMAs (A/B runs and precision checks; read per
-    // call so a test can switch it)
-    const bool mix = !(getenv("GPD_MIX") && std::string(getenv("GPD_MIX")) == "0");
+    // option mix = 0 keeps all harmonics on the f64 MFMAs (A/B runs and precision checks; read
+    // per call so a test can switch it)
+    const bool mix = opt(O_MIX) != 0;
     // Harmonic fitoffsets (non-faint, on request): the χ² of the 2×2 system needs the moments
     // G_n of the FC phasors (producer/consumer kernel in UNIT mode over the FC columns) and Σ d
     // per series.  METHOD_EXACT uses the exact evaluator; so do windows with fitoffsets.
@@ -392,8 +461,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     // iterate; METHOD_HARMONIC asks for the fast path anyway (parity ~1e-9).
     // Windows of ≥ HARM_MIN_SPAN samples: harmonic moments from k_moments_win (a shorter last
     // window is re-fitted exactly); shorter windows: the exact evaluator.
-    long long harm_min = HARM_MIN_SPAN;
-    if (const char *e = getenv("GPD_HARM_MIN_SPAN")) harm_min = std::max(1LL, atoll(e));  // sweep only
+    const long long harm_min = std::max(1LL, opt(O_HARM_MIN_SPAN));  // HARM_MIN_SPAN; sweeps only
     const bool want_exact =
         fp32 || (flags & GPD_METHOD_EXACT) || (window > 0 && window < harm_min) ||
         (offs && !(harm_offs_ok && window == 0 && (flags & GPD_METHOD_HARMONIC)));
@@ -415,7 +483,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     if (cx->n_cu == 0) HIP_TRY(hipDeviceGetAttribute(&cx->n_cu, hipDeviceAttributeMultiprocessorCount, device));
     // Small whole-exposure exact fits (one exposure: 32 series) spread each series over G
     // workgroups, one per CU (all resident: the per-series barrier needs its G parts on chip);
-    // the canonical reduction order makes the records identical for every G.  GPD_EXACT_G
+    // the canonical reduction order makes the records identical for every G.  Option exact_g
     // forces G (tests of that identity).
     int exact_g = 1;
     if (want_exact && !bphi && window == 0) {
@@ -424,73 +492,14 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         const long long filled = std::min<long long>(8, (N + 255) / 256);
         for (int gg = 8; gg >= 2 && exact_g == 1; gg >>= 1)
             if (p8 * gg <= cx->n_cu && gg <= filled) exact_g = gg;
-        if (const char *e = getenv("GPD_EXACT_G")) {
-            const int f = atoi(e);
-            if ((f == 1 || f == 2 || f == 4 || f == 8) && p8 * f <= (long long)cx->n_cu) exact_g = f;
+        if (const long long f = opt(O_EXACT_G)) {
+            if ((f == 1 || f == 2 || f == 4 || f == 8) && p8 * f <= (long long)cx->n_cu) exact_g = (int)f;
         }
     }
-    // Large whole-exposure exact batches, cohort form (r4, GPD_EXACT_COHORT=1): every series
-    // split over G = 8 workgroups and the grid persistent — exactly the workgroups resident at
-    // two per CU, a multiple of 8·G — so 2·n_cu / 8 series are in flight, their samples, model
-    // cache slots and shared phasor columns within the Infinity Cache over their ~70 passes.
-    // The per-series barrier needs all G parts resident: the grid never exceeds what the chip
-    // holds at once.  The records are the G = 1 records (canonical order).
-    long long xround = 0;
-    unsigned xgrid = 0;
-    // LDS model cache (r4): with G = 8 each thread of a part owns one canonical chain of
-    // ⌈N / 2048⌉ samples; the head of every chain's model (xlml samples, as many as the CU's LDS
-    // holds beside the kernel's static LDS) stays in LDS between the first and the residual
-    // pass, the rest in the part's global slot.  One workgroup per CU.  Measured slower than
-    // the global cache (C2 exact 3.32 → 3.46 ms, the residual pass 2.05 → 2.49 M cycles per
-    // workgroup; the C5 cohort form 375 → 486 ms at one workgroup per CU instead of two,
-    // profiles/r4/exact_lmc/), so opt-in: GPD_EXACT_LMC=1.
-    bool lmc_on = getenv("GPD_EXACT_LMC") && atoi(getenv("GPD_EXACT_LMC")) == 1;
-    // Split form (r4): at G = 8 every canonical chain shared by two threads of a 512-thread part
-    // (k_fit_exact WGT = 512, ExactChi2::cr_split_chain): two waves per SIMD where the G = 8
-    // form has one; the same records.  Measured slower (C2 exact 2.95-3.01 → 3.47 ms, fitoffsets
-    // 3.78-3.80 → 4.52-4.56 ms: the part's first pass takes as many cycles with twice the waves;
-    // profiles/r4/exact_split_pair/), so opt-in: GPD_EXACT_SPLIT=1.
-    const bool split_on = getenv("GPD_EXACT_SPLIT") && atoi(getenv("GPD_EXACT_SPLIT")) == 1 &&
-                          !fp32;
-    if (split_on) lmc_on = false;
-    const char *coh = getenv("GPD_EXACT_COHORT");
-    const int coh_mode = coh ? atoi(coh) : 0;
-    if (want_exact && !bphi && window == 0 && exact_g == 1 && !fp32 && P * 8 > cx->n_cu &&
-        coh_mode > 0 && N >= (long long)CR_SLOTS) {
-        // cohort form: two 256-thread workgroups per CU (global model cache), or one with the
-        // LDS model cache or in the split form
-        const long long cap = ((lmc_on || split_on ? 1LL : 2LL) * cx->n_cu) / 64 * 64;
-        if (cap >= 64) {
-            exact_g = 8;
-            xgrid = (unsigned)cap;
-            xround = cap / 8;
-        }
-    }
-    int xlml = 0;
-    size_t xlds_bytes = 0;
-    if (want_exact && !bphi && window == 0 && exact_g == CR_BLOCKS && !fp32 && lmc_on) {
-        hipFuncAttributes fa;
-        HIP_TRY(hipFuncGetAttributes(&fa, (const void *)k_fit_exact<false, true, false>));
-        int lds_max = 0;
-        HIP_TRY(hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor,
-                                      device));
-        const long long chain = (N + CR_SLOTS - 1) / CR_SLOTS;
-        const long long room = ((long long)lds_max - (long long)fa.sharedSizeBytes - 256) /
-                               ((long long)EXACT_WG * (long long)sizeof(c64));
-        xlml = (int)std::max<long long>(0, std::min<long long>(room, chain));
-        xlds_bytes = (size_t)xlml * EXACT_WG * sizeof(c64);
-    }
+    // (r5: the measured-slower exact forms of r4 — the cohort form, the LDS model cache and the
+    // split form, DESIGN.md §12 — are gone from the library; git history keeps them)
     const Layout L = plan(N, P, n_fc, faint, harmonic, phbuf, use_mfma, cx->n_cu, harm_offs,
-                          window > 0, exact_g, fp32, xround);
-    if (xlml > 0 && L.mstride == 0 && (long long)xlml * CR_SLOTS < N) {  // no global tail slot
-        xlml = 0;
-        xlds_bytes = 0;
-    }
-    // the split form needs the model cache (its sums run through cr_sum2m only) and 256 × NV
-    // doubles of LDS for its first butterfly step (NV = 8 with offsets, 4 without)
-    const bool split = split_on && want_exact && !bphi && window == 0 && exact_g == CR_BLOCKS &&
-                       L.mstride != 0 && xlml == 0;
-    const size_t split_lds = split ? (size_t)(offs ? 8 : 4) * EXACT_WG * sizeof(double) : 0;
+                          window > 0, exact_g, fp32, opt(O_EXACT_MCACHE) != 0);
     if (cx->ws_cap < L.total) {
         if (cx->ws) {
             cx->last_fstat = nullptr;  // points into the workspace being freed (advisor r4)
@@ -558,7 +567,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
 
     int nt = 0, ne = 0;
     // GPD_SYNC_DEBUG=1: synchronise after every stage and name the stage that faulted
-    static const bool sync_debug = getenv("GPD_SYNC_DEBUG") != nullptr;
+    const bool sync_debug = opt(O_SYNC_DEBUG) != 0;
     auto rec = [&](hipStream_t s) -> int {  // a timing event on stream s (index, or -1)
         if (ne >= kMaxEv) {
             static bool warned = false;
@@ -586,7 +595,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     };
     int lastA = rec(stream);  // consecutive intervals on the caller's stream
     auto mark = [&](const char *name) { lastA = mark_on(stream, lastA, name); };
-    // diagnostic counters (GPD_FIT_PROF, GPD_MOMENTS=ws_prof): zeroed, read back after the kernel
+    // diagnostic counters (options fit_prof, moments = 7): zeroed, read back after the kernel
     unsigned long long prof_h[PROF_LEN] = {};
     auto prof_reset = [&]() { return hipMemsetAsync(pb.prof, 0, sizeof prof_h, stream); };
     auto prof_read = [&]() {
@@ -607,15 +616,14 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     // caller's stream while cohort c−1's fit (latency-bound NEWUOA lanes, a few CUs) runs on the
     // side stream.  Per-series results do not depend on the cohort (fixed sample units, §7 of
     // DESIGN.md), so the records equal the one-cohort run's bit for bit.  Off by default
-    // (GPD_COHORTS=n opts in): the last cohort's fit is one round of waves whose latency
+    // (option cohorts = n opts in): the last cohort's fit is one round of waves whose latency
     // (~1.1-1.4 ms) is exposed whatever the cohort size, so C3, C4 and C5 gained nothing
     // (profiles/r3/cohorts.txt).
-    static const bool fit_prof_env = getenv("GPD_FIT_PROF") != nullptr;
+    const bool fit_prof = opt(O_FIT_PROF) != 0;  // diagnostics only
     int cohorts = 1;
-    if (harmonic && use_mfma && window == 0 && !bphi && !harm_offs && !fit_prof_env &&
-        !(mk && std::string(mk).rfind("ws_", 0) == 0)) {
-        cohorts = 1;  // measured: no gain by default, GPD_COHORTS opts in
-        if (const char *e = getenv("GPD_COHORTS")) cohorts = std::max(1, std::min(kMaxCohorts, atoi(e)));
+    if (harmonic && use_mfma && window == 0 && !bphi && !harm_offs && !fit_prof && mk < 2) {
+        // measured: no gain by default; option cohorts = n opts in
+        cohorts = (int)std::max(1LL, std::min<long long>(kMaxCohorts, opt(O_COHORTS)));
         cohorts = (int)std::min<long long>(cohorts, std::max<long long>(1, P / (2 * MM_PIX)));
     }
     auto ensure_side = [&]() -> hipError_t {  // the high-priority side stream and its events
@@ -633,14 +641,14 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     // pass on the side stream — measured on C5 (r3): no gain, both passes stream HBM (statistics
     // 2.57 → 4.5 ms, moments 1.8 → 3.5 ms when overlapped); off by default.
     const bool fsplit_on = faint && harmonic && use_mfma && window == 0;
-    const bool faint_side = getenv("GPD_FAINT_SIDE") && std::string(getenv("GPD_FAINT_SIDE")) == "1";
+    const bool faint_side = opt(O_FAINT_SIDE) == 1;
     // the state-split moment pass also forms compute_mean_var_power's sums (k_moments_ws<FAINT>
-    // producers, k_faint_fused_fin): one HBM pass for the faint series (r4).  GPD_FAINT_STATS=1
-    // (one-pass kernels k_faint_p1/p2/fin) or 2 (two-pass kernel) computes the statistics
-    // separately instead — the exact evaluator's statistics, bit for bit the oracle's (A/B and
-    // tests).
-    const char *fse = getenv("GPD_FAINT_STATS");
-    const bool fused = fsplit_on && !(fse && (std::string(fse) == "1" || std::string(fse) == "2"));
+    // producers, k_faint_fused_fin): one HBM pass for the faint series (r4).  Option
+    // faint_stats = 1 (one-pass kernels k_faint_p1/p2/fin) or 2 (two-pass kernel) computes the
+    // statistics separately instead — the exact evaluator's statistics, bit for bit the
+    // oracle's (A/B and tests).
+    const long long fse = opt(O_FAINT_STATS);
+    const bool fused = fsplit_on && !(fse == 1 || fse == 2);
     double *fsp = (double *)(ws + L.fsp), *fixs = (double *)(ws + L.fixs);
     int *fcnt = (int *)(ws + L.fcnt);
     unsigned *smask = (unsigned *)(ws + L.smask);
@@ -666,8 +674,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         mark("table");
         int *ccount = list + P + 64;  // one fallback counter per cohort
         HIP_TRY(hipMemsetAsync(ccount, 0, kMaxCohorts * sizeof(int), stream));
-        const bool fs1 = L.fs1 && !(getenv("GPD_FAINT_STATS") &&
-                                    std::string(getenv("GPD_FAINT_STATS")) == "2");
+        const bool fs1 = L.fs1 && fse != 2;
         const long long step = ((P + cohorts - 1) / cohorts + MM_PIX - 1) / MM_PIX * MM_PIX;
         int c = 0;
         for (long long k0 = 0; k0 < P; k0 += step, ++c) {
@@ -756,9 +763,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     } else if (faint && !fused) {
         // whole-exposure series: one pass over the series, one hypot per sample (k_faint_p1/p2/
         // fin); windows: the two-pass kernel over each window's span (same bits);
-        // GPD_FAINT_STATS=2 forces the two-pass kernel (tests of that identity)
-        const bool fs1 = L.fs1 && !(getenv("GPD_FAINT_STATS") &&
-                                    std::string(getenv("GPD_FAINT_STATS")) == "2");
+        // option faint_stats = 2 forces the two-pass kernel (tests of that identity)
+        const bool fs1 = L.fs1 && fse != 2;
         auto run_stats = [&](hipStream_t s) -> hipError_t {
             if (fs1)
                 return run_faint_onepass(pb, fstat, (double *)(ws + L.fsx),
@@ -819,7 +825,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                 k_moments_ws<0, false, c32, 2, false, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, smask, fsp, fcnt, dhdr);
             else if (faint)
                 k_moments_ws<0, false, c64, 2, false, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, smask, fsp, fcnt, dhdr);
-            else if (!tmix && is_c32)  // all-f64 MFMA variants (GPD_MIX=0)
+            else if (!tmix && is_c32)  // all-f64 MFMA variants (option mix = 0)
                 k_moments_ws<0, false, c32, 2, false><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
             else if (!tmix)
                 k_moments_ws<0, false, c64, 2, false><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
@@ -827,17 +833,17 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                 k_moments_ws<0, false, c32, 2><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
 #ifdef GPD_DIAG
             // timing variants (results invalid), diagnostics build only (build.py --diag)
-            else if (mk && std::string(mk) == "ws_nomfma")
+            else if (mk == 2)  // ws_nomfma
                 k_moments_ws<1><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
-            else if (mk && std::string(mk) == "ws_noload")
+            else if (mk == 3)  // ws_noload
                 k_moments_ws<2><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
-            else if (mk && std::string(mk) == "ws_nof0")
+            else if (mk == 4)  // ws_nof0
                 k_moments_ws<7><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
-            else if (mk && std::string(mk) == "ws_noq")
+            else if (mk == 5)  // ws_noq
                 k_moments_ws<8><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
-            else if (mk && std::string(mk) == "ws_mfmaonly")
+            else if (mk == 6)  // ws_mfmaonly
                 k_moments_ws<5><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
-            else if (mk && std::string(mk) == "ws_prof") {  // cycle split per role (stderr)
+            else if (mk == 7)  // ws_prof {  // cycle split per role (stderr)
                 HIP_TRY(prof_reset());
                 k_moments_ws<6><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
                 HIP_TRY(prof_read());
@@ -911,7 +917,6 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             cx->have_timers = true;
             return GPD_OK;
         }
-        static const bool fit_prof = getenv("GPD_FIT_PROF") != nullptr;  // diagnostics only
         if (fit_prof) {
             HIP_TRY(prof_reset());
             Problem pp = pb;
@@ -937,10 +942,6 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                     "n/a\n", (double)z[4] / nw, (double)zn[8] / nw, (double)zn[9] / nw,
                     (double)zn[11] / nw, (double)zn[12] / nw, (double)zn[13] / nw,
                     (double)zn[14] / nw);
-            // the phase-scheduled driver (drive_fit_sched): slot 5/13 = its glue (lane/wave
-            // level), slot 6 = rounds per wave, slot 7/15 = evaluation rounds (lane/wave)
-            fprintf(stderr, "fit_prof sched per wave: glue %.3g cycles, rounds %.3g, eval phase %.3g "
-                    "cycles\n", (double)zn[13] / nw, (double)zn[6] / nw, (double)zn[15] / nw);
 #endif
         } else {
             Problem pf = pb;
@@ -976,34 +977,31 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         }
         if (exact_g > 1) {
             HIP_TRY(hipMemsetAsync(ws + L.xcnt, 0, (size_t)(P + 3) / 4 * 16, stream));
-            // GPD_XSPIN_TEST=1 (tests): the per-series barrier gives up at once (poison path)
-            if (getenv("GPD_XSPIN_TEST") && atoi(getenv("GPD_XSPIN_TEST")) > 0) pb.flags |= F_XSPIN_TEST;
+            // option xspin_test (tests): the per-series barrier gives up at once (poison path)
+            if (opt(O_XSPIN_TEST) > 0) pb.flags |= F_XSPIN_TEST;
         }
-        // GPD_EXACT_FAST=0 (A/B, tests): the evaluator's general load path everywhere
-        if (getenv("GPD_EXACT_FAST") && atoi(getenv("GPD_EXACT_FAST")) == 0) pb.flags |= F_NOFAST;
-        // GPD_FIT_PROF (diagnostics): per-phase cycles of the multi-workgroup exact fit
-        static const bool xprof = getenv("GPD_FIT_PROF") != nullptr;
-        if (xprof && exact_g > 1 && !bphi) {
+        // option exact_fast = 0 (A/B, tests): the evaluator's general load path everywhere
+        if (opt(O_EXACT_FAST) == 0) pb.flags |= F_NOFAST;
+        // option fit_prof (diagnostics): per-phase cycles of the multi-workgroup exact fit
+        if (fit_prof && exact_g > 1 && !bphi) {
             pb.flags |= F_PROF;
             HIP_TRY(prof_reset());
         }
         const unsigned fit_grid =
-            xgrid ? xgrid : exact_g > 1 ? (unsigned)((P + 7) / 8 * 8 * exact_g) : exact_grid;
+            exact_g > 1 ? (unsigned)((P + 7) / 8 * 8 * exact_g) : exact_grid;
         // two waves per SIMD (k_fit_exact MINB = 2) when the grid needs more than one round of
-        // one-wave-per-SIMD workgroups, and for the persistent cohort form (its grid is two
-        // workgroups per CU); GPD_EXACT_WAVES=1|2 forces it (A/B and tests)
-        bool two_waves = (xgrid && xlml == 0) ||
-                         (exact_g == 1 && (long long)fit_grid * (EXACT_WG / 64) > 4LL * cx->n_cu);
-        if (const char *e = getenv("GPD_EXACT_WAVES")) two_waves = atoi(e) == 2 && exact_g == 1;
+        // one-wave-per-SIMD workgroups; option exact_waves = 1|2 forces it (A/B and tests)
+        bool two_waves = exact_g == 1 && (long long)fit_grid * (EXACT_WG / 64) > 4LL * cx->n_cu;
+        if (opt(O_EXACT_WAVES) > 0) two_waves = opt(O_EXACT_WAVES) == 2 && exact_g == 1;
         // short spans (every series or window ≤ 2048 samples = one sample per canonical slot,
         // e.g. windows of ≤ 4 s at 500 Hz): one wave per series (k_fit_exact WGT = 64; the same
         // records), no model cache, a persistent grid of two waves per SIMD — measured faster
         // from 100- to 2000-sample windows, slower on 5000 and on whole 1e5-sample series
-        // (DESIGN.md §9).  GPD_EXACT_WGT=64|256 forces it (A/B, tests).
+        // (DESIGN.md §9).  Option exact_wgt = 64|256 forces it (A/B, tests).
         const long long span = window > 0 ? std::min<long long>(window, N) : N;
         bool one_wave = exact_g == 1 && span <= CR_SLOTS &&
                         P > kOneWaveMinSeriesPerCU * std::max(1, cx->n_cu);
-        if (const char *e = getenv("GPD_EXACT_WGT")) one_wave = exact_g == 1 && atoi(e) == 64;
+        if (opt(O_EXACT_WGT) > 0) one_wave = exact_g == 1 && opt(O_EXACT_WGT) == 64;
         const unsigned grid64 = (unsigned)std::min<long long>(P, 8LL * std::max(1, cx->n_cu));
 #define GPD_LAUNCH_EXACT(FA, OF, PH)                                                                 \
     do {                                                                                        \
@@ -1014,28 +1012,16 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             k_fit_exact<FA, OF, PH, 2, 64><<<grid64, 64, 0, stream>>>(                         \
                 pb, info, ph, fstat, nullptr, nullptr, outp, raw, 0, nullptr, 0, 1, nullptr,    \
                 nullptr);                                                                       \
-        else if (split) {                                                                       \
-            HIP_TRY(hipFuncSetAttribute((const void *)k_fit_exact<FA, OF, PH, 1, 2 * EXACT_WG>,  \
-                                        hipFuncAttributeMaxDynamicSharedMemorySize,              \
-                                        (int)split_lds));                                        \
-            k_fit_exact<FA, OF, PH, 1, 2 * EXACT_WG><<<fit_grid, 2 * EXACT_WG, split_lds,       \
-                                                       stream>>>(                               \
-                pb, info, ph, fstat, nullptr, nullptr, outp, raw, 0, (c64 *)(ws + L.mcache),    \
-                L.mstride, exact_g, (double *)(ws + L.xtot), (unsigned *)(ws + L.xcnt), 0);     \
-        } else if (two_waves)                                                                   \
+        else if (two_waves)                                                                   \
             k_fit_exact<FA, OF, PH, 2><<<fit_grid, EXACT_WG, 0, stream>>>(                    \
                 pb, info, ph, fstat, nullptr, nullptr, outp, raw, 0,                            \
                 L.mstride ? (c64 *)(ws + L.mcache) : nullptr, L.mstride, exact_g,               \
                 (double *)(ws + L.xtot), (unsigned *)(ws + L.xcnt));                            \
         else {                                                                                  \
-            if (xlds_bytes > 0)                                                                 \
-                HIP_TRY(hipFuncSetAttribute((const void *)k_fit_exact<FA, OF, PH>,              \
-                                            hipFuncAttributeMaxDynamicSharedMemorySize,          \
-                                            (int)xlds_bytes));                                   \
-            k_fit_exact<FA, OF, PH><<<fit_grid, EXACT_WG, xlds_bytes, stream>>>(              \
+            k_fit_exact<FA, OF, PH><<<fit_grid, EXACT_WG, 0, stream>>>(                       \
                 pb, info, ph, fstat, nullptr, nullptr, outp, raw, 0,                            \
                 L.mstride ? (c64 *)(ws + L.mcache) : nullptr, L.mstride, exact_g,               \
-                (double *)(ws + L.xtot), (unsigned *)(ws + L.xcnt), xlml);                      \
+                (double *)(ws + L.xtot), (unsigned *)(ws + L.xcnt));                            \
         }                                                                                       \
     } while (0)
         if (faint) {
@@ -1198,10 +1184,10 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
         set_err(errbuf, errlen, "gpd_batch: no HIP device visible");
         return GPD_E_NODEV;
     }
-    // GPD_FAKE_GPUS=1 (tests): keep n_gpus shards even beyond the visible devices, shard g on
+    // option fake_gpus = 1 (tests): keep n_gpus shards even beyond the visible devices, shard g on
     // device g % ndev — the multi-device split (series / window ranges, FC column subsets,
     // record offsets) then runs on a one-GPU box exactly as on an 8-GPU node
-    const bool fake = getenv("GPD_FAKE_GPUS") && atoi(getenv("GPD_FAKE_GPUS")) > 0;
+    const bool fake = opt(O_FAKE_GPUS) > 0;
     int G = n_gpus <= 0 ? 1 : (fake ? std::min<int>(n_gpus, 64) : std::min<int>(n_gpus, ndev));
     const int64_t nwin = window > 0 ? (n_samples + window - 1) / window : 0;
     G = (int)std::min<int64_t>(G, window > 0 ? nwin : n_pixels);
@@ -1553,7 +1539,7 @@ int gpd_mean_var_power(int64_t n_samples, int64_t n_series, const gpd_c64 *d, in
                        const int8_t *state, uint32_t flags, double *out, int device, char *errbuf,
                        size_t errlen) {
     // compute_mean_var_power (src/Faint.jl:89-100) of whole series with demodulateall's valid
-    // mask — the statistics the fit uses (the one-pass kernels; GPD_FAINT_STATS=2: the two-pass
+    // mask — the statistics the fit uses (the one-pass kernels; option faint_stats = 2: the two-pass
     // kernel the windows use)
     if (n_samples < 1 || n_series < 1 || !d || !state || !out || ldd < n_samples) {
         set_err(errbuf, errlen, "gpd_mean_var_power: invalid shapes/pointers");
@@ -1571,7 +1557,7 @@ int gpd_mean_var_power(int64_t n_samples, int64_t n_series, const gpd_c64 *d, in
     HIP_TRY(hipSetDevice(device));
     const long long N = n_samples, P = n_series;
     const bool fs1 =
-        !(getenv("GPD_FAINT_STATS") && std::string(getenv("GPD_FAINT_STATS")) == "2");
+        opt(O_FAINT_STATS) != 2;
     const Layout L = plan(N, P, 1, true, false, false, false, 0, false);  // fs_pc, fs_mmax
     c64 *dd = nullptr;
     int8_t *dst = nullptr;

@@ -32,7 +32,6 @@
 #define GPD_U_MOM 0x44    // units 2, 6: k_moments_ws (Float64 / Float32 storage)
 #define GPD_U_EXACT 0xF198  // units 3, 4, 7, 8 / 12-15: k_fit_exact (faint × offsets, MINB 1 / 2)
 #define GPD_U_EXACT64 0xF0000  // units 16-19: k_fit_exact one wave per series (faint × offsets)
-#define GPD_U_EXACT512 0xF00000  // units 20-23: k_fit_exact split form, 512 threads per part
 #define GPD_U_CHI2X 0xE20  // units 5, 9, 10, 11: k_chi2_exact, k_refine_exact
 
 namespace gpd {
@@ -61,7 +60,7 @@ constexpr uint32_t F_PROF = 0x80000000u;  // internal: k_fit_harmonic cycle spli
 constexpr uint32_t F_XSPIN_TEST = 0x40000000u;
 // internal (A/B, tests): the exact evaluator's general load path even where FAST applies
 constexpr uint32_t F_NOFAST = 0x20000000u;
-// Diagnostic cycle counters (GPD_FIT_PROF, GPD_MOMENTS=ws_prof) live in the workspace, reached
+// Diagnostic cycle counters (options fit_prof, moments = 7: ws_prof) live in the workspace, reached
 // through Problem::prof: [0..3] fit split (objective, whole fit, evals, exact exchange),
 // [8..15] moment-kernel roles, [16..31] NEWUOA phases (diagnostics build: lane- and wave-level)
 constexpr int PROF_FIT = 0, PROF_WS = 8, PROF_NW = 16, PROF_LEN = 40;
@@ -217,190 +216,6 @@ __device__ __forceinline__ void drive_fit(F &f, const Problem &pb, double (&x)[2
         if (!(lklval > f(xf))) break;  // "bad minima" (src/Modulation.jl:411-414)
         status |= ST_REFIT;
         x[1] = php;
-    }
-}
-
-// A/B: 0 = greedy (the phase most lanes wait at), 1 = fixed cyclic order of the phases
-#ifndef GPD_SCHED_POLICY
-#define GPD_SCHED_POLICY 0
-#endif
-// A/B: inline the NEWUOA phases at their one call site each in drive_fit_sched
-#if defined(GPD_SCHED_INLINE) && GPD_SCHED_INLINE
-#define GPD_SCHED_INL [[clang::always_inline]]
-#else
-#define GPD_SCHED_INL
-#endif
-// The same driver for a wave of lane-per-series fits (k_fit_harmonic, r4): every lane's drive —
-// the 8-point grid, NEWUOB (NewuoaCo, gpd_newuoa.hpp), the π-flip check and its re-fit — is a
-// sequence of heavy phases (objective evaluations, TRSAPP, BIGLAG, BIGDEN, UPDATE) joined by
-// light code.  Each round the wave picks the phase most of its lanes wait at (ties: evaluation,
-// TRSAPP, UPDATE, BIGLAG, BIGDEN), runs it for those lanes and then their light code up to
-// their next heavy phase; the others wait.  A phase then executes about as often as the lane
-// needing it most (a greedy schedule over recorded NEWUOA traces: 1.2 M instead of 1.9 M cycles
-// per 64-series wave), where run()'s goto structure made the wave execute the union of the
-// lanes' orders.  Per lane the arithmetic and its order are drive_fit's and run()'s, so the
-// records are the same bits (tests/test_abi.py::test_newuoa_coroutine_equals_run_bitwise,
-// and on the device every harmonic parity test).  Lanes whose expansion went out of range
-// (f.fallback) stop: their series is re-fitted by the exact evaluator.
-template <class F, class NW>
-__device__ __forceinline__ void drive_fit_sched(F &f, const Problem &pb, double (&x)[2],
-                                                int &status, NW &nw) {
-    NewuoaCo<2, 5, true> co;
-    enum { S_GRID, S_RUN1, S_FLIPA, S_FLIPB, S_RUN2, S_DONE };
-    int stage, ph, gk = 0, best = 0;
-    double fb = 0.0, lkl = 0.0, php = 0.0, px[2];
-    bool g = false;  // glue pending (NEWUOB started or resumed)
-    int last = 4;    // GPD_SCHED_POLICY 1: index of the last phase run (cyclic order)
-    (void)last;
-    if (pb.has_xinit) {
-        x[0] = pb.x0;
-        x[1] = pb.x1;
-        co.start(nw, x, 1.0, 1e-3, pb.maxfun);
-        stage = S_RUN1;
-        g = true;
-    } else {
-        stage = S_GRID;
-        ph = NW_EVAL;
-        px[0] = 0.1;
-        px[1] = c_phi_grid[0];
-    }
-    for (;;) {
-#if defined(GPD_DIAG)
-        {  // rounds per wave (slot 6, first active lane)
-            if ((int)threadIdx.x == __builtin_amdgcn_readfirstlane((int)threadIdx.x)) nw.prof_[6] += 1;
-        }
-        const unsigned long long tg0 = __builtin_amdgcn_s_memtime();
-#endif
-        if (g) {  // NEWUOB's light code up to its next heavy phase (one inlined copy)
-            co.glue(nw);
-            g = false;
-            ph = co.phase;
-            if (ph == NW_EVAL) {
-                px[0] = co.x[0];
-                px[1] = co.x[1];
-            } else if (ph == NW_DONE) {
-                x[0] = co.x[0];
-                x[1] = co.x[1];
-                if (co.ret >= pb.maxfun) status |= ST_MAXFUN;
-                if (stage == S_RUN1) {  // lklval = lkl(x), then lkl at ϕ ∓ π (:408-410)
-                    stage = S_FLIPA;
-                    ph = NW_EVAL;
-                    px[0] = x[0];
-                    px[1] = x[1];
-                } else {
-                    stage = S_DONE;
-                }
-            }
-        }
-        if (f.fallback) ph = NW_DONE;
-#if defined(GPD_DIAG)
-        {  // glue cycles: lane-level slot 5, wave-level slot 13
-            const unsigned long long dt = __builtin_amdgcn_s_memtime() - tg0;
-            nw.prof_[5] += dt;
-            if ((int)threadIdx.x == __builtin_amdgcn_readfirstlane((int)threadIdx.x)) nw.prof_[13] += dt;
-        }
-#endif
-        const unsigned long long mE = __builtin_amdgcn_ballot_w64(ph == NW_EVAL);
-        const unsigned long long mT = __builtin_amdgcn_ballot_w64(ph == NW_TRSAPP);
-        const unsigned long long mU = __builtin_amdgcn_ballot_w64(ph == NW_UPDATE);
-        const unsigned long long mL = __builtin_amdgcn_ballot_w64(ph == NW_BIGLAG);
-        const unsigned long long mD = __builtin_amdgcn_ballot_w64(ph == NW_BIGDEN);
-        if ((mE | mT | mU | mL | mD) == 0) break;
-        int P = NW_EVAL;
-#if GPD_SCHED_POLICY == 1
-        {  // fixed cyclic order TRSAPP, BIGLAG, BIGDEN, evaluation, UPDATE: the next phase
-           // after the last one run that has a lane waiting (run()'s own order of phases)
-            const unsigned long long mk[5] = {mT, mL, mD, mE, mU};
-            const int ph_of[5] = {NW_TRSAPP, NW_BIGLAG, NW_BIGDEN, NW_EVAL, NW_UPDATE};
-#pragma unroll
-            for (int q = 1; q <= 5; ++q) {
-                const int c = (last + q) % 5;
-                if (mk[c]) {
-                    P = ph_of[c];
-                    last = c;
-                    break;
-                }
-            }
-        }
-#else
-        {  // greedy: the phase most lanes wait at
-            int cmax = __builtin_popcountll(mE);
-            const int cT = __builtin_popcountll(mT), cU = __builtin_popcountll(mU),
-                      cL = __builtin_popcountll(mL), cD = __builtin_popcountll(mD);
-            if (cT > cmax) { P = NW_TRSAPP; cmax = cT; }
-            if (cU > cmax) { P = NW_UPDATE; cmax = cU; }
-            if (cL > cmax) { P = NW_BIGLAG; cmax = cL; }
-            if (cD > cmax) { P = NW_BIGDEN; cmax = cD; }
-        }
-#endif
-        if (ph != P) continue;
-#if defined(GPD_DIAG)
-        const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
-#endif
-        if (P == NW_EVAL) {
-            const double fv = f(px);
-            if (stage == S_RUN1 || stage == S_RUN2) {
-                co.f = fv;  // NW_EVAL's resume label was set when the point was requested
-                g = true;
-            } else if (stage == S_GRID) {  // findmin: first NaN wins, else first minimum
-                if (gk == 0) {
-                    fb = fv;
-                } else if (!(fb != fb) && ((fv != fv) || fb > fv)) {
-                    best = gk;
-                    fb = fv;
-                }
-                if (++gk < 8) {
-                    px[1] = c_phi_grid[gk];
-                } else {
-                    x[0] = 0.1;
-                    x[1] = c_phi_grid[best];
-                    co.start(nw, x, 1.0, 1e-3, pb.maxfun);
-                    stage = S_RUN1;
-                    g = true;
-                }
-            } else if (stage == S_FLIPA) {
-                lkl = fv;
-                php = x[1] + (x[1] < 0 ? PI_F64 : -PI_F64);
-                px[1] = php;
-                stage = S_FLIPB;
-            } else {  // S_FLIPB: "bad minima" (src/Modulation.jl:411-414)
-                if (lkl > fv) {
-                    status |= ST_REFIT;
-                    x[1] = php;
-                    co.start(nw, x, 1.0, 1e-3, pb.maxfun);
-                    stage = S_RUN2;
-                    g = true;
-                } else {
-                    stage = S_DONE;
-                    ph = NW_DONE;
-                }
-            }
-        } else {
-            if (P == NW_TRSAPP) {
-                GPD_SCHED_INL nw.trsapp(co.delta, nw.d, co.crvmin);
-                co.lbl = co.L_TRS_POST;
-            } else if (P == NW_UPDATE) {
-                GPD_SCHED_INL nw.update(co.idz, co.beta, co.knew);
-                co.lbl = co.L_UPD_POST;
-            } else if (P == NW_BIGLAG) {
-                GPD_SCHED_INL nw.biglag(co.idz, co.knew, co.dstep, co.alpha);
-                co.lbl = co.L_VLAG;
-            } else {
-                GPD_SCHED_INL nw.bigden(co.idz, co.kopt, co.knew, co.beta);
-                co.lbl = co.L290;
-            }
-            g = true;
-        }
-#if defined(GPD_DIAG)
-        {  // lane-level cycles per phase in prof_[slot], wave-level in prof_[8 + slot]
-            const int slot = P == NW_TRSAPP ? 0 : P == NW_BIGLAG ? 1 : P == NW_BIGDEN ? 2
-                           : P == NW_UPDATE ? 3 : 7;
-            const unsigned long long dt = __builtin_amdgcn_s_memtime() - tp0;
-            nw.prof_[slot] += dt;
-            if ((int)threadIdx.x == __builtin_amdgcn_readfirstlane((int)threadIdx.x))
-                nw.prof_[8 + slot] += dt;
-        }
-#endif
     }
 }
 
@@ -2458,11 +2273,6 @@ __device__ __forceinline__ void harm_offsets(HarmChi2 &f, const Problem &pb, lon
 #ifndef GPD_FIT_MINB
 #define GPD_FIT_MINB 1
 #endif
-// 1: the phase-scheduled driver (drive_fit_sched, r4; measured slower);
-// 0: drive_fit + run() (default)
-#ifndef GPD_FIT_SCHED
-#define GPD_FIT_SCHED 0
-#endif
 __global__ __launch_bounds__(64, GPD_FIT_MINB) void k_fit_harmonic(Problem pb, const Info *__restrict__ info,
                                                      const double *__restrict__ mom,
                                                      const double *__restrict__ aux,
@@ -2513,11 +2323,7 @@ __global__ __launch_bounds__(64, GPD_FIT_MINB) void k_fit_harmonic(Problem pb, c
 #pragma unroll
     for (int q = 0; q < 16; ++q) nwpool[threadIdx.x].prof_[q] = 0;
 #endif
-#if GPD_FIT_SCHED
-    drive_fit_sched(f, pb, x, status, nwpool[threadIdx.x]);
-#else
     drive_fit(f, pb, x, status, nwpool[threadIdx.x]);
-#endif
     const double chi2 = f(x);  // likelihood[idx] = lkl(x) (src/Modulation.jl:416)
     if (f.prof) {
         atomicAdd(&pb.prof[PROF_FIT + 0], f.prof_cycles);
@@ -2585,8 +2391,7 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 // 8 at two waves per SIMD (C5 exact 339 → 315-320 ms), 4 at one (r2: 2/6/8/16 no better there).
 // WGT: threads per series — EXACT_WG (256: thread t owns slot t of each canonical block), or 64
 // for short spans (k_fit_exact with WGT = 64: lane l owns the block's slots l, l+64, l+128,
-// l+192 and reduces them as block_sum's four waves would — the same sums, one wave per series),
-// or 512 (the split form, opt-in: two lanes of a wave per canonical chain, cr_split_chain).
+// l+192 and reduces them as block_sum's four waves would — the same sums, one wave per series).
 // r4: an evaluation reads the functor's fields once (View), streams the per-series arrays
 // non-temporally (ld_s) and, for ComplexF64 storage and Float64 arithmetic, takes the FAST form
 // whose per-sample loads are unconditional (eval<true>): C5 exact 316 → 254 ms, same bits.
@@ -2609,13 +2414,6 @@ struct ExactChi2 {
     // pass computed (same values, so the same sums) instead of re-evaluating sin/sincos and the
     // FC phasor; element i − s0 of the series' slot
     c64 *mc;
-    // LDS-resident head of the model cache (r4, G = 8: each thread owns exactly one canonical
-    // chain, so chain sample m = (i − s0) / 2048 of thread t sits at lmc[m·WGT + t] for m < lml;
-    // the chain's later samples stay in the global slot mc).  lml = 0: all in mc.
-    __attribute__((address_space(3))) c64 *lmc;
-    int lml;
-    // the split form's (WGT = 512) LDS for the first butterfly step: 256 × NV doubles
-    __attribute__((address_space(3))) double *xbuf;
     // multi-workgroup split: G workgroups per series, this one is g; x: the series' exchange
     int G, g;
     Xchg x;
@@ -2646,8 +2444,6 @@ struct ExactChi2 {
         // the model cache, read once per evaluation (members of an out-of-line functor are
         // read through its pointer, again after every store that may alias it)
         __attribute__((address_space(1))) c64 *mc;
-        __attribute__((address_space(3))) c64 *lmc;
-        int lml;
         long long s0;
         long long doff, foff;   // series column / raw FC column offsets
         const double *m5, *w5;  // faint power and weight per state (the functor's)
@@ -2665,8 +2461,6 @@ struct ExactChi2 {
         v.only_high = (pb->flags & F_ONLY_HIGH) != 0;
         v.xr = (const __attribute__((address_space(1))) float *)(fp32 ? pb->xr32 : nullptr);
         v.mc = (__attribute__((address_space(1))) c64 *)mc;
-        v.lmc = lmc;
-        v.lml = lml;
         v.s0 = s0;
         v.doff = doff;
         v.foff = foff;
@@ -2739,7 +2533,7 @@ struct ExactChi2 {
         double t;
         int st;
     };
-    // FAST (r4): ComplexF64 storage, Float64 arithmetic, no LDS model cache, and the state
+    // FAST (r4): ComplexF64 storage, Float64 arithmetic, and the state
     // array present exactly when FAINT — every load of a sample unconditional, so that the
     // compiler counts the prefetched batch's loads exactly and waits only for the batch in use
     // (with the runtime storage / fp32 / state selects it fell back to waiting for all
@@ -2767,33 +2561,19 @@ struct ExactChi2 {
             return;
         }
         r.st = v.state ? (int)v.state[i] : 0;
-        const long long e = i - v.s0;
-        const int mm = (int)(e >> 11);  // wave-uniform: the chain's sample index
-        if (mm < v.lml) {
-            const __attribute__((address_space(3))) c64 *q = v.lmc + mm * WGT + (int)threadIdx.x;
-            r.f = c64{q->re, q->im};
-        } else {
-            r.f = ld_s(v.mc + e);
-        }
+        r.f = ld_s(v.mc + (i - v.s0));
         r.d = d_of(v, v.doff + i);
     }
-    // the first pass's store of sample i's model into the cache (LDS head or global slot)
+    // the first pass's store of sample i's model into the workgroup's model-cache slot
     template <bool FAST = false>
     __device__ __forceinline__ static void mc_put(const View &v, long long i, const c64 &m) {
         const long long e = i - v.s0;
-        const int mm = (int)(e >> 11);
-        if (!FAST && mm < v.lml) {
-            __attribute__((address_space(3))) c64 *q = v.lmc + mm * WGT + (int)threadIdx.x;
-            q->re = m.re;
-            q->im = m.im;
-        } else {
 #if GPD_EXACT_NT
-            __builtin_nontemporal_store(nv2d{m.re, m.im}, (__attribute__((address_space(1))) nv2d *)(v.mc + e));
+        __builtin_nontemporal_store(nv2d{m.re, m.im}, (__attribute__((address_space(1))) nv2d *)(v.mc + e));
 #else
-            v.mc[e].re = m.re;
-            v.mc[e].im = m.im;
+        v.mc[e].re = m.re;
+        v.mc[e].im = m.im;
 #endif
-        }
     }
     // sample_valid on a loaded state (TRANSIENT dropped, onlyhigh keeps HIGH ∪ NORMAL)
     template <bool FAST = false>
@@ -3014,11 +2794,6 @@ struct ExactChi2 {
     template <int NV, class C>
     __device__ __forceinline__ void cr_sum_blocks(C &&chain, double (&tot)[NV]) {
         ldouble *lp = (ldouble *)lds;
-        if constexpr (WGT == 2 * EXACT_WG) {  // the split form sums through cr_sum2m only (the
-#pragma unroll                                // engine runs it with a model cache)
-            for (int k = 0; k < NV; ++k) tot[k] = __builtin_nan("");
-            return;
-        }
         if (sync_fail) {  // the series' barrier was poisoned: every part stops passing samples
 #pragma unroll
             for (int k = 0; k < NV; ++k) tot[k] = __builtin_nan("");
@@ -3127,10 +2902,6 @@ struct ExactChi2 {
     // in chain order.
     template <int NV, int U = CR_U, class L, class B, class A>
     __device__ __forceinline__ void cr_sum2m(L &&load, B &&batch, A &&accum, double (&tot)[NV]) {
-        if constexpr (WGT == 2 * EXACT_WG) {
-            cr_sum2m_split<NV, U>(load, batch, accum, tot);
-            return;
-        }
         cr_sum_blocks<NV>(
             [&](long long i0, double (&acc)[NV]) {
                 const int M = i0 < s1 ? (int)((s1 - 1 - i0) / CR_SLOTS + 1) : 0;
@@ -3164,128 +2935,16 @@ struct ExactChi2 {
             },
             tot);
     }
-    // The split form (r4, WGT = 512 threads per part, G = 8): wave w (0-7) of the part holds
-    // the block's canonical chains c = 32·w + (lane mod 32), lanes l and l + 32 sharing chain c —
-    // lane l (h = 0) evaluates its samples m = 0, 2, 4, …, lane l + 32 (h = 1) the odd ones.
-    // Each evaluates its sample's terms (accum into zeroed temporaries: a term x becomes 0.0 + x,
-    // which differs from x only for x = −0.0, and a chain sum is never −0.0, so adding either gives
-    // the same bits); the odd term crosses to lane l (lane_xor<32>) and lane l adds both in chain
-    // order.  Both lanes of a pair run the same ⌈M/2⌉ steps.  Then block_sum<256>'s tree over the
-    // block's 256 chains (its butterfly's first step pairs chains c and c ± 32, which sit in waves
-    // 2q and 2q + 1: through LDS) and the parts' exchange as in cr_sum_blocks — the G = 8 sums,
-    // bit for bit, with two waves per SIMD instead of one.
-    template <int NV, int U, class L, class B, class A>
-    __device__ __forceinline__ void cr_split_chain(L &&load, B &&batch, A &&accum,
-                                                   double (&acc)[NV]) {
-        const int lane = (int)threadIdx.x & 63, w = (int)threadIdx.x >> 6, h = lane >> 5;
-        const long long i0 = s0 + (long long)g * EXACT_WG + 32 * w + (lane & 31);
-        const int M = i0 < s1 ? (int)((s1 - 1 - i0) / CR_SLOTS + 1) : 0;
-        const int J = (M + 1) >> 1;  // the pair's steps (the same in both lanes)
-#pragma unroll
-        for (int k = 0; k < NV; ++k) acc[k] = 0.0;
-        if (J == 0) return;
-        Raw A_[U], B_[U];
-        auto issue = [&](Raw (&X)[U], int j0) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                int m = 2 * (j0 + u < J ? j0 + u : J - 1) + h;
-                m = m < M ? m : M - 1;
-                load(i0 + (long long)m * CR_SLOTS, X[u]);
-            }
-        };
-        auto run = [&](const Raw (&X)[U], int j0) {
-            c64 mb[U];
-            batch(X, mb);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (j0 + u >= J) break;
-                double t[NV];
-#pragma unroll
-                for (int k = 0; k < NV; ++k) t[k] = 0.0;
-                const int m = 2 * (j0 + u) + h;
-                if (m < M) accum(i0 + (long long)m * CR_SLOTS, X[u], mb[u], t);
-                double p[NV];
-#pragma unroll
-                for (int k = 0; k < NV; ++k) p[k] = lane_xor<32>(t[k]);  // lane l: the odd term
-                if (h == 0) {
-#pragma unroll
-                    for (int k = 0; k < NV; ++k) acc[k] += t[k];
-#pragma unroll
-                    for (int k = 0; k < NV; ++k) acc[k] += p[k];
-                }
-            }
-        };
-        issue(A_, 0);
-        int j0 = 0;
-        for (; j0 + U < J; j0 += 2 * U) {
-            issue(B_, j0 + U);
-            run(A_, j0);
-            if (j0 + 2 * U < J) issue(A_, j0 + 2 * U);
-            run(B_, j0 + U);
-        }
-        if (j0 < J) run(A_, j0);
-    }
-    template <int NV, int U, class L, class B, class A>
-    __device__ __forceinline__ void cr_sum2m_split(L &&load, B &&batch, A &&accum, double (&tot)[NV]) {
-        ldouble *lp = (ldouble *)lds;
-        if (sync_fail) {
-#pragma unroll
-            for (int k = 0; k < NV; ++k) tot[k] = __builtin_nan("");
-            return;
-        }
-        double acc[NV];
-        cr_split_chain<NV, U>(load, batch, accum, acc);
-        const int lane = (int)threadIdx.x & 63, w = (int)threadIdx.x >> 6;
-        // block_sum<256>'s butterfly: partner 32 (chains c, c ± 32: waves w and w ^ 1) via LDS
-        ldouble *xb = xbuf;
-        if (lane < 32) {
-#pragma unroll
-            for (int k = 0; k < NV; ++k) xb[(w * 32 + lane) * NV + k] = acc[k];
-        }
-        __syncthreads();
-        if (lane < 32) {
-#pragma unroll
-            for (int k = 0; k < NV; ++k) acc[k] = acc[k] + xb[((w ^ 1) * 32 + lane) * NV + k];
-        }
-        // partners 16 … 1 within the 32 chains of each wave (lanes 0-31)
-#pragma unroll
-        for (int k = 0; k < NV; ++k) acc[k] = acc[k] + lane_xor<16>(acc[k]);
-#pragma unroll
-        for (int k = 0; k < NV; ++k) acc[k] = acc[k] + lane_xor<8>(acc[k]);
-#pragma unroll
-        for (int k = 0; k < NV; ++k) acc[k] = acc[k] + lane_xor<4>(acc[k]);
-#pragma unroll
-        for (int k = 0; k < NV; ++k) acc[k] = acc[k] + lane_xor<2>(acc[k]);
-#pragma unroll
-        for (int k = 0; k < NV; ++k) acc[k] = acc[k] + lane_xor<1>(acc[k]);
-        // the LDS stage: canonical wave q's total (lane 0 of wave 2q), left to right
-        if (lane == 0 && (w & 1) == 0) {
-#pragma unroll
-            for (int k = 0; k < NV; ++k) lp[(w >> 1) * NV + k] = acc[k];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < NV; ++k) {
-            double sv = lp[k];
-#pragma unroll
-            for (int q = 1; q < EXACT_WG / 64; ++q) sv = sv + lp[q * NV + k];
-            acc[k] = sv;
-        }
-        __syncthreads();
-        xpublish<NV>(g, acc);
-        xfinish<NV>(tot);
-    }
-
     __device__ double operator()(const double (&xx)[2]) {
         ++nfev;
         const View V = view();
-        const bool fast = V.d32 == nullptr && V.fc32 == nullptr && !fp32 && V.lml == 0 &&
+        const bool fast = V.d32 == nullptr && V.fc32 == nullptr && !fp32 &&
                           (FAINT == (V.state != nullptr)) && !(pb->flags & F_NOFAST);
         return fast ? eval<true>(V, xx[0], xx[1]) : eval<false>(V, xx[0], xx[1]);
     }
     template <bool FAST>
     __device__ __forceinline__ double eval(const View &V, const double b, const double phi) {
-        const bool mcg = mc != nullptr || lml > 0;  // a model cache (global and/or LDS)
+        const bool mcg = mc != nullptr;  // a model cache
         const unsigned long long tp0 = prof ? __builtin_amdgcn_s_memtime() : 0;
         if (OFFS) {
             double v[8];  // a11, a12(2), a22, b1(2), b2(2)
@@ -3416,6 +3075,18 @@ struct ExactChi2 {
                            resid(r.f, r.d, weight_of(V, r.st), a);
                        },
                        s);
+        } else if (FAST) {
+            // no model cache (GPD option exact_mcache = 0, or a batch whose cache would exceed
+            // 8 GB): the residual pass evaluates the first pass's batched model again — the same
+            // values, so the same sums (r5: 82 → 66 B per sample-evaluation, twice the model's
+            // VALU work)
+            cr_sum2m<1>([&](long long i, Raw &r) { load_raw<FAST>(V, i, r); },
+                        [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch(V, X, b, phi, mb); },
+                        [&](long long i, const Raw &r, const c64 &m, double (&a)[1]) {
+                            if (!valid_st<FAST>(V, r.st)) return;
+                            resid(m, r.d, weight_of(V, r.st), a);
+                        },
+                        s);
         } else {
             cr_sum<1>(
                 [&](long long i, double (&a)[1]) {
@@ -3446,9 +3117,6 @@ __device__ __forceinline__ void setup_exact(F &f, const Problem &pb, long long k
     f.src = phbuf ? phbuf + fcol * pb.N : nullptr;
     f.lds = lds;
     f.mc = nullptr;
-    f.lmc = nullptr;
-    f.lml = 0;
-    f.xbuf = nullptr;
     f.s0 = sp.s0;
     f.s1 = sp.s1;
     f.G = G;
@@ -3496,24 +3164,18 @@ __global__ __launch_bounds__(WGT, MINB) void k_fit_exact(Problem pb, const Info 
                                                         c64 *__restrict__ mcache = nullptr,
                                                         long long mstride = 0, int G = 1,
                                                         double *__restrict__ xtot = nullptr,
-                                                        unsigned *__restrict__ xcnt = nullptr,
-                                                        int lml = 0)
-#if GPD_OWNS(GPD_U_EXACT | GPD_U_EXACT64 | GPD_U_EXACT512)
+                                                        unsigned *__restrict__ xcnt = nullptr)
+#if GPD_OWNS(GPD_U_EXACT | GPD_U_EXACT64)
 {
     __shared__ double lds[EXACT_LDS];
-    // G = 8 with lml > 0: the head of every chain's model cache in dynamic LDS (lml·WGT c64)
-    extern __shared__ __attribute__((aligned(16))) double xlds_dyn[];
     // NEWUOA state: one copy per wave in LDS (all lanes of a wave run the same iteration and
     // read/write the same addresses), instead of replicated in every thread's registers
     __shared__ Newuoa<2, 5, true> nwx[WGT / 64];
     const double nvalid = (double)info->nvalid;
-    // WGT = 512: the split form (two threads per canonical chain), always G = 8 parts
-    if ((WGT == EXACT_WG && G > 1) || WGT == 2 * EXACT_WG) {  // one series per G workgroups
-      // persistent over rounds of gridDim.x / G series (r4, large batches: gridDim.x = the
-      // resident workgroups, a multiple of 8·G, so a series' G parts are in one round and move
-      // on together; the series in flight — their samples and model cache slots — stay within
-      // the 256 MB Infinity Cache across the ~70 passes of their fits).  The model cache has a
-      // slot per series of a round (mstride apart); with one round (gridDim.x ≥ G·P) slot = k.
+    if (WGT == EXACT_WG && G > 1) {  // one series per G workgroups
+      // one round of gridDim.x / G series (gridDim.x = G·⌈P/8⌉·8: a series' G parts are resident
+      // together); written as a loop over rounds of per_round series, model-cache slot k mod
+      // per_round
       const long long per_round = gridDim.x / G;
       for (long long bb = blockIdx.x;; bb += gridDim.x) {
         const long long k = xser(bb, G);
@@ -3523,11 +3185,6 @@ __global__ __launch_bounds__(WGT, MINB) void k_fit_exact(Problem pb, const Info 
         setup_exact(f, pb, k, PHBUF ? phbuf : nullptr, lds, nvalid, G, g,
                     Xchg{xtot + k * (2 * CR_BLOCKS * CR_NV), xcnt + k});
         if (mcache) f.mc = mcache + (k % per_round) * mstride;
-        if (WGT == EXACT_WG && G == CR_BLOCKS && lml > 0) {  // one chain per thread
-            f.lmc = (__attribute__((address_space(3))) c64 *)xlds_dyn;
-            f.lml = lml;
-        }
-        if (WGT == 2 * EXACT_WG) f.xbuf = (__attribute__((address_space(3))) double *)xlds_dyn;
         if (FAINT) {
 #pragma unroll
             for (int q = 0; q < 5; ++q) {

@@ -171,54 +171,11 @@ struct Newuoa {
 
     // Powell's search over the trial angles i·2π/50 (TRSAPP's boundary iterations, BIGLAG):
     // f(0) = fbeg, f(i) = val(i) for i = 1..49.  The published loop walks i in order keeping the
-    // first strictly better value (better(a, b); NaN is never better) and the values around it;
-    // with GPD_NW_TREE the 49 values are formed seven at a time and the first best index is found
-    // by a tree (right wins only when strictly better, or when left is NaN) — the same index, so
-    // the same fbest = f(isave), tempa = f(isave − 1) (f(−1) = f(49)) and tempb = f(isave + 1)
-    // (f(50) = fbeg), recomputed from val() with the same operations: the same bits, with a
-    // dependency chain of 7 × 3 selects instead of 49 × 4.
+    // first strictly better value (better(a, b); NaN is never better) and the values around it:
+    // fbest = f(isave), tempa = f(isave − 1) (f(−1) = f(49)), tempb = f(isave + 1) (f(50) = fbeg).
     template <class V, class B>
     GPD_HD static void angle_search(double fbeg, V &&val, B &&better, int &isave, double &fbest,
                                     double &tempa, double &tempb) {
-#if defined(GPD_NW_TREE) && GPD_NW_TREE
-        if (fbeg != fbeg) {  // a NaN start: the published loop never moves
-            isave = 0;
-            fbest = fbeg;
-            tempa = val(49);
-            tempb = val(1);
-            return;
-        }
-        auto pick = [&](double lv, int li, double rv, int ri, double &ov, int &oi) {
-            const bool r = better(rv, lv) || (lv != lv && rv == rv);
-            ov = r ? rv : lv;
-            oi = r ? ri : li;
-        };
-        int bi = 0;
-        double bv = fbeg;
-#pragma unroll
-        for (int c = 0; c < 7; ++c) {
-            double v[7];
-#pragma unroll
-            for (int u = 0; u < 7; ++u) v[u] = val(7 * c + u + 1);
-            const int i0 = 7 * c + 1;
-            double a, b2, cc, e, f2, gv;
-            int ia, ib, ic, ie, jf, ig;
-            pick(v[0], i0, v[1], i0 + 1, a, ia);
-            pick(v[2], i0 + 2, v[3], i0 + 3, b2, ib);
-            pick(v[4], i0 + 4, v[5], i0 + 5, cc, ic);
-            pick(a, ia, b2, ib, e, ie);
-            pick(cc, ic, v[6], i0 + 6, f2, jf);
-            pick(e, ie, f2, jf, gv, ig);
-            if (better(gv, bv)) {
-                bv = gv;
-                bi = ig;
-            }
-        }
-        isave = bi;
-        fbest = bv;
-        tempa = bi == 0 ? val(49) : bi == 1 ? fbeg : val(bi - 1);
-        tempb = bi == 49 ? fbeg : val(bi + 1);
-#else
         double fsav = fbeg, fnew = fbeg;
         fbest = fbeg;
         tempa = 0.0;
@@ -238,7 +195,6 @@ struct Newuoa {
         }
         if (isave == 0) tempa = fnew;
         if (isave == 49) tempb = fbeg;
-#endif
     }
 
     // ---------------------------------------------------- hd = ∇²Q · v (TRSAPP label 170)
@@ -1450,595 +1406,6 @@ struct Newuoa {
             xopt[j] = 0.0;
         }
         xoptsq = 0.0;
-    }
-};
-
-// ---------------------------------------------------------------------------------------
-// NEWUOB as a resumable coroutine (r4, k_fit_harmonic).  In a wave of lane-per-series fits the
-// lanes reach NEWUOB's phases — the objective, TRSAPP, BIGLAG, BIGDEN, UPDATE — at different
-// times; run()'s goto structure left the wave executing each phase about twice per lane's own
-// use (objective 68 executions per wave for 34 per series, profiles/r3/fit_lanes/).  Here the
-// locals of run() live in this register-resident object, the arrays stay in the Newuoa object
-// (LDS), and NEWUOB is cut at its heavy phases: `phase` names the next one, exec() runs it
-// and then the light code after it up to the next heavy phase.  The kernel runs every phase
-// once per round for the lanes waiting at it (gpd_kernels.hpp k_fit_harmonic), so a phase
-// executes about as often as the lane that needs it most, not the union of all orders.  The
-// arithmetic is run()'s, statement for statement (same operations, same order): the same bits
-// (tests/test_abi.py::test_newuoa_coroutine_equals_run_bitwise).
-// glue()'s dispatch (A/B, GPD_GLUE_SEQ): a switch on the label in a loop, or the label blocks
-// tested one after the other in program order (a `break` leaves a block; the loop takes the few
-// backward transitions) — the same transitions either way
-#if defined(GPD_GLUE_SEQ) && GPD_GLUE_SEQ
-#define NW_SW_OPEN {
-#define NW_SW_CLOSE }
-#define NW_CASE(X) if (lbl == X) do {
-#define NW_END } while (0);
-#else
-#define NW_SW_OPEN switch (lbl) {
-#define NW_SW_CLOSE }
-#define NW_CASE(X) case X: {
-#define NW_END }
-#endif
-enum NwPhase { NW_EVAL = 0, NW_TRSAPP = 1, NW_BIGLAG = 2, NW_BIGDEN = 3, NW_UPDATE = 4, NW_DONE = 5 };
-
-template <int N, int NPT, bool DIRECT = false>
-struct NewuoaCo {
-    typedef Newuoa<N, NPT, DIRECT> NW;
-    static constexpr int NPTM = NW::NPTM;
-    static constexpr int NH = NW::NH;
-    enum Lbl { L_INIT_PRE, L_INIT_POST, L90, L100, L_TRS_POST, L120, L_VLAG, L290, L_EVAL_POST,
-               L_UPD_POST, L460, L490, L530 };
-    int phase, lbl;
-    int nf, nftest, kopt, idz, itest, knew, nfsav, ksave, init_nf, nfm, nfmm, ipt, jpt;
-    double rhobeg, rhoend, rhosq, recip, reciq, f, fbeg, fopt, rho, delta, diffa, diffb, diffc;
-    double ratio, crvmin, dnorm, dsq, dstep, alpha, beta, vquad, diff, xoptsq, fsave, xipt, xjpt;
-    double x[N];  // the point to evaluate (phase NW_EVAL); the result once NW_DONE
-    double fx;    // f(x) once NW_DONE
-    int ret;      // evaluations once NW_DONE (run()'s return value)
-
-    GPD_HD void start(NW &nw, const double (&x0)[N], double rb, double re, int maxfun) {
-        rhobeg = rb;
-        rhoend = re;
-        nftest = maxfun > 1 ? maxfun : 1;
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            x[j] = x0[j];
-            nw.xbase[j] = x0[j];
-#pragma unroll
-            for (int k = 0; k < NPT; ++k) nw.xpt[k][j] = 0.0;
-#pragma unroll
-            for (int i = 0; i < NW::NDIM; ++i) nw.bmat[i][j] = 0.0;
-        }
-#pragma unroll
-        for (int ih = 0; ih < NH; ++ih) nw.hq[ih] = 0.0;
-#pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-            nw.pq[k] = 0.0;
-#pragma unroll
-            for (int j = 0; j < NPTM; ++j) nw.zmat[k][j] = 0.0;
-        }
-        rhosq = rhobeg * rhobeg;
-        recip = 1.0 / rhosq;
-        reciq = sqrt(0.5) / rhosq;
-        f = 0.0;
-        fbeg = 0.0;
-        fopt = 0.0;
-        kopt = 1;
-        init_nf = 1;
-        lbl = L_INIT_PRE;  // the caller runs glue(): its one call site in k_fit_harmonic
-    }
-
-    // the heavy phase `phase` (fnew: f(x) when phase == NW_EVAL), then the light code up to
-    // the next heavy phase (host driver and tests; the kernel calls the phases itself)
-    GPD_HDN void exec(NW &nw, double fnew) {
-        switch (phase) {
-        case NW_EVAL:
-            f = fnew;
-            break;  // lbl: L_INIT_POST or L_EVAL_POST, set when the evaluation was requested
-        case NW_TRSAPP:
-            nw.trsapp(delta, nw.d, crvmin);
-            lbl = L_TRS_POST;
-            break;
-        case NW_BIGLAG:
-            nw.biglag(idz, knew, dstep, alpha);
-            lbl = L_VLAG;
-            break;
-        case NW_BIGDEN:
-            nw.bigden(idz, kopt, knew, beta);
-            lbl = L290;
-            break;
-        case NW_UPDATE:
-            nw.update(idz, beta, knew);
-            lbl = L_UPD_POST;
-            break;
-        default:
-            return;
-        }
-        glue(nw);
-    }
-
-    // run()'s code between heavy phases, label by label (inlined: its object lives in registers)
-    GPD_HD void glue(NW &nw) {
-        for (;;) {
-            NW_SW_OPEN
-            NW_CASE(L_INIT_PRE)
-                nf = init_nf;
-                nfm = nf - 1;
-                nfmm = nf - 1 - N;
-                ipt = 0;
-                jpt = 0;
-                xipt = 0.0;
-                xjpt = 0.0;
-                if (nfm <= 2 * N) {
-                    if (nfm >= 1 && nfm <= N) {
-                        NW::wr2_(nw.xpt, nf - 1, nfm - 1, rhobeg);
-                    } else if (nfm > N) {
-#pragma unroll
-                        for (int j = 0; j < N; ++j)
-                            if (j == nfmm - 1) NW::wr2_(nw.xpt, nf - 1, j, -rhobeg);
-                    }
-                } else {
-                    int itemp = (nfmm - 1) / N;
-                    jpt = nfm - itemp * N - N;
-                    ipt = jpt + itemp;
-                    if (ipt > N) {
-                        itemp = jpt;
-                        jpt = ipt - N;
-                        ipt = itemp;
-                    }
-                    xipt = rhobeg;
-                    if (NW::rd_(nw.fval, ipt + N) < NW::rd_(nw.fval, ipt)) xipt = -xipt;
-                    xjpt = rhobeg;
-                    if (NW::rd_(nw.fval, jpt + N) < NW::rd_(nw.fval, jpt)) xjpt = -xjpt;
-#pragma unroll
-                    for (int j = 0; j < N; ++j) {
-                        if (j == ipt - 1) NW::wr2_(nw.xpt, nf - 1, j, xipt);
-                        if (j == jpt - 1) NW::wr2_(nw.xpt, nf - 1, j, xjpt);
-                    }
-                }
-                double xe[N];
-#pragma unroll
-                for (int j = 0; j < N; ++j) xe[j] = NW::rd2_(nw.xpt, nf - 1, j) + nw.xbase[j];
-#pragma unroll
-                for (int j = 0; j < N; ++j) x[j] = xe[j];
-                if (nf > nftest) {  // maxfun < NPT: stop during initialisation
-                    fx = f;
-                    nw.finish(x, fopt, f);
-                    fx = f;
-                    ret = nf - 1;
-                    phase = NW_DONE;
-                    return;
-                }
-                lbl = L_INIT_POST;
-                phase = NW_EVAL;
-                return;
-            NW_END
-            NW_CASE(L_INIT_POST)
-                NW::wr_(nw.fval, nf - 1, f);
-                if (nf == 1) {
-                    fbeg = f;
-                    fopt = f;
-                    kopt = 1;
-                } else if (f < fopt) {
-                    fopt = f;
-                    kopt = nf;
-                }
-                if (nfm <= 2 * N) {
-                    if (nfm >= 1 && nfm <= N) {
-                        NW::wr_(nw.gq, nfm - 1, (f - fbeg) / rhobeg);
-                        if (NPT < nf + N) {
-#pragma unroll
-                            for (int j = 0; j < N; ++j)
-                                if (j == nfm - 1) {
-                                    nw.bmat[0][j] = -1.0 / rhobeg;
-                                    NW::wr2_(nw.bmat, nf - 1, j, 1.0 / rhobeg);
-                                    NW::wr2_(nw.bmat, NPT + nfm - 1, j, -0.5 * rhosq);
-                                }
-                        }
-                    } else if (nfm > N) {
-#pragma unroll
-                        for (int j = 0; j < N; ++j) {
-                            if (j == nfmm - 1) {
-                                NW::wr2_(nw.bmat, nf - N - 1, j, 0.5 / rhobeg);
-                                NW::wr2_(nw.bmat, nf - 1, j, -0.5 / rhobeg);
-                            }
-                        }
-#pragma unroll
-                        for (int j = 0; j < NPTM; ++j) {
-                            if (j == nfmm - 1) {
-                                nw.zmat[0][j] = -reciq - reciq;
-                                NW::wr2_(nw.zmat, nf - N - 1, j, reciq);
-                                NW::wr2_(nw.zmat, nf - 1, j, reciq);
-                            }
-                        }
-                        const int ih = (nfmm * (nfmm + 1)) / 2;
-                        const double temp = (fbeg - f) / rhobeg;
-                        const double g = NW::rd_(nw.gq, nfmm - 1);
-                        NW::wr_(nw.hq, ih - 1, (g - temp) / rhobeg);
-                        NW::wr_(nw.gq, nfmm - 1, 0.5 * (g + temp));
-                    }
-                } else {
-                    const int ih = (ipt * (ipt - 1)) / 2 + jpt;
-                    if (xipt < 0.0) ipt = ipt + N;
-                    if (xjpt < 0.0) jpt = jpt + N;
-#pragma unroll
-                    for (int j = 0; j < NPTM; ++j) {
-                        if (j == nfmm - 1) {
-                            nw.zmat[0][j] = recip;
-                            NW::wr2_(nw.zmat, nf - 1, j, recip);
-                            NW::wr2_(nw.zmat, ipt, j, -recip);
-                            NW::wr2_(nw.zmat, jpt, j, -recip);
-                        }
-                    }
-                    NW::wr_(nw.hq, ih - 1,
-                            (fbeg - NW::rd_(nw.fval, ipt) - NW::rd_(nw.fval, jpt) + f) / (xipt * xjpt));
-                }
-                if (init_nf < NPT) {
-                    ++init_nf;
-                    lbl = L_INIT_PRE;
-                    break;
-                }
-                nf = NPT;
-                rho = rhobeg;
-                delta = rho;
-                idz = 1;
-                diffa = diffb = diffc = ratio = crvmin = 0.0;
-                dnorm = dsq = dstep = alpha = beta = vquad = 0.0;
-                diff = 0.0;
-                itest = 0;
-                knew = 0;
-                xoptsq = 0.0;
-#pragma unroll
-                for (int i = 0; i < N; ++i) {
-                    nw.xopt[i] = NW::rd2_(nw.xpt, kopt - 1, i);
-                    xoptsq = xoptsq + nw.xopt[i] * nw.xopt[i];
-                }
-                lbl = L90;
-                break;
-            NW_END
-            NW_CASE(L90)
-                nfsav = nf;
-                lbl = L100;
-                break;
-            NW_END
-            NW_CASE(L100)
-                knew = 0;
-                lbl = L_TRS_POST;
-                phase = NW_TRSAPP;
-                return;
-            NW_END
-            NW_CASE(L_TRS_POST)
-                dsq = 0.0;
-#pragma unroll
-                for (int i = 0; i < N; ++i) dsq = dsq + nw.d[i] * nw.d[i];
-                dnorm = fmin(delta, sqrt(dsq));
-                if (dnorm < 0.5 * rho) {
-                    knew = -1;
-                    delta = 0.1 * delta;
-                    ratio = -1.0;
-                    if (delta <= 1.5 * rho) delta = rho;
-                    if (nf <= nfsav + 2) {
-                        lbl = L460;
-                        break;
-                    }
-                    const double temp = 0.125 * crvmin * rho * rho;
-                    if (temp <= fmax(fmax(diffa, diffb), diffc)) {
-                        lbl = L460;
-                        break;
-                    }
-                    lbl = L490;
-                    break;
-                }
-                lbl = L120;
-                break;
-            NW_END
-            NW_CASE(L120)
-                if (dsq <= 1.0e-3 * xoptsq) nw.shift_base(xoptsq, idz);
-                if (knew > 0) {
-                    lbl = L_VLAG;
-                    phase = NW_BIGLAG;
-                    return;
-                }
-                lbl = L_VLAG;
-                break;
-            NW_END
-            NW_CASE(L_VLAG)
-#pragma unroll
-                for (int k = 0; k < NPT; ++k) {
-                    double suma = 0.0, sumb = 0.0, sum = 0.0;
-#pragma unroll
-                    for (int j = 0; j < N; ++j) {
-                        suma = suma + nw.xpt[k][j] * nw.d[j];
-                        sumb = sumb + nw.xpt[k][j] * nw.xopt[j];
-                        sum = sum + nw.bmat[k][j] * nw.d[j];
-                    }
-                    nw.w[k] = suma * (0.5 * suma + sumb);
-                    nw.vlag[k] = sum;
-                }
-                beta = 0.0;
-#pragma unroll
-                for (int k = 0; k < NPTM; ++k) {
-                    double sum = 0.0;
-#pragma unroll
-                    for (int i = 0; i < NPT; ++i) sum = sum + nw.zmat[i][k] * nw.w[i];
-                    if (k + 1 < idz) {
-                        beta = beta + sum * sum;
-                        sum = -sum;
-                    } else {
-                        beta = beta - sum * sum;
-                    }
-#pragma unroll
-                    for (int i = 0; i < NPT; ++i) nw.vlag[i] = nw.vlag[i] + sum * nw.zmat[i][k];
-                }
-                double bsum = 0.0, dx = 0.0;
-#pragma unroll
-                for (int j = 0; j < N; ++j) {
-                    double sum = 0.0;
-#pragma unroll
-                    for (int i = 0; i < NPT; ++i) sum = sum + nw.w[i] * nw.bmat[i][j];
-                    bsum = bsum + sum * nw.d[j];
-                    const int jp = NPT + j;
-#pragma unroll
-                    for (int k = 0; k < N; ++k) sum = sum + nw.bmat[jp][k] * nw.d[k];
-                    nw.vlag[jp] = sum;
-                    bsum = bsum + sum * nw.d[j];
-                    dx = dx + nw.d[j] * nw.xopt[j];
-                }
-                beta = dx * dx + dsq * (xoptsq + dx + dx + 0.5 * dsq) + beta - bsum;
-                NW::wr_(nw.vlag, kopt - 1, NW::rd_(nw.vlag, kopt - 1) + 1.0);
-                if (knew > 0) {
-                    const double vk = NW::rd_(nw.vlag, knew - 1);
-                    const double temp = 1.0 + alpha * beta / (vk * vk);
-                    if (fabs(temp) <= 0.8) {
-                        lbl = L290;
-                        phase = NW_BIGDEN;
-                        return;
-                    }
-                }
-                lbl = L290;
-                break;
-            NW_END
-            NW_CASE(L290)
-#pragma unroll
-                for (int i = 0; i < N; ++i) {
-                    nw.xnew[i] = nw.xopt[i] + nw.d[i];
-                    x[i] = nw.xbase[i] + nw.xnew[i];
-                }
-                nf = nf + 1;
-                if (nf > nftest) {
-                    nf = nf - 1;
-                    lbl = L530;
-                    break;
-                }
-                lbl = L_EVAL_POST;
-                phase = NW_EVAL;
-                return;
-            NW_END
-            NW_CASE(L_EVAL_POST)
-                if (knew == -1) {
-                    lbl = L530;
-                    break;
-                }
-                vquad = 0.0;
-                {
-                    int ih = 0;
-#pragma unroll
-                    for (int j = 0; j < N; ++j) {
-                        vquad = vquad + nw.d[j] * nw.gq[j];
-#pragma unroll
-                        for (int i = 0; i <= j; ++i) {
-                            double temp = nw.d[i] * nw.xnew[j] + nw.d[j] * nw.xopt[i];
-                            if (i == j) temp = 0.5 * temp;
-                            vquad = vquad + temp * nw.hq[ih];
-                            ++ih;
-                        }
-                    }
-#pragma unroll
-                    for (int k = 0; k < NPT; ++k) vquad = vquad + nw.pq[k] * nw.w[k];
-                }
-                diff = f - fopt - vquad;
-                diffc = diffb;
-                diffb = diffa;
-                diffa = fabs(diff);
-                if (dnorm > rho) nfsav = nf;
-                fsave = fopt;
-                if (f < fopt) {
-                    fopt = f;
-                    xoptsq = 0.0;
-#pragma unroll
-                    for (int i = 0; i < N; ++i) {
-                        nw.xopt[i] = nw.xnew[i];
-                        xoptsq = xoptsq + nw.xopt[i] * nw.xopt[i];
-                    }
-                }
-                ksave = knew;
-                if (knew <= 0) {
-                    if (vquad >= 0.0) {  // trust-region step failed to reduce Q
-                        lbl = L530;
-                        break;
-                    }
-                    ratio = (f - fsave) / vquad;
-                    if (ratio <= 0.1) {
-                        delta = 0.5 * dnorm;
-                    } else if (ratio <= 0.7) {
-                        delta = fmax(0.5 * delta, dnorm);
-                    } else {
-                        delta = fmax(0.5 * delta, dnorm + dnorm);
-                    }
-                    if (delta <= 1.5 * rho) delta = rho;
-                    double rs = fmax(0.1 * delta, rho);
-                    rs = rs * rs;
-                    int ktemp = 0;
-                    double detrat = 0.0;
-                    if (f >= fsave) {
-                        ktemp = kopt;
-                        detrat = 1.0;
-                    }
-#pragma unroll
-                    for (int k = 0; k < NPT; ++k) {
-                        double hdiag = 0.0;
-#pragma unroll
-                        for (int j = 0; j < NPTM; ++j) {
-                            double temp = 1.0;
-                            if (j + 1 < idz) temp = -1.0;
-                            hdiag = hdiag + temp * nw.zmat[k][j] * nw.zmat[k][j];
-                        }
-                        double temp = fabs(beta * hdiag + nw.vlag[k] * nw.vlag[k]);
-                        double distsq = 0.0;
-#pragma unroll
-                        for (int j = 0; j < N; ++j)
-                            distsq = distsq + (nw.xpt[k][j] - nw.xopt[j]) * (nw.xpt[k][j] - nw.xopt[j]);
-                        if (distsq > rs) {
-                            const double r = distsq / rs;
-                            temp = temp * (r * r * r);
-                        }
-                        if (temp > detrat && k + 1 != ktemp) {
-                            detrat = temp;
-                            knew = k + 1;
-                        }
-                    }
-                    if (knew == 0) {
-                        lbl = L460;
-                        break;
-                    }
-                }
-                lbl = L_UPD_POST;
-                phase = NW_UPDATE;
-                return;
-            NW_END
-            NW_CASE(L_UPD_POST)
-                NW::wr_(nw.fval, knew - 1, f);
-                const double pqk = NW::rd_(nw.pq, knew - 1);
-                int ih = 0;
-#pragma unroll
-                for (int i = 0; i < N; ++i) {
-                    const double temp = pqk * NW::rd2_(nw.xpt, knew - 1, i);
-#pragma unroll
-                    for (int j = 0; j <= i; ++j) {
-                        nw.hq[ih] = nw.hq[ih] + temp * NW::rd2_(nw.xpt, knew - 1, j);
-                        ++ih;
-                    }
-                }
-                NW::wr_(nw.pq, knew - 1, 0.0);
-#pragma unroll
-                for (int j = 0; j < NPTM; ++j) {
-                    double temp = diff * NW::rd2_(nw.zmat, knew - 1, j);
-                    if (j + 1 < idz) temp = -temp;
-#pragma unroll
-                    for (int k = 0; k < NPT; ++k) nw.pq[k] = nw.pq[k] + temp * nw.zmat[k][j];
-                }
-                double gqsq = 0.0;
-#pragma unroll
-                for (int i = 0; i < N; ++i) {
-                    nw.gq[i] = nw.gq[i] + diff * NW::rd2_(nw.bmat, knew - 1, i);
-                    gqsq = gqsq + nw.gq[i] * nw.gq[i];
-                    NW::wr2_(nw.xpt, knew - 1, i, nw.xnew[i]);
-                }
-                if (ksave == 0 && delta == rho) {
-                    if (fabs(ratio) > 1.0e-2) {
-                        itest = 0;
-                    } else {
-                        const double fk = NW::rd_(nw.fval, kopt - 1);
-#pragma unroll
-                        for (int k = 0; k < NPT; ++k) nw.vlag[k] = nw.fval[k] - fk;
-                        double gisq = 0.0;
-#pragma unroll
-                        for (int i = 0; i < N; ++i) {
-                            double sum = 0.0;
-#pragma unroll
-                            for (int k = 0; k < NPT; ++k) sum = sum + nw.bmat[k][i] * nw.vlag[k];
-                            gisq = gisq + sum * sum;
-                            nw.w[i] = sum;
-                        }
-                        itest = itest + 1;
-                        if (gqsq < 1.0e2 * gisq) itest = 0;
-                        if (itest >= 3) {
-#pragma unroll
-                            for (int i = 0; i < N; ++i) nw.gq[i] = nw.w[i];
-#pragma unroll
-                            for (int ih2 = 0; ih2 < NH; ++ih2) nw.hq[ih2] = 0.0;
-                            double wz[NPTM];
-#pragma unroll
-                            for (int j = 0; j < NPTM; ++j) {
-                                wz[j] = 0.0;
-#pragma unroll
-                                for (int k = 0; k < NPT; ++k) wz[j] = wz[j] + nw.vlag[k] * nw.zmat[k][j];
-                                if (j + 1 < idz) wz[j] = -wz[j];
-                            }
-#pragma unroll
-                            for (int j = 0; j < NPTM; ++j) nw.w[j] = wz[j];
-#pragma unroll
-                            for (int k = 0; k < NPT; ++k) {
-                                nw.pq[k] = 0.0;
-#pragma unroll
-                                for (int j = 0; j < NPTM; ++j) nw.pq[k] = nw.pq[k] + nw.zmat[k][j] * nw.w[j];
-                            }
-                            itest = 0;
-                        }
-                    }
-                }
-                if (f < fsave) kopt = knew;
-                if (f <= fsave + 0.1 * vquad || ksave > 0) {
-                    lbl = L100;
-                    break;
-                }
-                knew = 0;
-                lbl = L460;
-                break;
-            NW_END
-            NW_CASE(L460)
-                double distsq = 4.0 * delta * delta;
-#pragma unroll
-                for (int k = 0; k < NPT; ++k) {
-                    double sum = 0.0;
-#pragma unroll
-                    for (int j = 0; j < N; ++j)
-                        sum = sum + (nw.xpt[k][j] - nw.xopt[j]) * (nw.xpt[k][j] - nw.xopt[j]);
-                    if (sum > distsq) {
-                        knew = k + 1;
-                        distsq = sum;
-                    }
-                }
-                if (knew > 0) {
-                    dstep = fmax(fmin(0.1 * sqrt(distsq), 0.5 * delta), rho);
-                    dsq = dstep * dstep;
-                    lbl = L120;
-                    break;
-                }
-                if (ratio > 0.0 || fmax(delta, dnorm) > rho) {
-                    lbl = L100;
-                    break;
-                }
-                lbl = L490;
-                break;
-            NW_END
-            NW_CASE(L490)
-                if (rho > rhoend) {
-                    delta = 0.5 * rho;
-                    ratio = rho / rhoend;
-                    if (ratio <= 16.0) {
-                        rho = rhoend;
-                    } else if (ratio <= 250.0) {
-                        rho = sqrt(ratio) * rhoend;
-                    } else {
-                        rho = 0.1 * rho;
-                    }
-                    delta = fmax(delta, rho);
-                    lbl = L90;
-                    break;
-                }
-                lbl = knew == -1 ? L290 : L530;
-                break;
-            NW_END
-            NW_CASE(L530)  // default
-                nw.finish(x, fopt, f);
-                fx = f;
-                ret = nf;
-                phase = NW_DONE;
-                return;
-            NW_END
-            NW_SW_CLOSE
-        }
     }
 };
 

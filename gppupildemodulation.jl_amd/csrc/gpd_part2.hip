@@ -10,7 +10,7 @@ namespace gpd {
 #if GPD_PART == 2
 __attribute__((used)) void *const k_moments_ws_c64_units[] = {
     (void *)&k_moments_ws<0, false, c64, 2>,              // production (mixed precision)
-    (void *)&k_moments_ws<0, false, c64, 2, false>,       // all-f64 (GPD_MIX=0)
+    (void *)&k_moments_ws<0, false, c64, 2, false>,       // all-f64 (option mix = 0)
     (void *)&k_moments_ws<0, false, c64, 2, true, true>,  // faint series
     (void *)&k_moments_ws<0, false, c64, 2, false, true>,
     (void *)&k_moments_ws<0, true>,                       // UNIT mode (harmonic fitoffsets)

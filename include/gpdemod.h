@@ -99,6 +99,20 @@ int gpd_device_count(void);           /* visible HIP devices (0 if none)        
  * counterpart (Julia frees through its GC); call it after a one-off very large batch. */
 int gpd_release(int device);
 
+/* Test and diagnostics controls (no reference counterpart: demodulateall has no such knobs,
+ * src/Modulation.jl:344-351).  The library reads no environment variable; these process-wide
+ * options default to the production path and are set only by tests and A/B tools, through this
+ * call.  Names and defaults (INTEGRATION.md lists them): mix 1, faint_stats 0, faint_side 0,
+ * fake_gpus 0, exact_g 0, exact_waves 0, exact_wgt 0, exact_fast 1, exact_mcache 1,
+ * xspin_test 0, units 0, upw 0, fit_lanes 0, cohorts 1, harm_min_span 256, fs_cohort_mb 4096,
+ * moments 0, fit_prof 0, sync_debug 0 (0 = automatic where a count is meant).
+ * gpd_set_option / gpd_get_option: GPD_OK, or GPD_E_ARG for an unknown name.
+ * gpd_option_name(i): the i-th option's name, NULL past the last. */
+int gpd_set_option(const char *name, int64_t value);
+int gpd_get_option(const char *name, int64_t *value);
+void gpd_reset_options(void);
+const char *gpd_option_name(int index);
+
 /*
  * Fit (and optionally demodulate) a batch of series.  Replaces the diode loop of
  * demodulateall (src/Modulation.jl:387-433): per series, the FC phasor
@@ -267,7 +281,7 @@ int gpd_buildstates_dev(int64_t n_samples, const double *t, int64_t n1, const do
  * valid samples (TRANSIENT dropped; GPD_ONLY_HIGH in flags keeps HIGH ∪ NORMAL),
  *   m = mean(abs, d[state .== s]),   w = 1 / var(abs.(d[state .== s]); mean = m)
  * — computed by the kernels of the exact evaluator (method EXACT, and the harmonic path with
- * GPD_FAINT_STATS=1|2), bit for bit the oracle's two-pass restatement.  The default
+ * option faint_stats = 1|2), bit for bit the oracle's two-pass restatement.  The default
  * whole-exposure harmonic path forms these statistics inside its moment pass (one pass,
  * shifted sums per state: m within 1e-14, w within 1e-13 relative of these values) and its
  * exact re-fit of FALLBACK series uses those, so faint GPD_ST_FALLBACK records are within that

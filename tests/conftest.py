@@ -50,3 +50,13 @@ def wrap_diff(a, b):
     """|a-b| modulo 2π (ϕ compared modulo 2π after sign normalisation)."""
     d = (np.asarray(a) - np.asarray(b) + np.pi) % (2 * np.pi) - np.pi
     return np.abs(d)
+
+
+@pytest.fixture
+def opts(gpd):
+    """opts(name, value): set one of the library's test/diagnostics options (gpd_set_option; the
+    library reads no environment variable) for this test; every option is reset afterwards."""
+    def set_(name, value):
+        gpd.set_option(name, int(value))
+    yield set_
+    gpd.reset_options()

@@ -43,6 +43,34 @@ def _no_gpu(gpd):
     return gpd.load().gpd_device_count() == 0
 
 
+def test_options_api_and_no_environment(gpd):
+    """The library's test/diagnostics controls go through gpd_set_option only: every option has a
+    production default, unknown names are rejected, reset restores the defaults — and the
+    library imports no getenv at all, so an inherited environment cannot change its path (r5)."""
+    defaults = {"mix": 1, "faint_stats": 0, "faint_side": 0, "fake_gpus": 0, "exact_g": 0,
+                "exact_waves": 0, "exact_wgt": 0, "exact_fast": 1, "exact_mcache": 1,
+                "xspin_test": 0, "units": 0, "upw": 0, "fit_lanes": 0, "cohorts": 1,
+                "harm_min_span": 256, "fs_cohort_mb": 4096, "moments": 0, "fit_prof": 0,
+                "sync_debug": 0}
+    gpd.reset_options()
+    assert gpd.option_names() == list(defaults)
+    assert {k: gpd.get_option(k) for k in defaults} == defaults
+    with gpd.options(mix=0, fit_lanes=7):
+        assert gpd.get_option("mix") == 0 and gpd.get_option("fit_lanes") == 7
+    assert gpd.get_option("mix") == 1 and gpd.get_option("fit_lanes") == 0
+    gpd.set_option("cohorts", 3)
+    gpd.reset_options()
+    assert gpd.get_option("cohorts") == 1
+    with pytest.raises(gpd.GpdError):
+        gpd.set_option("no_such_option", 1)
+    with pytest.raises(gpd.GpdError):
+        gpd.get_option("GPD_MIX")
+    import re
+    data = open(gpd._lib.LIB_PATH, "rb").read()
+    assert not re.search(rb"\bgetenv\b", data), "libgpdemod.so references getenv"
+    assert b"GPD_MIX" not in data and b"GPD_FAINT_STATS" not in data
+
+
 def test_invalid_arguments_rejected_before_device(gpd):
     B = synth.make_batch(100, 4, seed=1)
     with pytest.raises(gpd.GpdError) as e:
@@ -132,12 +160,10 @@ extern "C" int devnw(double* x, double rb, double re, int maxfun, cb_t cb, doubl
 ''' % CSRC
 
 
-@pytest.mark.parametrize("nw_tree", [0, 1])
-def test_device_newuoa_equals_oracle_newuoa_bitwise(tmp_path, oracle, nw_tree):
+def test_device_newuoa_equals_oracle_newuoa_bitwise(tmp_path, oracle):
     """The device NEWUOA (gpd_newuoa.hpp, an independent structured implementation) compiled for
-    the host follows the oracle's Fortran-structured NEWUOA bit for bit — with the trial-angle
-    searches sequential or as a tree (GPD_NW_TREE)."""
-    L = _host_build(tmp_path, "#define GPD_NW_TREE %d\n" % nw_tree + DEVNW, f"devnw{nw_tree}")
+    the host follows the oracle's Fortran-structured NEWUOA bit for bit."""
+    L = _host_build(tmp_path, DEVNW, "devnw")
     OBJ = oracle.lib()._OBJ
     L.devnw.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_double, ctypes.c_int, OBJ,
                         ctypes.c_void_p]
@@ -160,125 +186,6 @@ def test_device_newuoa_equals_oracle_newuoa_bitwise(tmp_path, oracle, nw_tree):
         assert nd == no
         np.testing.assert_array_equal(xd, xo)
         assert fx[0] == fo
-
-
-DEVCO = r'''
-#define __host__
-#define __device__
-#define __forceinline__ inline
-#include <cmath>
-#include "%s/gpd_newuoa.hpp"
-typedef double (*cb_t)(void*, int, const double*);
-template <bool D>
-static int co_run(double* x, double rb, double re, int maxfun, cb_t cb, double* fx) {
-  gpd::Newuoa<2,5,D> nw; gpd::NewuoaCo<2,5,D> co; double x0[2]={x[0],x[1]};
-  co.start(nw, x0, rb, re, maxfun);
-  co.glue(nw);
-  while (co.phase != gpd::NW_DONE) {
-    double fv = 0.0;
-    if (co.phase == gpd::NW_EVAL) { double xx[2] = {co.x[0], co.x[1]}; fv = cb(nullptr, 2, xx); }
-    co.exec(nw, fv);
-  }
-  x[0]=co.x[0]; x[1]=co.x[1]; *fx = co.fx; return co.ret;
-}
-extern "C" int devco(double* x, double rb, double re, int maxfun, cb_t cb, double* fx, int direct) {
-  return direct ? co_run<true>(x, rb, re, maxfun, cb, fx) : co_run<false>(x, rb, re, maxfun, cb, fx); }
-''' % CSRC
-
-
-@pytest.mark.parametrize("glue_seq,nw_tree", [(0, 0), (1, 0), (0, 1)])
-def test_newuoa_coroutine_equals_run_bitwise(tmp_path, oracle, glue_seq, nw_tree):
-    """The resumable NEWUOB (NewuoaCo, the form k_fit_harmonic schedules phase by phase) gives
-    run()'s and the oracle's iterates bit for bit: the same points evaluated in the same order,
-    the same result, evaluation count and f — for χ² landscapes of the harmonic path, standard
-    test functions, maxfun below NPT and a few evaluations, both state layouts."""
-    L = _host_build(tmp_path, "#define GPD_GLUE_SEQ %d\n#define GPD_NW_TREE %d\n" % (glue_seq, nw_tree)
-                    + DEVCO, f"devco{glue_seq}{nw_tree}")
-    OBJ = oracle.lib()._OBJ
-    L.devco.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_double, ctypes.c_int, OBJ,
-                        ctypes.c_void_p, ctypes.c_int]
-    B = synth.make_batch(2000, 24, seed=12)
-    grid = oracle.phi_grid()
-    funcs = [lambda x: (1 - x[0]) ** 2 + 100 * (x[1] - x[0] ** 2) ** 2,
-             lambda x: np.sin(3 * x[0]) * np.cos(2 * x[1]) + 0.1 * (x[0] ** 2 + x[1] ** 2),
-             lambda x: (x[0] - 0.3) ** 2 + 4.0 * (x[1] + 0.2) ** 2]
-    starts = [np.array([-1.2, 1.0]), np.array([0.1, 0.5]), np.array([2.0, -1.0])]
-    for k in range(24):
-        p = np.exp(1j * np.angle(B["fc"][B["fc_of_pixel"][k]]))
-        f = (lambda d: lambda x: oracle.chi2(B["t"], d, p, x[0], x[1])[0])(B["d"][k])
-        funcs.append(f)
-        starts.append(np.array([0.1, grid[int(np.argmin([f([0.1, g]) for g in grid]))]]))
-    for i, (f, x0) in enumerate(zip(funcs, starts)):
-        for maxfun in ((60, 3, 7) if i < 3 else (60,)):
-            seen = {}
-            for direct in (0, 1):
-                pts = []
-
-                def wrapped(ctx, n, xp):
-                    x = np.ctypeslib.as_array(xp, shape=(n,)).copy()
-                    pts.append(x)
-                    return float(f(x))
-                cb = OBJ(wrapped)
-                xd = x0.copy()
-                fx = np.zeros(1)
-                nd = L.devco(xd.ctypes.data, 1.0, 1e-3, maxfun, cb, fx.ctypes.data, direct)
-                seen[direct] = (nd, xd, fx[0], np.array(pts))
-            xo, fo, no = oracle.newuoa(f, x0, 1.0, 1e-3, maxfun=maxfun)
-            for direct, (nd, xd, fd, pts) in seen.items():
-                assert nd == no, (i, maxfun, direct)
-                np.testing.assert_array_equal(xd, xo)
-                assert fd == fo or (np.isnan(fd) and np.isnan(fo))
-            np.testing.assert_array_equal(seen[0][3], seen[1][3])
-
-
-ANGSEARCH = r'''
-#define __host__
-#define __device__
-#define __forceinline__ inline
-#include <cmath>
-#include "%s/gpd_newuoa.hpp"
-extern "C" void search(const double* f, int mode, int* isave, double* out) {
-  double fb, ta, tb;
-  auto val = [&](int i) { return f[i]; };
-  if (mode == 0)
-    gpd::Newuoa<2,5>::angle_search(f[0], val, [](double a, double b) { return a < b; }, *isave, fb, ta, tb);
-  else
-    gpd::Newuoa<2,5>::angle_search(f[0], val, [](double a, double b) { return std::fabs(a) > std::fabs(b); }, *isave, fb, ta, tb);
-  out[0] = fb; out[1] = ta; out[2] = tb;
-}
-''' % CSRC
-
-
-def test_angle_search_tree_equals_sequential(tmp_path):
-    """NEWUOA's trial-angle search (TRSAPP: first minimum; BIGLAG: first maximum of |f|) as the
-    published sequential loop and as the tree of GPD_NW_TREE: the same index and values on random
-    values, ties (first index wins), ±0, ±inf and NaNs anywhere, the start value included."""
-    libs = [_host_build(tmp_path, "#define GPD_NW_TREE %d\n" % t + ANGSEARCH, f"as{t}") for t in (0, 1)]
-    for L in libs:
-        L.search.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
-    rng = np.random.default_rng(5)
-    specials = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1.0, -1.0])
-    for trial in range(20000):
-        kind = trial % 4
-        if kind == 0:
-            f = rng.normal(size=50)
-        elif kind == 1:  # few distinct values: ties everywhere
-            f = rng.integers(-3, 4, size=50).astype(np.float64)
-        elif kind == 2:  # specials sprinkled
-            f = rng.normal(size=50)
-            idx = rng.integers(0, 50, size=rng.integers(1, 8))
-            f[idx] = rng.choice(specials, size=idx.size)
-        else:
-            f = rng.choice(specials, size=50)
-        f = np.ascontiguousarray(f)
-        for mode in (0, 1):
-            res = []
-            for L in libs:
-                isave = ctypes.c_int(-1)
-                out = np.zeros(3)
-                L.search(f.ctypes.data, mode, ctypes.byref(isave), out.ctypes.data)
-                res.append((isave.value, out.tobytes()))
-            assert res[0] == res[1], (trial, mode, f)
 
 
 BESSEL = r'''

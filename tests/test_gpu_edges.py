@@ -56,12 +56,12 @@ def test_nan_sample_propagates(gpu, oracle):
 
 
 @pytest.mark.parametrize("kernel", [None, "valu"])
-def test_nan_fc_sample_propagates(gpu, oracle, monkeypatch, kernel):
+def test_nan_fc_sample_propagates(gpu, oracle, opts, kernel):
     """A NaN in a fibre-coupler column: exp(im·angle(NaN)) is NaN (src/Modulation.jl:388), so
     every diode sharing that column ends with a NaN χ² and status NAN — for both evaluators and
     both harmonic moment kernels; the exact evaluator gives the oracle's records bit for bit."""
     if kernel:
-        monkeypatch.setenv("GPD_MOMENTS", kernel)
+        opts("moments", {"valu": 1}[kernel])
     B = synth.make_batch(2000, 12, seed=15)
     g = 1
     B["fc"][g, 700] = complex(np.nan, 0.0)
@@ -109,10 +109,10 @@ def test_two_samples(gpu, oracle):
 
 @pytest.mark.parametrize("kernel", ["valu", "ws_f64"])
 @pytest.mark.parametrize("faint", [False, True])
-def test_alternative_moment_kernels(gpu, oracle, monkeypatch, kernel, faint):
+def test_alternative_moment_kernels(gpu, oracle, opts, kernel, faint):
     """The VALU kernel (used when a series row or the cos/sin table exceeds the producer/consumer
     kernel's 32-bit buffer offsets) gives the same fits, and so does the producer/consumer kernel
-    with every harmonic on the f64 MFMAs (GPD_MIX=0)."""
+    with every harmonic on the f64 MFMAs (option mix = 0)."""
     from test_gpu_parity import faint_states
     N, P = 3000, 40
     B = synth.make_batch(N, P, seed=77)
@@ -122,9 +122,9 @@ def test_alternative_moment_kernels(gpu, oracle, monkeypatch, kernel, faint):
         st = faint_states(N, seed=5)
         B["d"] = B["d"] * np.where(st == 3, 1.1, np.where(st == 1, 0.3, 0.6))[None, :]
     if kernel == "ws_f64":
-        monkeypatch.setenv("GPD_MIX", "0")
+        opts("mix", 0)
     else:
-        monkeypatch.setenv("GPD_MOMENTS", kernel)
+        opts("moments", {"valu": 1}[kernel])
     got = gpu.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], state=st, method="harmonic")
     ref = oracle.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], state=st, flags=flags)
     pert = [oracle.fit_batch(B["t"], B["d"], B["fc"], B["fc_of_pixel"], state=st, flags=flags,

@@ -2,7 +2,7 @@
 as demodulateall applies it (valid mask, src/Modulation.jl:373-396).
 - The separate kernels (the exact evaluator's statistics and gpd_mean_var_power): one-pass
   k_faint_p1/p2/fin (one hypot per sample, |d| through a scratch) and the two-pass kernel
-  (GPD_FAINT_STATS=2; the windows' kernel) against the oracle, bit for bit, NaN for empty /
+  (option faint_stats = 2; the windows' kernel) against the oracle, bit for bit, NaN for empty /
   1-sample states included.
 - The fused statistics of the whole-exposure harmonic path (r4: formed by the state-split moment
   pass's producer waves, k_faint_fused_fin; one HBM pass for faint series) against the two-pass
@@ -34,9 +34,9 @@ def _series(N, P, seed):
 @pytest.mark.parametrize("kernel", ["one-pass", "two-pass"])
 @pytest.mark.parametrize("onlyhigh", [False, True])
 @pytest.mark.parametrize("N", [6000, 100_000])
-def test_mean_var_power_matches_oracle(gpu, oracle, monkeypatch, kernel, onlyhigh, N):
+def test_mean_var_power_matches_oracle(gpu, oracle, opts, kernel, onlyhigh, N):
     if kernel == "two-pass":
-        monkeypatch.setenv("GPD_FAINT_STATS", "2")
+        opts("faint_stats", 2)
     d, st = _series(N, 12, seed=N % 97)
     m5, w5 = gpu.mean_var_power_batch(st, d, onlyhigh=onlyhigh)
     for k in range(d.shape[0]):
@@ -58,27 +58,27 @@ def test_compute_mean_var_power_is_the_reference_function(gpu, oracle):
 
 
 @pytest.mark.parametrize("N,P", [(2047, 8), (131_073, 8), (100_000, 300)])
-def test_one_pass_equals_two_pass(gpu, monkeypatch, N, P):
+def test_one_pass_equals_two_pass(gpu, opts, N, P):
     """The two kernels give the same bits on every length (a part with no sample, ragged last
     slots) and across several cohorts (300 series × 1e5 samples = 2 cohorts of ≤ 239)."""
     d, st = _series(N, P, seed=3)
     a = gpu.mean_var_power_batch(st, d)
-    monkeypatch.setenv("GPD_FAINT_STATS", "2")
+    opts("faint_stats", 2)
     b = gpu.mean_var_power_batch(st, d)
     assert _bits(a[0], b[0]) and _bits(a[1], b[1])
 
 
 @pytest.mark.parametrize("method", ["exact", "harmonic"])
-def test_faint_fit_same_with_either_kernel(gpu, monkeypatch, method):
+def test_faint_fit_same_with_either_kernel(gpu, opts, method):
     """The separate kernels (one-pass, two-pass) give the same fits bit for bit (the harmonic
-    path takes them with GPD_FAINT_STATS=1/2 instead of its fused statistics)."""
+    path takes them with option faint_stats = 1|2 instead of its fused statistics)."""
     d, st = _series(30_000, 16, seed=9)
     B = synth.make_batch(30_000, 16, seed=9)
     args = (B["t"], d, B["fc"], B["fc_of_pixel"])
     st = np.where(st == 0, 2, st).astype(np.int8)  # no 1-sample state: finite fits
-    monkeypatch.setenv("GPD_FAINT_STATS", "1")
+    opts("faint_stats", 1)
     a = gpu.fit_batch(*args, state=st, method=method)
-    monkeypatch.setenv("GPD_FAINT_STATS", "2")
+    opts("faint_stats", 2)
     b = gpu.fit_batch(*args, state=st, method=method)
     assert a.tobytes() == b.tobytes()
 
@@ -106,7 +106,7 @@ def _check_fused(m, w, st, d, oracle, onlyhigh):
 @pytest.mark.parametrize("N,P,onlyhigh,c32", [(6000, 40, False, False), (100_000, 140, False, False),
                                               (100_000, 64, True, False), (30_000, 36, False, True),
                                               (2047, 8, False, False)])
-def test_fused_statistics_match_oracle(gpu, oracle, monkeypatch, N, P, onlyhigh, c32):
+def test_fused_statistics_match_oracle(gpu, oracle, opts, N, P, onlyhigh, c32):
     """The harmonic whole-exposure fit's faint statistics come from its moment pass (fused,
     r4): every series' m and w against the two-pass oracle within 1e-14 / 1e-13 relative,
     NaN where the oracle has no sample / one sample; the χ² aggregates Σw|d|², Σw m² n,
@@ -122,7 +122,7 @@ def test_fused_statistics_match_oracle(gpu, oracle, monkeypatch, N, P, onlyhigh,
     dw = d.astype(np.complex128)
     wm, ww = _check_fused(m, w, st, dw, oracle, onlyhigh)
     print(f"fused statistics N={N} P={P}: max rel m {wm:.2e}, w {ww:.2e}")
-    monkeypatch.setenv("GPD_FAINT_STATS", "1")
+    opts("faint_stats", 1)
     gpu.fit_batch(*args, state=st, onlyhigh=onlyhigh, method="harmonic")
     m1, w1, agg1 = gpu.last_faint_stats(P)
     np.testing.assert_allclose(agg, agg1, rtol=1e-13)

@@ -42,12 +42,12 @@ def test_fp32_arithmetic_close_to_fp64(gpu, faint):
     assert np.median(chi) < 1e-5
 
 
-def test_fp32_records_are_deterministic_and_shard_invariant(gpu, monkeypatch):
+def test_fp32_records_are_deterministic_and_shard_invariant(gpu, opts):
     B = synth.make_batch(8000, 48, seed=3)
     args = (B["t"], B["d"], B["fc"], B["fc_of_pixel"])
     one = gpu.fit_batch(*args, method="fp32")
     assert gpu.fit_batch(*args, method="fp32").tobytes() == one.tobytes()
-    monkeypatch.setenv("GPD_FAKE_GPUS", "1")
+    opts("fake_gpus", 1)
     two = gpu.fit_batch(*args, method="fp32", n_gpus=3)
     assert two.tobytes() == one.tobytes()
 

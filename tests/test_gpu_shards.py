@@ -3,7 +3,7 @@
 Series are independent (src/Modulation.jl:387-389), so a batch split over devices must give the
 1-device records bit for bit.  The harmonic moments are sums over fixed sample units (a function
 of N only), so neither the shard a series lands in nor the moment grid's fill (units per
-workgroup, GPD_UPW) changes them.  GPD_FAKE_GPUS=1 keeps n_gpus shards on a one-GPU box (shard g
+workgroup, option upw) changes them.  Option fake_gpus = 1 keeps n_gpus shards on a one-GPU box (shard g
 on device g % ndev): the library's multi-device split — series or window ranges, per-shard FC
 column subsets, record and output offsets — runs here exactly as on an 8-GPU node."""
 import numpy as np
@@ -24,8 +24,8 @@ def _same(a, b):
 
 @pytest.mark.parametrize("method", ["auto", "exact"])
 @pytest.mark.parametrize("faint", [False, True])
-def test_fit_batch_shards_bit_identical(gpu, monkeypatch, method, faint):
-    monkeypatch.setenv("GPD_FAKE_GPUS", "1")
+def test_fit_batch_shards_bit_identical(gpu, opts, method, faint):
+    opts("fake_gpus", 1)
     N, P = 5003, 70  # ragged: P not a multiple of 4 or of the shard count
     B = synth.make_batch(N, P, seed=61)
     st = faint_states(N, seed=3) if faint else None
@@ -37,9 +37,9 @@ def test_fit_batch_shards_bit_identical(gpu, monkeypatch, method, faint):
         np.testing.assert_array_equal(out, ref_out)
 
 
-def test_fit_batch_shards_offsets_harmonic(gpu, monkeypatch):
+def test_fit_batch_shards_offsets_harmonic(gpu, opts):
     """Harmonic fitoffsets: the shards' FC-column subsets carry their own G_n moments."""
-    monkeypatch.setenv("GPD_FAKE_GPUS", "1")
+    opts("fake_gpus", 1)
     B = synth.make_batch(4000, 48, seed=62, offsets=True)
     args = (B["t"], B["d"], B["fc"], B["fc_of_pixel"])
     ref = gpu.fit_batch(*args, fitoffsets=True, method="harmonic")
@@ -48,10 +48,10 @@ def test_fit_batch_shards_offsets_harmonic(gpu, monkeypatch):
 
 
 @pytest.mark.parametrize("window", [1500, 200])
-def test_fit_windows_shards_bit_identical(gpu, monkeypatch, window):
+def test_fit_windows_shards_bit_identical(gpu, opts, window):
     """Windows are split over devices (not diodes): a ragged last window, window-major record
     offsets and the demodulated output slices must land where the 1-device call puts them."""
-    monkeypatch.setenv("GPD_FAKE_GPUS", "1")
+    opts("fake_gpus", 1)
     N = 12_345
     B = synth.make_batch(N, 32, seed=63)
     fop = np.arange(32) // 4
@@ -63,7 +63,7 @@ def test_fit_windows_shards_bit_identical(gpu, monkeypatch, window):
         np.testing.assert_array_equal(out, ref_out)
 
 
-def test_records_independent_of_batch_and_grid(gpu, monkeypatch):
+def test_records_independent_of_batch_and_grid(gpu, opts):
     """A series' harmonic record does not depend on the other series of its batch (a sub-batch
     starting mid-workgroup) nor on the moment grid (units per workgroup 1, 2, 3, 7)."""
     N, P = 20_000, 96
@@ -76,7 +76,7 @@ def test_records_independent_of_batch_and_grid(gpu, monkeypatch):
                         method="harmonic")
     _same(got, ref[sub])
     for upw in ("1", "2", "3", "7"):
-        monkeypatch.setenv("GPD_UPW", upw)
+        opts("upw", int(upw))
         _same(gpu.fit_batch(*args, method="harmonic"), ref)
 
 
@@ -118,7 +118,7 @@ def test_full_length_shard_invariance_device(gpu):
 
 @pytest.mark.parametrize("faint", [False, True])
 @pytest.mark.parametrize("storage", ["c64", "c32"])
-def test_cohort_pipeline_records_bitwise(gpu, monkeypatch, faint, storage):
+def test_cohort_pipeline_records_bitwise(gpu, opts, faint, storage):
     """The pipelined harmonic path (series cohorts: moments of cohort c on the caller's stream
     while cohort c−1's fit runs on the side stream, gpd_engine.hip) gives the one-cohort records
     bit for bit, for any cohort count — the fixed sample units make a series' moments
@@ -137,18 +137,18 @@ def test_cohort_pipeline_records_bitwise(gpu, monkeypatch, faint, storage):
     args = (B["t"], d, fc, B["fc_of_pixel"])
     recs = {}
     for c in ("1", "2", "3", "5"):
-        monkeypatch.setenv("GPD_COHORTS", c)
+        opts("cohorts", int(c))
         recs[c] = gpu.fit_batch(*args, state=st, method="harmonic")
     for c, r in recs.items():
         _same(r, recs["1"])
     assert not np.any(recs["1"]["status"] & gpu.GPD_ST_NAN)
-    monkeypatch.setenv("GPD_COHORTS", "2")
+    opts("cohorts", 2)
     gpu.fit_batch(*args, state=st, method="harmonic")
     t = gpu.timings(0)
     assert "fit_tail" in t and t["moments"] > 0, t  # the cohort path ran
 
 
-def test_series_per_fit_wave_does_not_change_records(gpu, monkeypatch):
+def test_series_per_fit_wave_does_not_change_records(gpu, opts):
     """The harmonic fit packs ⌈P / CUs⌉ series per wave (fit_lanes_for, gpd_engine.hip); every
     lane runs the same arithmetic whatever its wave holds, so the records are the same bytes for
     1, 7, 49 and 64 series per wave and for the automatic choice (C2-sized batch and a batch
@@ -156,10 +156,10 @@ def test_series_per_fit_wave_does_not_change_records(gpu, monkeypatch):
     for N, P in ((20_000, 32), (8_000, 700)):
         B = synth.make_batch(N, P, seed=N + P, b_range=(0.3, 5.5))  # b > 4.5: exact fallback
         args = (B["t"], B["d"], B["fc"], B["fc_of_pixel"])
-        monkeypatch.delenv("GPD_FIT_LANES", raising=False)
+        opts("fit_lanes", 0)
         ref = gpu.fit_batch(*args, method="auto")
         for lanes in ("1", "7", "49", "64"):
-            monkeypatch.setenv("GPD_FIT_LANES", lanes)
+            opts("fit_lanes", int(lanes))
             _same(gpu.fit_batch(*args, method="auto"), ref)
         assert np.any(ref["status"] & gpu.GPD_ST_FALLBACK)
         assert np.mean((ref["status"] & gpu.GPD_ST_EXACT) == 0) > 0.5  # mostly harmonic

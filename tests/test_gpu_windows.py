@@ -144,7 +144,7 @@ def test_demodulate_windows_api(gpu, oracle):
 
 
 @pytest.mark.parametrize("faint,fitoffsets", [(False, False), (True, False), (False, True)])
-def test_short_windows_one_wave_per_series(gpu, oracle, monkeypatch, faint, fitoffsets):
+def test_short_windows_one_wave_per_series(gpu, oracle, opts, faint, fitoffsets):
     """Windows of < 256 samples are fitted exactly; past two 256-thread workgroups per CU of them
     the library takes one wave per series (k_fit_exact WGT = 64, which reduces a canonical block
     as block_sum's four waves would).  Its records equal the 256-thread kernel's byte for byte
@@ -155,10 +155,10 @@ def test_short_windows_one_wave_per_series(gpu, oracle, monkeypatch, faint, fito
     st = faint_states(N, seed=3) if faint else None
     args = (B["t"], B["d"], B["fc"], B["fc_of_pixel"], w)
     kw = dict(state=st, fitoffsets=fitoffsets, method="exact")
-    monkeypatch.delenv("GPD_EXACT_WGT", raising=False)
+    opts("exact_wgt", 0)
     auto = gpu.fit_windows(*args, **kw)
     assert auto.size > 2 * 256  # the one-wave kernel's range on a 256-CU part
-    monkeypatch.setenv("GPD_EXACT_WGT", "256")
+    opts("exact_wgt", 256)
     wg256 = gpu.fit_windows(*args, **kw)
     assert auto.tobytes() == wg256.tobytes()
     flags = oracle.RECENTER | (oracle.FIT_OFFSETS if fitoffsets else 0)

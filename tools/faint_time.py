@@ -30,6 +30,7 @@ def main():
 
     gpd = gpdemod_loader.load()
     L = gpd.load()
+    gpd.options_from_env()  # GPD_OPTS="name=value,..." (A/B runs)
     dev = torch.device("cuda", 0)
     sptr = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     P, N = args.series, args.samples

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Series per wave of the harmonic fit (GPD_FIT_LANES) against the batch size (GPU box): for each
+"""Series per wave of the harmonic fit (option fit_lanes) against the batch size (GPU box): for each
 P, device-resident synthetic series (N = 1e5, C3 generator), the fit kernel's HIP-event time per
 lanes-per-wave setting, and the records of every setting compared byte for byte with the first setting's.
 One JSON line per (P, lanes)."""
@@ -19,7 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pixels", default="32,128,256,512,1024,2048,4096,12500")
     ap.add_argument("--lanes", default="auto,64,32,16,8,4,2,1",
-                    help="'auto': the library's own choice (fit_lanes_for, GPD_FIT_LANES unset)")
+                    help="'auto': the library's own choice (fit_lanes_for, option fit_lanes = 0)")
     ap.add_argument("--samples", type=int, default=100_000)
     ap.add_argument("--reps", type=int, default=8)
     args = ap.parse_args()
@@ -47,9 +47,9 @@ def main():
         ref = None
         for lanes in args.lanes.split(","):
             if lanes == "auto":
-                os.environ.pop("GPD_FIT_LANES", None)
+                gpd.set_option("fit_lanes", 0)
             else:
-                os.environ["GPD_FIT_LANES"] = lanes
+                gpd.set_option("fit_lanes", int(lanes))
             fit, step = [], []
             for r in range(args.reps + 2):
                 s0 = torch.cuda.Event(enable_timing=True)

@@ -7,7 +7,7 @@ bit for bit:
                on the same values widened to ComplexF64;
   * faint    — gpd_mean_var_power (m, w per series and state) vs the oracle's
                compute_mean_var_power restatement, random state runs, onlyhigh;
-  * shards   — gpd_fit_batch(n_gpus = 2..5) with GPD_FAKE_GPUS=1 (shard g on device g mod 1)
+  * shards   — gpd_fit_batch(n_gpus = 2..5) with option fake_gpus = 1 (shard g on device g mod 1)
                vs n_gpus = 1, automatic method, demodulated output included;
   * mixed    — windows × ComplexF32 × faint × fitoffsets × MJD-scale t0 × device shards, exact
                evaluator, against the oracle per window slice.
@@ -31,7 +31,6 @@ def main():
     ap.add_argument("--seconds", type=float, default=150.0)
     ap.add_argument("--seed", type=int, default=11)
     args = ap.parse_args()
-    os.environ["GPD_FAKE_GPUS"] = "1"
     import numpy as np
 
     import gpdemod_loader
@@ -40,6 +39,7 @@ def main():
     from test_gpu_parity import assert_exact_bitwise
 
     gpd = gpdemod_loader.load()
+    gpd.set_option("fake_gpus", 1)
     gpd.load()
     oracle.build()
     rng = np.random.default_rng(args.seed)

@@ -5,7 +5,7 @@ processmetrology's windowed mode fits every window of `nwindow` samples on its o
 (src/GPPupilDemodulation.jl:191-205; 1-s windows at 500 Hz = 500 samples).  For each window length
 w, `--exposures` exposures of 8 windows × 32 diodes are fitted through gpd_fit_windows with the
 harmonic evaluator forced (METHOD_HARMONIC is refused below HARM_MIN_SPAN, so the sweep asks
-the library's windows API with GPD_HARM_MIN_SPAN=1, a test override) and by the oracle on every
+the library's windows API with option harm_min_span = 1, a test override) and by the oracle on every
 window's slice, with 12 perturbed oracle runs (χ² × (1 ± 128 ulp)).  Reports per w: the fraction
 within 1e-10, the max deviation, the oracle's own envelope, and how many series land beyond
 NEWUOA's rhoend (1e-3).  Output: one JSON object (profiles/r3/window_sweep.json)."""
@@ -27,7 +27,6 @@ def main():
     ap.add_argument("--exposures", type=int, default=4)
     ap.add_argument("--perturb", type=int, default=12)
     args = ap.parse_args()
-    os.environ["GPD_HARM_MIN_SPAN"] = "1"
     import numpy as np
 
     import gpdemod_loader
@@ -35,6 +34,7 @@ def main():
     import synth
 
     gpd = gpdemod_loader.load()
+    gpd.set_option("harm_min_span", 1)
     gpd.load()
 
     def dev(x, r):

@@ -37,7 +37,7 @@ def main():
                               method=args.method)
         ts.append(time.perf_counter() - t0)
     print(json.dumps({"window": args.window, "series": int(rec.size), "method": args.method,
-                      "fit_lanes": os.environ.get("GPD_FIT_LANES", "auto"),
+                      "fit_lanes": gpd.get_option("fit_lanes") or "auto",
                       "call_ms": round(1e3 * float(np.median(ts[1:])), 3),
                       "kernels_ms": {k: round(v, 3) for k, v in gpd.timings(0).items()},
                       "records_sha": __import__("hashlib").sha256(rec.tobytes()).hexdigest()[:16]}))
