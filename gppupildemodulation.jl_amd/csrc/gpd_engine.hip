@@ -57,6 +57,8 @@ enum OptId {
     O_UNITS,         // 0: automatic sample units of the moment pass; n forced
     O_UPW,           // 0: automatic units per moment workgroup; n forced
     O_FIT_LANES,     // 0: automatic series per harmonic-fit wave; n forced
+    O_FIT_LPS,       // 0: automatic lanes per series of the harmonic fit; 1|2|4|8 forced
+    O_FIT_WPB,       // 0: automatic waves per harmonic-fit workgroup; 1..4 forced
     O_COHORTS,       // 1: one series cohort; n > 1: pipelined harmonic cohorts
     O_HARM_MIN_SPAN, // shortest window fitted from harmonic moments (samples)
     O_FS_COHORT_MB,  // |d| scratch per cohort of the one-pass faint statistics (MB)
@@ -73,10 +75,10 @@ constexpr OptDef kOpt[O_COUNT] = {
     {"mix", 1},          {"faint_stats", 0},   {"faint_side", 0},    {"fake_gpus", 0},
     {"exact_g", 0},      {"exact_waves", 0},   {"exact_wgt", 0},     {"exact_fast", 1},
     {"exact_mcache", 1}, {"xspin_test", 0},    {"units", 0},         {"upw", 0},
-    {"fit_lanes", 0},    {"cohorts", 1},       {"harm_min_span", 256}, {"fs_cohort_mb", 4096},
+    {"fit_lanes", 0},    {"fit_lps", 0},       {"fit_wpb", 0},       {"cohorts", 1},       {"harm_min_span", 256}, {"fs_cohort_mb", 4096},
     {"moments", 0},      {"fit_prof", 0},      {"sync_debug", 0}};
-std::atomic<long long> g_opt[O_COUNT] = {
-    {1}, {0}, {0}, {0}, {0}, {0}, {0}, {1}, {1}, {0}, {0}, {0}, {0}, {1}, {256}, {4096}, {0}, {0}, {0}};
+std::atomic<long long> g_opt[O_COUNT] = {{1}, {0}, {0},   {0},    {0}, {0}, {0}, {1}, {1}, {0}, {0},
+                                          {0}, {0}, {0},   {0},    {1}, {256}, {4096}, {0}, {0}, {0}};
 inline long long opt(OptId o) { return g_opt[o].load(std::memory_order_relaxed); }
 int opt_find(const char *name) {
     if (!name) return -1;
@@ -178,19 +180,66 @@ struct Layout {
 // C3 (782 series groups, 256 CUs, U = 26): upw 1 or 2 → 79.4 / 39.7 waves; 12 500 series per GPU
 // (C4 on 8 GPUs, 98 groups): upw 1 → 2548 workgroups = 9.95 waves (with 32 units: 12.25 waves,
 // a 0.75-wave tail).
-// Series per wave of the lane-per-series fit (k_fit_harmonic).  A wave lasts as long as its
-// slowest lane, and lanes diverging through NEWUOA's branches serialise its phases,
-// so fewer series per wave finish sooner — as long as the waves do not crowd the CUs: the fewest
-// lanes (≤ 64) that keep the fit at one wave per CU, ⌈P / n_cu⌉.  Measured on one MI355X
-// (tools/fit_lanes_sweep.py, profiles/r3/fit_lanes_*.jsonl): one exposure (32 series) 0.71 →
-// 0.42 ms, 512 series 0.95 → 0.58 ms, 2048 series 0.96 → 0.82 ms, a C4 rank (12 500 series, 49
-// lanes) 1.05 → 1.01 ms; 1e5 series stay at 64.  Every lane runs the same arithmetic whatever the
-// wave holds: the records are the same bits for any setting.  GPD_FIT_LANES overrides (A/B).
-int fit_lanes_for(long long P, int n_cu) {
-    long long lanes = (P + std::max(1, n_cu) - 1) / std::max(1, n_cu);
-    lanes = std::max<long long>(1, std::min<long long>(GPD_FIT_WAVE_LANES, lanes));
-    if (opt(O_FIT_LANES) > 0) lanes = std::min<long long>(GPD_FIT_WAVE_LANES, opt(O_FIT_LANES));
-    return (int)lanes;
+// Shape of the harmonic fit (k_fit_harmonic<lps>): lps lanes per series, gpw series per wave,
+// wpb waves per workgroup.  A wave lasts as long as its slowest series' NEWUOA (lanes diverging
+// through NEWUOA's branches serialise its phases), and one series' own path is a
+// long latency-bound chain; so a small batch gets several lanes per series (the objective's
+// harmonics and the 49-angle searches split across them), a large one one lane per series.
+// lps: the most lanes (≤ 8) that keep the fit within one wave per SIMD; gpw: the series spread
+// over every SIMD; wpb: 4 (a workgroup's waves go to the 4 SIMDs of a CU).  The canonical
+// objective makes the records the same bits for every shape.  Options fit_lps, fit_lanes,
+// fit_wpb override (A/B).
+struct FitShape {
+    int lps, gpw, wpb;
+    unsigned grid;
+    size_t lds;
+};
+FitShape fit_shape(long long P, int n_cu) {
+    const long long simds = 4LL * std::max(1, n_cu);
+    FitShape f{};
+    f.lps = 1;
+    for (int l = 8; l >= 2; l >>= 1)
+        if ((P + 64 / l - 1) / (64 / l) <= simds) {
+            f.lps = l;
+            break;
+        }
+    if (opt(O_FIT_LPS) > 0) f.lps = (int)opt(O_FIT_LPS);
+    const long long cap = 64 / f.lps;
+    long long gpw = (P + simds - 1) / simds;
+    gpw = std::max<long long>(1, std::min<long long>(cap, gpw));
+    if (opt(O_FIT_LANES) > 0) gpw = std::min<long long>(cap, opt(O_FIT_LANES));
+    f.gpw = (int)gpw;
+    f.wpb = 4;
+    if (opt(O_FIT_WPB) > 0) f.wpb = (int)std::min(4LL, opt(O_FIT_WPB));
+    const long long waves = (P + gpw - 1) / gpw;
+    f.wpb = (int)std::max(1LL, std::min<long long>(f.wpb, waves));
+    f.grid = (unsigned)((waves + f.wpb - 1) / f.wpb);
+    f.lds = (size_t)f.wpb * (size_t)f.gpw * sizeof(Newuoa<2, 5, true, 1>);
+    return f;
+}
+
+hipError_t launch_fit(const FitShape &fs, Problem pb, const Info *info, const double *mom,
+                      const double *aux, const double *momG, long long PG, const double *d0,
+                      Param *out, double *raw, int *list, int *count, hipStream_t s) {
+    pb.fit_lanes = fs.gpw;
+    const dim3 g(fs.grid), b(64 * fs.wpb);
+    hipError_t e = hipSuccess;
+    auto go = [&](auto kern) {
+        if (fs.lds > 48 * 1024) {  // beyond the default dynamic-LDS limit (C3: 4 × 64 states)
+            e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)fs.lds);
+            if (e != hipSuccess) return;
+        }
+        kern<<<g, b, fs.lds, s>>>(pb, info, mom, aux, momG, PG, d0, out, raw, list, count);
+        e = hipGetLastError();
+    };
+    switch (fs.lps) {
+        case 8: go(k_fit_harmonic<8>); break;
+        case 4: go(k_fit_harmonic<4>); break;
+        case 2: go(k_fit_harmonic<2>); break;
+        default: go(k_fit_harmonic<1>); break;
+    }
+    return e;
 }
 
 void moment_grid(long long N, long long P, int n_cu, bool harmonic, bool mfma, int &units,
@@ -744,9 +793,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             HIP_TRY(hipEventRecord(cx->fork[c], stream));
             HIP_TRY(hipStreamWaitEvent(side, cx->fork[c], 0));
             const int b0 = rec(side);
-            sp.fit_lanes = fit_lanes_for(n, cx->n_cu);
-            k_fit_harmonic<<<(unsigned)((n + sp.fit_lanes - 1) / sp.fit_lanes), 64, 0, side>>>(
-                sp, info, mom_c, aux_c, nullptr, n_fc, nullptr, out_c, raw_c, list_c, count_c);
+            HIP_TRY(launch_fit(fit_shape(n, cx->n_cu), sp, info, mom_c, aux_c, nullptr, n_fc,
+                               nullptr, out_c, raw_c, list_c, count_c, side));
             const int b1 = mark_on(side, b0, "fit_harmonic");
             const unsigned xg = (unsigned)std::min<long long>(n, 1024);
             if (faint)
@@ -921,11 +969,9 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             HIP_TRY(prof_reset());
             Problem pp = pb;
             pp.flags |= F_PROF;
-            pp.fit_lanes = fit_lanes_for(P, cx->n_cu);
-            const unsigned fit_wg = (unsigned)((P + pp.fit_lanes - 1) / pp.fit_lanes);
-            k_fit_harmonic<<<fit_wg, 64, 0, stream>>>(pp, info, mom, aux, momG,
-                                                                       n_fc, d0, outp, raw, list,
-                                                                       count);
+            const FitShape fsh = fit_shape(P, cx->n_cu);
+            HIP_TRY(launch_fit(fsh, pp, info, mom, aux, momG, n_fc, d0, outp, raw, list, count,
+                               stream));
             HIP_TRY(prof_read());
             const unsigned long long *z = prof_h + PROF_FIT;
             fprintf(stderr, "fit_prof per series: objective %.3g cycles, whole fit %.3g, evals %.3g\n",
@@ -933,10 +979,12 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
 #ifdef GPD_DIAG
             const unsigned long long *zn = prof_h + PROF_NW;
             fprintf(stderr, "fit_prof newuoa per series: trsapp %.3g biglag %.3g bigden %.3g "
-                    "update %.3g init %.3g vlag/beta %.3g model-update %.3g cycles (lanes %d)\n",
+                    "update %.3g init %.3g vlag/beta %.3g model-update %.3g cycles (lps %d, "
+                    "series per wave %d, waves per workgroup %d)\n",
                     (double)zn[0] / P, (double)zn[1] / P, (double)zn[2] / P, (double)zn[3] / P,
-                    (double)zn[4] / P, (double)zn[5] / P, (double)zn[6] / P, pp.fit_lanes);
-            const double nw = (double)fit_wg;  // waves
+                    (double)zn[4] / P, (double)zn[5] / P, (double)zn[6] / P, fsh.lps, fsh.gpw,
+                    fsh.wpb);
+            const double nw = (double)((P + fsh.gpw - 1) / fsh.gpw);  // waves
             fprintf(stderr, "fit_prof per wave: objective %.3g trsapp %.3g biglag %.3g update %.3g "
                     "init %.3g vlag/beta %.3g model-update %.3g cycles, whole fit (max lane) "
                     "n/a\n", (double)z[4] / nw, (double)zn[8] / nw, (double)zn[9] / nw,
@@ -944,10 +992,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                     (double)zn[14] / nw);
 #endif
         } else {
-            Problem pf = pb;
-            pf.fit_lanes = fit_lanes_for(P, cx->n_cu);
-            k_fit_harmonic<<<(unsigned)((P + pf.fit_lanes - 1) / pf.fit_lanes), 64, 0, stream>>>(
-                pf, info, mom, aux, momG, n_fc, d0, outp, raw, list, count);
+            HIP_TRY(launch_fit(fit_shape(P, cx->n_cu), pb, info, mom, aux, momG, n_fc, d0, outp,
+                               raw, list, count, stream));
         }
         mark("fit_harmonic");
         // fallback: series whose fit left the expansion's safe range, re-fitted exactly

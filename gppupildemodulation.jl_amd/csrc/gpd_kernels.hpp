@@ -2121,13 +2121,29 @@ __global__ __launch_bounds__(256) void k_moments_win(Problem pb, const double *_
 #endif
 
 
-// χ²(b,ϕ) from the moments of one series (lane).
+// χ²(b,ϕ) from the moments of one series, evaluated by a group of LPS consecutive lanes of a
+// wave (LPS ∈ {1, 2, 4, 8}; sub-lane r = lane mod LPS).  The arithmetic is canonical — the
+// same operations in the same order whatever LPS is (r5), so that the records do not depend on
+// how many lanes a series gets (the engine picks LPS from the batch size):
+//   S(b,ϕ) = J_0·F_0 + T,  T = Σ_{n=1..24} 2J_n·t_n(ϕ) summed as 8 slot partials — slot s holds
+//   n = s+1, s+9, s+17 (in that order, the first product then two fmas) — combined by the xor
+//   butterfly over the slots at distances 4, 2, 1 (each level: lower slot + upper slot, so both
+//   partners hold the same bits); e^{-jnϕ}'s components by angle addition: (c_m, s_m) for
+//   m = 1..8 from (cos ϕ, sin ϕ), then n = m + 8q by q rotations through (c_8, s_8).
+// Lane r of the group holds slots r, r + LPS, …: with LPS = 8 every level of the butterfly is a
+// cross-lane exchange, with LPS = 1 every level is in-lane.  (Before r5: one lane per series, the
+// 24 harmonics in one sequential recurrence and fma chain — a different rounding of the same
+// sum, within the harmonic evaluator's stated χ² error.)
+template <int LPS>
 struct HarmChi2 {
+    static_assert(LPS == 1 || LPS == 2 || LPS == 4 || LPS == 8, "lanes per series");
+    static constexpr int NS = 8 / LPS;  // slots per lane
     const double *__restrict__ mom;
     long long P, k;
     double nvalid, W2, DEN, tailref, qbase, phimax;
     double a_re, a_im;
     int nfev;
+    int r;  // sub-lane of the group (0 for LPS = 1)
     bool fallback;
     // fitoffsets (ModulationWithOffsets, src/Modulation.jl:174-192): moments G of the series' FC
     // phasor (momG[m][g], PG columns), Σw and Σw d
@@ -2136,47 +2152,118 @@ struct HarmChi2 {
     long long PG, g;
     double W0, D0r, D0i, c_re, c_im;
 
-    // Σ_n J_n(b) e^{-jnϕ} M_n for moments M in the layout of k_moments (F0 re/im at rows 0-1,
-    // (A,B,C,D)_n at rows 3+4(n-1)..)
     // The moments are read through a global-address-space pointer: reached through this
     // out-of-line functor, a plain pointer is generic, and flat loads both cost more and make
     // every wait drain all outstanding loads (flat counts on vmcnt and lgkmcnt).
     typedef const __attribute__((address_space(1))) double gdouble;
+
+    // Σ_n J_n(b) e^{-jnϕ} M_n for moments M in the layout of k_moments (F0 re/im at rows 0-1,
+    // (A,B,C,D)_n at rows 3+4(n-1)..), canonical order (above)
     __device__ __forceinline__ void combine(const double *__restrict__ m_, long long ld, long long col,
                                             const double (&J)[KH + 2], double cph, double sph,
                                             double &Sr, double &Si) const {
-        gdouble *p = (gdouble *)m_ + col;  // row r of this series at p[r·ld]
-        Sr = J[0] * p[0];
-        Si = J[0] * p[ld];
-        p += 3 * ld;
-        double cn = 1.0, sn = 0.0;
+        gdouble *p = (gdouble *)m_ + col;  // row q of this series at p[q·ld]
+        double c[9], s[9];
+        c[1] = cph;
+        s[1] = sph;
 #pragma unroll
-        for (int n = 1; n <= KH; ++n) {
-            const double c2 = cn * cph - sn * sph;
-            const double s2 = sn * cph + cn * sph;
-            cn = c2;
-            sn = s2;
-            gdouble *q = p;
-            const double A = *q;
-            q += ld;
-            const double B = *q;
-            q += ld;
-            const double C = *q;
-            q += ld;
-            const double D = *q;
-            p = q + ld;
-            double tr, ti;
-            if ((n & 1) == 0) {
-                tr = fma(A, cn, -(D * sn));
-                ti = fma(C, cn, -(B * sn));
-            } else {
-                tr = fma(B, cn, C * sn);
-                ti = -fma(D, cn, A * sn);
-            }
-            const double j2 = 2.0 * J[n];
-            Sr = fma(j2, tr, Sr);
-            Si = fma(j2, ti, Si);
+        for (int m = 2; m <= 8; ++m) {
+            c[m] = c[m - 1] * cph - s[m - 1] * sph;
+            s[m] = s[m - 1] * cph + c[m - 1] * sph;
         }
+        const double c8 = c[8], s8 = s[8];
+        double vr[NS], vi[NS];
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            // slot j's angle components and Bessel factors: compile-time for LPS = 1; for LPS > 1
+            // the slot depends on the lane — captured by compare-and-select against every
+            // candidate (no register array indexed at run time, which would go through scratch)
+            int m;
+            double cn, sn, jq[3];
+            if constexpr (LPS == 1) {
+                m = j + 1;
+                cn = c[m];
+                sn = s[m];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) jq[q] = J[m + 8 * q];
+            } else {
+                m = r + LPS * j + 1;
+                cn = c[1];
+                sn = s[1];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) jq[q] = J[1 + 8 * q];
+#pragma unroll
+                for (int mm = 2; mm <= 8; ++mm) {
+                    const bool hit = m == mm;
+                    cn = hit ? c[mm] : cn;
+                    sn = hit ? s[mm] : sn;
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) jq[q] = hit ? J[mm + 8 * q] : jq[q];
+                }
+            }
+            // odd n: the even form with (A', B', C', D') = (B, A, −D, −C) gives fma(B, cn, C sn)
+            // and −fma(D, cn, A sn), bit for bit (negation and ×(±1) are exact)
+            const bool odd = (m & 1) != 0;
+            const int oA = odd ? 1 : 0, oB = odd ? 0 : 1, oC = odd ? 3 : 2, oD = odd ? 2 : 3;
+            const double sg = odd ? -1.0 : 1.0;
+            double pr = 0.0, pi = 0.0;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const int n = m + 8 * q;
+                if (q > 0) {
+                    const double c2 = cn * c8 - sn * s8;
+                    const double s2 = sn * c8 + cn * s8;
+                    cn = c2;
+                    sn = s2;
+                }
+                gdouble *rw = p + (long long)(3 + 4 * (n - 1)) * ld;
+                const double A = rw[oA * ld], B = rw[oB * ld];
+                const double C = sg * rw[oC * ld], D = sg * rw[oD * ld];
+                const double tr = fma(A, cn, -(D * sn));
+                const double ti = fma(C, cn, -(B * sn));
+                const double j2 = 2.0 * jq[q];
+                if (q == 0) {
+                    pr = j2 * tr;
+                    pi = j2 * ti;
+                } else {
+                    pr = fma(j2, tr, pr);
+                    pi = fma(j2, ti, pi);
+                }
+            }
+            vr[j] = pr;
+            vi[j] = pi;
+        }
+        // the butterfly over the 8 slots: distance 4, 2, 1 (in-lane while the distance spans
+        // this lane's slots, then across the group's lanes)
+        if constexpr (LPS <= 4) {
+#pragma unroll
+            for (int j = 0; j < 4 / LPS; ++j) {
+                vr[j] = vr[j] + vr[j + 4 / LPS];
+                vi[j] = vi[j] + vi[j + 4 / LPS];
+            }
+        } else {
+            vr[0] = vr[0] + lane_xor<4>(vr[0]);
+            vi[0] = vi[0] + lane_xor<4>(vi[0]);
+        }
+        if constexpr (LPS <= 2) {
+#pragma unroll
+            for (int j = 0; j < 2 / LPS; ++j) {
+                vr[j] = vr[j] + vr[j + 2 / LPS];
+                vi[j] = vi[j] + vi[j + 2 / LPS];
+            }
+        } else {
+            vr[0] = vr[0] + lane_xor<2>(vr[0]);
+            vi[0] = vi[0] + lane_xor<2>(vi[0]);
+        }
+        if constexpr (LPS == 1) {
+            vr[0] = vr[0] + vr[1];
+            vi[0] = vi[0] + vi[1];
+        } else {
+            vr[0] = vr[0] + lane_xor<1>(vr[0]);
+            vi[0] = vi[0] + lane_xor<1>(vi[0]);
+        }
+        Sr = J[0] * p[0] + vr[0];
+        Si = J[0] * p[ld] + vi[0];
     }
 
     // one out-of-line copy: NEWUOA calls the objective from several sites, and each inlined
@@ -2190,13 +2277,13 @@ struct HarmChi2 {
     __device__ GPD_FIT_OBJ_ATTR double operator()(const double (&x)[2]) {
         // one inlined copy of eval (the cycle split only brackets it)
         const unsigned long long t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
-        const double r = eval(x);
+        const double v = eval(x);
         if (prof) {
             const unsigned long long dt = __builtin_amdgcn_s_memtime() - t0;
             prof_cycles += dt;
             if ((int)threadIdx.x == __builtin_amdgcn_readfirstlane((int)threadIdx.x)) prof_wave += dt;
         }
-        return r;
+        return v;
     }
     __device__ __forceinline__ double eval(const double (&x)[2]) {
         ++nfev;
@@ -2251,7 +2338,8 @@ struct HarmChi2 {
 // range are appended to `list` for the exact evaluator.
 // Offsets fields of the objective (fitoffsets, non-faint): G moments of the FC columns and
 // Σ d of the series.
-__device__ __forceinline__ void harm_offsets(HarmChi2 &f, const Problem &pb, long long k,
+template <class F>
+__device__ __forceinline__ void harm_offsets(F &f, const Problem &pb, long long k,
                                              const double *__restrict__ momG, long long PG,
                                              const double *__restrict__ d0) {
     f.offs = (pb.flags & F_OFFSETS) != 0;
@@ -2265,43 +2353,43 @@ __device__ __forceinline__ void harm_offsets(HarmChi2 &f, const Problem &pb, lon
     f.D0i = d0[2 * k + 1];
 }
 
-// A/B builds: GPD_FIT_WAVE_LANES series per 64-thread workgroup (the other lanes idle; LDS and
-// the launch grid scale with it), GPD_FIT_MINB workgroups per CU the register allocation must allow
-#ifndef GPD_FIT_WAVE_LANES
-#define GPD_FIT_WAVE_LANES 64
-#endif
-#ifndef GPD_FIT_MINB
-#define GPD_FIT_MINB 1
-#endif
-__global__ __launch_bounds__(64, GPD_FIT_MINB) void k_fit_harmonic(Problem pb, const Info *__restrict__ info,
-                                                     const double *__restrict__ mom,
-                                                     const double *__restrict__ aux,
-                                                     const double *__restrict__ momG, long long PG,
-                                                     const double *__restrict__ d0,
-                                                     Param *__restrict__ out, double *__restrict__ raw,
-                                                     int *__restrict__ list, int *__restrict__ count)
+// k_fit_harmonic<LPS>: a group of LPS lanes per series (the canonical objective above and
+// NEWUOA's trial-angle searches split across the group; NEWUOA itself runs replicated on the
+// group's lanes, its state shared in LDS), pb.fit_lanes series per wave, blockDim.x / 64 waves
+// per workgroup (a workgroup's waves are placed on different SIMDs of one CU).  Dynamic LDS:
+// one NEWUOA state (71 doubles, odd 8-byte stride) per series of the workgroup.  Series whose
+// NEWUOA probes leave the expansion's safe range are appended to `list` for the exact evaluator.
+template <int LPS>
+__global__ __launch_bounds__(256, 1) void k_fit_harmonic(Problem pb, const Info *__restrict__ info,
+                                                         const double *__restrict__ mom,
+                                                         const double *__restrict__ aux,
+                                                         const double *__restrict__ momG, long long PG,
+                                                         const double *__restrict__ d0,
+                                                         Param *__restrict__ out, double *__restrict__ raw,
+                                                         int *__restrict__ list, int *__restrict__ count)
 #if GPD_OWNS(GPD_U_FITH)
 {
-    // NEWUOA state of each lane in LDS (71 doubles, odd 8-byte stride): its ~1e3 dependent
-    // accesses per iteration stay at LDS latency instead of spilling through the caches
-    __shared__ Newuoa<2, 5, true> nwpool[GPD_FIT_WAVE_LANES];
-    // series per wave (pb.fit_lanes, fit_lanes_for() in gpd_engine.hip): only the first `lanes`
-    // lanes of each wave hold a series
-    const int lanes = pb.fit_lanes > 0 ? pb.fit_lanes : GPD_FIT_WAVE_LANES;
-    if ((int)threadIdx.x >= lanes) return;
-    const long long k = (long long)blockIdx.x * lanes + threadIdx.x;
+    typedef Newuoa<2, 5, true, LPS> NW;
+    extern __shared__ __attribute__((aligned(16))) double fit_lds[];
+    const int lane = (int)threadIdx.x & 63, wv = (int)threadIdx.x >> 6;
+    const int gpw = pb.fit_lanes > 0 ? pb.fit_lanes : 64 / LPS;  // series per wave
+    const int grp = lane / LPS, r = lane & (LPS - 1);
+    if (grp >= gpw) return;
+    const long long k = ((long long)blockIdx.x * (blockDim.x >> 6) + wv) * gpw + grp;
     if (k >= pb.P) return;
+    NW &nw = ((NW *)fit_lds)[wv * gpw + grp];
     const Info in = *info;
     const Span sp = span_of(pb, k);
     // harmonic path unusable for these timestamps, or a short (last) window: exact fit
     if (in.mode == 2 || sp.s1 - sp.s0 < pb.harm_min) {
-        list[atomicAdd(count, 1)] = (int)k;
+        if (r == 0) list[atomicAdd(count, 1)] = (int)k;
         return;
     }
-    HarmChi2 f;
+    HarmChi2<LPS> f;
     f.mom = mom;
     f.P = pb.P;
     f.k = k;
+    f.r = r;
     f.nvalid = aux[4 * k + 3];
     f.W2 = aux[4 * k + 0];
     f.DEN = aux[4 * k + 1];
@@ -2321,20 +2409,21 @@ __global__ __launch_bounds__(64, GPD_FIT_MINB) void k_fit_harmonic(Problem pb, c
     int status = 0;
 #ifdef GPD_DIAG
 #pragma unroll
-    for (int q = 0; q < 16; ++q) nwpool[threadIdx.x].prof_[q] = 0;
+    for (int q = 0; q < 16; ++q) nw.prof_[q] = 0;
 #endif
-    drive_fit(f, pb, x, status, nwpool[threadIdx.x]);
+    drive_fit(f, pb, x, status, nw);
     const double chi2 = f(x);  // likelihood[idx] = lkl(x) (src/Modulation.jl:416)
-    if (f.prof) {
+    if (f.prof && r == 0) {
         atomicAdd(&pb.prof[PROF_FIT + 0], f.prof_cycles);
         atomicAdd(&pb.prof[PROF_FIT + 1], __builtin_amdgcn_s_memtime() - tfit);
         atomicAdd(&pb.prof[PROF_FIT + 2], (unsigned long long)f.nfev);
 #ifdef GPD_DIAG
 #pragma unroll
-        for (int q = 0; q < 16; ++q) atomicAdd(&pb.prof[PROF_NW + q], nwpool[threadIdx.x].prof_[q]);
+        for (int q = 0; q < 16; ++q) atomicAdd(&pb.prof[PROF_NW + q], nw.prof_[q]);
         atomicAdd(&pb.prof[PROF_FIT + 4], f.prof_wave);
 #endif
     }
+    if (r != 0) return;
     if (f.fallback) {
         list[atomicAdd(count, 1)] = (int)k;
         return;
@@ -3331,7 +3420,8 @@ __global__ __launch_bounds__(64) void k_chi2_harmonic(Problem pb, const Info *__
     const long long k = (long long)blockIdx.x * 64 + threadIdx.x;
     if (k >= pb.P) return;
     const Info in = *info;
-    HarmChi2 f;
+    HarmChi2<1> f;
+    f.r = 0;
     f.mom = mom;
     f.P = pb.P;
     f.k = k;

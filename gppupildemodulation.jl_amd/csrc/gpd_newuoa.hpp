@@ -124,7 +124,10 @@ constexpr double kAngSin[50] = {
 #define GPD_NW_T1(v, slot)
 #endif
 
-template <int N, int NPT, bool DIRECT = false>
+// LPS: lanes per fit (k_fit_harmonic<LPS>: a group of LPS consecutive lanes runs one NEWUOA,
+// replicated — every lane of the group holds the same values and takes the same branches — and
+// splits the 49-angle searches of TRSAPP, BIGLAG and BIGDEN across its lanes, angle_search).
+template <int N, int NPT, bool DIRECT = false, int LPS = 1>
 struct Newuoa {
 #ifdef GPD_DIAG
     unsigned long long prof_[16];
@@ -169,13 +172,48 @@ struct Newuoa {
     double bmat[NDIM][N], zmat[NPT][NPTM], d[N], vlag[NDIM], w[NDIM];
 
 
-    // Powell's search over the trial angles i·2π/50 (TRSAPP's boundary iterations, BIGLAG):
-    // f(0) = fbeg, f(i) = val(i) for i = 1..49.  The published loop walks i in order keeping the
-    // first strictly better value (better(a, b); NaN is never better) and the values around it:
-    // fbest = f(isave), tempa = f(isave − 1) (f(−1) = f(49)), tempb = f(isave + 1) (f(50) = fbeg).
+    // Powell's search over the trial angles i·2π/50 (TRSAPP's boundary iterations, BIGLAG,
+    // BIGDEN): f(0) = fbeg, f(i) = val(i) for i = 1..49.  The published loop walks i in order
+    // keeping the first strictly better value (better(a, b); NaN is never better) and the values
+    // around it: fbest = f(isave), tempa = f(isave − 1) (f(−1) = f(49)), tempb = f(isave + 1)
+    // (f(50) = fbeg).  isave is therefore the first index of the best key among the non-NaN
+    // values, index 0 winning ties (none of f(1..49) strictly better than fbeg, or fbeg NaN).
+    // LPS > 1 (device): lane r of the group takes i = r + 1, r + 1 + LPS, … in order and keeps
+    // its first best, the group combines (value, index) pairs by a butterfly whose rule — a
+    // valid value strictly better wins, between equals the smaller index — picks that same
+    // index on every lane; fbest, tempa, tempb are then val() at isave and its neighbours,
+    // recomputed with the same operations: the same bits as the sequential loop.
     template <class V, class B>
     GPD_HD static void angle_search(double fbeg, V &&val, B &&better, int &isave, double &fbest,
                                     double &tempa, double &tempb) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        if constexpr (LPS > 1) {
+            const int r = (int)threadIdx.x & (LPS - 1);
+            int bi = 0;
+            double bv = __builtin_nan("");
+            for (int i = r + 1; i <= 49; i += LPS) {
+                const double v = val(i);
+                if (v == v && (bv != bv || better(v, bv))) {
+                    bv = v;
+                    bi = i;
+                }
+            }
+            auto merge = [&](double pv, int pi) {
+                if (pv == pv && (bv != bv || better(pv, bv) || (!better(bv, pv) && pi < bi))) {
+                    bv = pv;
+                    bi = pi;
+                }
+            };
+            if constexpr (LPS >= 8) merge(lane_xor<4>(bv), __shfl_xor(bi, 4, 64));
+            if constexpr (LPS >= 4) merge(lane_xor<2>(bv), __shfl_xor(bi, 2, 64));
+            merge(lane_xor<1>(bv), __shfl_xor(bi, 1, 64));
+            isave = better(bv, fbeg) ? bi : 0;
+            fbest = isave == 0 ? fbeg : val(isave);
+            tempa = isave == 0 ? val(49) : isave == 1 ? fbeg : val(isave - 1);
+            tempb = isave == 49 ? fbeg : val(isave + 1);
+            return;
+        }
+#endif
         double fsav = fbeg, fnew = fbeg;
         fbest = fbeg;
         tempa = 0.0;
@@ -676,34 +714,30 @@ struct Newuoa {
 
             sum = denex[0] + denex[1] + denex[3] + denex[5] + denex[7];
             denold = sum;
-            denmax = sum;
             int isave = 0;
             const int iu = 49;
             const double dang = kTwoPi / (double)(iu + 1);
             par[0] = 1.0;
-            #pragma unroll 7  // 49 = 7·7 trial angles: independent values, ILP across 7
-            for (int i = 1; i <= iu; ++i) {
-                par[1] = kAngCos[i];
-                par[2] = kAngSin[i];
+            // the published loop over i = 1..49 (first strictly larger |Σ denex·par|) as
+            // angle_search: the same index and values (split across the group for LPS > 1)
+            angle_search(
+                denold,
+                [&](int i) {
+                    double pw[9];
+                    pw[0] = 1.0;
+                    pw[1] = kAngCos[i];
+                    pw[2] = kAngSin[i];
 #pragma unroll
-                for (int j = 3; j <= 7; j += 2) {
-                    par[j] = par[1] * par[j - 2] - par[2] * par[j - 1];
-                    par[j + 1] = par[1] * par[j - 1] + par[2] * par[j - 2];
-                }
-                const double sumold = sum;
-                sum = 0.0;
+                    for (int j = 3; j <= 7; j += 2) {
+                        pw[j] = pw[1] * pw[j - 2] - pw[2] * pw[j - 1];
+                        pw[j + 1] = pw[1] * pw[j - 1] + pw[2] * pw[j - 2];
+                    }
+                    double sm = 0.0;
 #pragma unroll
-                for (int j = 0; j < 9; ++j) sum = sum + denex[j] * par[j];
-                if (fabs(sum) > fabs(denmax)) {
-                    denmax = sum;
-                    isave = i;
-                    tempa = sumold;
-                } else if (i == isave + 1) {
-                    tempb = sum;
-                }
-            }
-            if (isave == 0) tempa = sum;
-            if (isave == iu) tempb = denold;
+                    for (int j = 0; j < 9; ++j) sm = sm + denex[j] * pw[j];
+                    return sm;
+                },
+                [](double a, double b) { return fabs(a) > fabs(b); }, isave, denmax, tempa, tempb);
             double stp = 0.0;
             if (tempa != tempb) {
                 tempa = tempa - denmax;

@@ -2,3 +2,9 @@
 // k_fit_harmonic and k_chi2_harmonic.
 #define GPD_PART 1
 #include "gpd_kernels.hpp"
+
+namespace gpd {
+__attribute__((used)) void *const k_fit_harmonic_units[] = {
+    (void *)&k_fit_harmonic<1>, (void *)&k_fit_harmonic<2>, (void *)&k_fit_harmonic<4>,
+    (void *)&k_fit_harmonic<8>};
+}  // namespace gpd

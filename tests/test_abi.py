@@ -49,7 +49,8 @@ def test_options_api_and_no_environment(gpd):
     library imports no getenv at all, so an inherited environment cannot change its path (r5)."""
     defaults = {"mix": 1, "faint_stats": 0, "faint_side": 0, "fake_gpus": 0, "exact_g": 0,
                 "exact_waves": 0, "exact_wgt": 0, "exact_fast": 1, "exact_mcache": 1,
-                "xspin_test": 0, "units": 0, "upw": 0, "fit_lanes": 0, "cohorts": 1,
+                "xspin_test": 0, "units": 0, "upw": 0, "fit_lanes": 0, "fit_lps": 0,
+                "fit_wpb": 0, "cohorts": 1,
                 "harm_min_span": 256, "fs_cohort_mb": 4096, "moments": 0, "fit_prof": 0,
                 "sync_debug": 0}
     gpd.reset_options()

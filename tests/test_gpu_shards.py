@@ -149,17 +149,23 @@ def test_cohort_pipeline_records_bitwise(gpu, opts, faint, storage):
 
 
 def test_series_per_fit_wave_does_not_change_records(gpu, opts):
-    """The harmonic fit packs ⌈P / CUs⌉ series per wave (fit_lanes_for, gpd_engine.hip); every
-    lane runs the same arithmetic whatever its wave holds, so the records are the same bytes for
-    1, 7, 49 and 64 series per wave and for the automatic choice (C2-sized batch and a batch
-    that fills several waves per CU), the exact fallback and the π-flip re-fits included."""
+    """The harmonic fit's shape follows the batch (fit_shape, gpd_engine.hip): lanes per series
+    (1, 2, 4, 8 — the objective's harmonic slots and NEWUOA's 49-angle searches split across
+    them), series per wave and waves per workgroup.  The objective's arithmetic is canonical and
+    the split angle searches pick the sequential loop's index and values, so the records are the
+    same bytes for every shape and for the automatic choice (C2-sized batch and a batch that
+    fills several waves per CU), the exact fallback and the π-flip re-fits included."""
     for N, P in ((20_000, 32), (8_000, 700)):
         B = synth.make_batch(N, P, seed=N + P, b_range=(0.3, 5.5))  # b > 4.5: exact fallback
         args = (B["t"], B["d"], B["fc"], B["fc_of_pixel"])
-        opts("fit_lanes", 0)
+        gpu.reset_options()
         ref = gpu.fit_batch(*args, method="auto")
-        for lanes in ("1", "7", "49", "64"):
-            opts("fit_lanes", int(lanes))
+        for lps, lanes, wpb in ((1, 1, 1), (1, 7, 4), (1, 64, 1), (1, 49, 4), (2, 1, 1),
+                                (2, 32, 4), (4, 3, 2), (4, 16, 4), (8, 1, 1), (8, 8, 4),
+                                (8, 5, 3)):
+            opts("fit_lps", lps)
+            opts("fit_lanes", lanes)
+            opts("fit_wpb", wpb)
             _same(gpu.fit_batch(*args, method="auto"), ref)
         assert np.any(ref["status"] & gpu.GPD_ST_FALLBACK)
         assert np.mean((ref["status"] & gpu.GPD_ST_EXACT) == 0) > 0.5  # mostly harmonic

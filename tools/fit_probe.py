@@ -22,6 +22,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pixels", default="32,4096,12500")
     ap.add_argument("--lanes", default="0", help="option fit_lanes values (0 = automatic)")
+    ap.add_argument("--lps", default="0", help="option fit_lps values (0 = automatic)")
+    ap.add_argument("--wpb", default="0", help="option fit_wpb values (0 = automatic)")
     ap.add_argument("--samples", type=int, default=100_000)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--prof", action="store_true")
@@ -55,8 +57,12 @@ def main():
                                                G, N, fcop.data_ptr(), None, gpd.M_2PI, None,
                                                gpd.GPD_RECENTER, 60, out.data_ptr(), None, N, 0,
                                                sptr, err, len(err)), err)
-        for lanes in [int(x) for x in args.lanes.split(",")]:
+        import itertools
+        for lps, lanes, wpb in itertools.product(*[[int(x) for x in a.split(",")]
+                                                   for a in (args.lps, args.lanes, args.wpb)]):
+            gpd.set_option("fit_lps", lps)
             gpd.set_option("fit_lanes", lanes)
+            gpd.set_option("fit_wpb", wpb)
             ks = {}
             for r in range(args.reps + 2):
                 call()
@@ -65,17 +71,19 @@ def main():
                     for k, v in gpd.timings(0).items():
                         ks.setdefault(k, []).append(v)
             rec = out.cpu().numpy().tobytes()
-            line = {"P": P, "fit_lanes": lanes, "options": applied,
+            line = {"P": P, "fit_lps": lps, "fit_lanes": lanes, "fit_wpb": wpb, "options": applied,
                     "kernels_ms": {k: round(float(np.median(v)), 4) for k, v in ks.items()},
                     "records_sha": hashlib.sha256(rec).hexdigest()[:16]}
             print(json.dumps(line), flush=True)
             if args.prof:
                 gpd.set_option("fit_prof", 1)
-                print(f"--- prof P={P} fit_lanes={lanes}", file=sys.stderr, flush=True)
+                print(f"--- prof P={P} lps={lps} fit_lanes={lanes} wpb={wpb}", file=sys.stderr,
+                      flush=True)
                 call()
                 torch.cuda.synchronize(dev)
                 gpd.set_option("fit_prof", 0)
-        gpd.set_option("fit_lanes", 0)
+        gpd.reset_options()
+        gpd.options_from_env()
         del t, d, fc, fcop, out
         torch.cuda.empty_cache()
 
