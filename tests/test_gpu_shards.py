@@ -155,11 +155,13 @@ def test_series_per_fit_wave_does_not_change_records(gpu, opts):
     the split angle searches pick the sequential loop's index and values, so the records are the
     same bytes for every shape and for the automatic choice (C2-sized batch and a batch that
     fills several waves per CU), the exact fallback and the π-flip re-fits included."""
+    fallbacks = 0
     for N, P in ((20_000, 32), (8_000, 700)):
         B = synth.make_batch(N, P, seed=N + P, b_range=(0.3, 5.5))  # b > 4.5: exact fallback
         args = (B["t"], B["d"], B["fc"], B["fc_of_pixel"])
         gpu.reset_options()
         ref = gpu.fit_batch(*args, method="auto")
+        fallbacks += int(np.count_nonzero(ref["status"] & gpu.GPD_ST_FALLBACK))
         for lps, lanes, wpb in ((1, 1, 1), (1, 7, 4), (1, 64, 1), (1, 49, 4), (2, 1, 1),
                                 (2, 32, 4), (4, 3, 2), (4, 16, 4), (8, 1, 1), (8, 8, 4),
                                 (8, 5, 3)):
@@ -167,8 +169,11 @@ def test_series_per_fit_wave_does_not_change_records(gpu, opts):
             opts("fit_lanes", lanes)
             opts("fit_wpb", wpb)
             _same(gpu.fit_batch(*args, method="auto"), ref)
-        assert np.any(ref["status"] & gpu.GPD_ST_FALLBACK)
         assert np.mean((ref["status"] & gpu.GPD_ST_EXACT) == 0) > 0.5  # mostly harmonic
+    # the fallback path is part of the comparison (whether NEWUOA probes |b| > 4.5 depends on
+    # its trajectory: the 700-series batch mostly stops at maxfun below b ≈ 4.5, as the
+    # oracle's own fits do)
+    assert fallbacks > 0
 
 
 def test_faint_state_pointer_alignment(gpu):
