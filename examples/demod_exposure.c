@@ -1,8 +1,9 @@
 /*
  * Plain C host of the drop-in boundary: one GRAVITY-like exposure (32 diodes + 8 fibre-coupler
- * columns, Julia's column-major Matrix{ComplexF64} layout) fitted by ONE gpd_fit_batch call, the
- * way the Julia wrapper of INTEGRATION.md calls it through `ccall` in place of the
- * `Threads.@threads` diode loop of demodulateall (src/Modulation.jl:387-433).
+ * columns in idx() order, Julia's column-major Matrix{ComplexF64} layout) through ONE
+ * gpd_demodulateall call — demodulateall (src/Modulation.jl:344-435) as the Julia wrapper of
+ * INTEGRATION.md calls it through `ccall`: the exposure in, the 32 records and the N×40 output
+ * (demodulated diodes, FC columns as given) back.
  *
  * The synthetic series follow the reference's model d = p·a·exp(j·b·sin(ωt + ϕ)) + noise
  * (src/Modulation.jl:57-64, 122-148) with ω = M_2PI = 6.283185 (src/Modulation.jl:11) and 500 Hz
@@ -44,9 +45,8 @@ int main(int argc, char **argv) {
     }
     double *t = malloc(N * sizeof *t);
     gpd_c64 *data = malloc((size_t)N * NCOL * sizeof *data); /* column k at data + k·N */
-    gpd_c64 *out = malloc((size_t)N * NDIODE * sizeof *out);
+    gpd_c64 *out = malloc((size_t)N * NCOL * sizeof *out); /* output, N×40 like data */
     double bt[NDIODE], pt[NDIODE];
-    int32_t fc_of_pixel[NDIODE];
     gpd_param par[NDIODE];
     if (!t || !data || !out) return 4;
     for (int64_t i = 0; i < N; ++i) t[i] = (double)i * dt;
@@ -58,8 +58,8 @@ int main(int argc, char **argv) {
         }
     }
     for (int k = 0; k < NDIODE; ++k) {
-        const int g = k / 4; /* the 4 diodes of one (telescope, side) share its FC column */
-        fc_of_pixel[k] = NDIODE + g;
+        const int g = k / 4; /* the 4 diodes of one (telescope, side) share its FC column:
+                                idx(side, telescope, FC) − 1 = 32 + k ÷ 4 */
         bt[k] = 0.3 + 2.2 * urand();
         pt[k] = -3.141592653589793 + 6.283185307179586 * urand();
         const double amp = 0.5 + urand(), arg = 6.283185307179586 * urand();
@@ -73,15 +73,21 @@ int main(int argc, char **argv) {
         }
     }
     char err[512];
-    /* demodulateall(t, data; recenter=true) for the 32 diodes: fc is the whole 40-column
-     * matrix, fc_of_pixel picks each diode's FC column (0-based) */
-    const int rc = gpd_fit_batch(N, NDIODE, t, data, N, data, NCOL, N, fc_of_pixel, NULL, omega,
-                                 NULL, GPD_RECENTER, 60, par, out, N, 1, err, sizeof err);
+    /* (output, param, likelihood) = demodulateall(t, data; recenter=true) */
+    const int rc = gpd_demodulateall(N, t, data, N, NULL, NULL, GPD_RECENTER, 60, par, out, N, 1,
+                                     err, sizeof err);
     if (rc != GPD_OK) {
-        fprintf(stderr, "gpd_fit_batch: %s: %s\n", gpd_strerror(rc), err);
+        fprintf(stderr, "gpd_demodulateall: %s: %s\n", gpd_strerror(rc), err);
         return 5;
     }
     int bad = 0;
+    for (int64_t i = 0; i < (int64_t)NFC * N; ++i) { /* the FC columns pass through */
+        const gpd_c64 a = out[(int64_t)NDIODE * N + i], b = data[(int64_t)NDIODE * N + i];
+        if (a.re != b.re || a.im != b.im) {
+            fprintf(stderr, "FC column sample %lld differs in the output\n", (long long)i);
+            return 6;
+        }
+    }
     for (int k = 0; k < NDIODE; ++k) {
         const double db = fabs(par[k].b - bt[k]);
         printf("diode %2d  b %.6f (truth %.6f)  phi %+.6f  |a| %.6f  chi2 %.6e  nfev %d  status 0x%x\n",

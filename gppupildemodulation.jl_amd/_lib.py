@@ -50,7 +50,8 @@ EXPORTS = ("gpd_version", "gpd_strerror", "gpd_device_count", "gpd_fit_batch",
            "gpd_process_volt", "gpd_fit_batch_c32", "gpd_fit_batch_c32_dev", "gpd_fit_windows_c32",
            "gpd_fit_windows_c32_dev", "gpd_buildstates_dev", "gpd_release", "gpd_libm_eval",
            "gpd_mean_var_power", "gpd_build_id", "gpd_last_faint_stats", "gpd_set_option",
-           "gpd_get_option", "gpd_reset_options", "gpd_option_name")
+           "gpd_get_option", "gpd_reset_options", "gpd_option_name", "gpd_demodulateall",
+           "gpd_demodulateall_c32")
 
 
 class GpdError(RuntimeError):
@@ -125,6 +126,10 @@ def load():
     L.gpd_last_timings.restype = ctypes.c_int
     L.gpd_last_timings.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                    ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+    for name in ("gpd_demodulateall", "gpd_demodulateall_c32"):
+        getattr(L, name).restype = ctypes.c_int
+        getattr(L, name).argtypes = [I64, V, V, I64, V, V, U32, I32, V, V, I64, I32,
+                                     ctypes.c_char_p, ctypes.c_size_t]
     L.gpd_set_option.restype = ctypes.c_int
     L.gpd_set_option.argtypes = [ctypes.c_char_p, I64]
     L.gpd_get_option.restype = ctypes.c_int

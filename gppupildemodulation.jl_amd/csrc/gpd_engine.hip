@@ -6,9 +6,13 @@
 // host round trip (the harmonic → exact fallback list is consumed on device).
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
 #include <climits>
+#include <condition_variable>
+#include <functional>
 #include <cstdarg>
 #include <cstdio>
 #include <cmath>
@@ -134,6 +138,9 @@ struct DevCtx {
     char *harena = nullptr;
     size_t harena_cap = 0;
     hipStream_t hstream = nullptr;
+    // gpd_demodulateall: pinned staging of the demodulated columns (grow-only)
+    char *hpin = nullptr;
+    size_t hpin_cap = 0;
     // the last fit call's faint statistics in the workspace (gpd_last_faint_stats; tests)
     const double *last_fstat = nullptr;
     long long last_fstat_P = 0;
@@ -368,6 +375,92 @@ hipError_t run_faint_onepass(const Problem &pb, double *fstat, double *scr, doub
     return hipGetLastError();
 }
 
+// Host copy workers (gpd_demodulateall): a persistent pool that spreads host copies — and the
+// first touch of the caller's fresh output pages, which dominates them — over threads.  At most
+// 16 threads (the CPU share of one GPU on the MI355X boxes), fewer if the process may run on
+// fewer CPUs.  run(n, fn) calls fn(0..n-1) on the pool's threads and the caller's, returns when
+// all are done; one job at a time.  Leaked on purpose (no join during static destruction).
+class HostPool {
+  public:
+    static HostPool &get() {
+        static HostPool *p = new HostPool();
+        return *p;
+    }
+    int size() const { return n_; }
+    void run(int n, const std::function<void(int)> &fn) {
+        std::lock_guard<std::mutex> one(run_mu_);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            job_ = &fn;
+            njob_ = n;
+            next_.store(0);
+            acked_ = 0;
+            ++gen_;
+        }
+        cv_.notify_all();
+        work(fn, n);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return acked_ == n_ - 1; });  // every worker is done with this job
+    }
+
+  private:
+    HostPool() {
+        int ncpu = 8;
+        cpu_set_t cs;
+        if (sched_getaffinity(0, sizeof cs, &cs) == 0) ncpu = CPU_COUNT(&cs);
+        n_ = std::max(1, std::min(16, ncpu));
+        for (int i = 1; i < n_; ++i) th_.emplace_back([this] { loop(); });
+    }
+    void work(const std::function<void(int)> &fn, int n) {
+        for (int i; (i = next_.fetch_add(1)) < n;) fn(i);
+    }
+    void loop() {
+        unsigned long seen = 0;
+        for (;;) {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [&] { return gen_ != seen; });
+            seen = gen_;
+            const std::function<void(int)> *fn = job_;
+            const int n = njob_;
+            lk.unlock();
+            work(*fn, n);
+            lk.lock();
+            if (++acked_ == n_ - 1) done_.notify_all();
+        }
+    }
+    int n_ = 1;
+    std::vector<std::thread> th_;
+    std::mutex mu_, run_mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)> *job_ = nullptr;
+    int njob_ = 0, acked_ = 0;
+    unsigned long gen_ = 0;
+    std::atomic<int> next_{0};
+};
+
+// Copy ncols columns of rows elements (src: element size ses, leading dimension sld; dst: des,
+// dld) with the host pool, in pieces of about 1 MB; ses == des copies, ses = 16 → des = 8
+// rounds ComplexF64 to ComplexF32 (Complex{Float32}.(…): each part rounded to nearest).
+void pool_copy_cols(char *dst, size_t des, int64_t dld, const char *src, size_t ses, int64_t sld,
+                    int64_t rows, int64_t ncols) {
+    const int64_t per = std::max<int64_t>(1, (int64_t)(1 << 20) / (int64_t)ses);  // rows per piece
+    const int64_t pieces_per_col = (rows + per - 1) / per;
+    const int64_t npieces = pieces_per_col * ncols;
+    HostPool::get().run((int)npieces, [&](int i) {
+        const int64_t c = i / pieces_per_col, r0 = (i % pieces_per_col) * per;
+        const int64_t nr = std::min(per, rows - r0);
+        const char *s = src + ((size_t)c * sld + r0) * ses;
+        char *d = dst + ((size_t)c * dld + r0) * des;
+        if (ses == des) {
+            std::memcpy(d, s, (size_t)nr * ses);
+        } else {
+            const double *sv = (const double *)s;
+            float *dv = (float *)d;
+            for (int64_t k = 0; k < 2 * nr; ++k) dv[k] = (float)sv[k];
+        }
+    });
+}
+
 const char *kErrStr[] = {"ok", "invalid argument", "HIP runtime error", "no HIP device",
                          "out of device memory", "harmonic method unsafe for these timestamps"};
 
@@ -428,8 +521,10 @@ int gpd_release(int device) {
     if (cx->done) (void)hipEventSynchronize(cx->done);
     (void)hipFree(cx->ws);
     (void)hipFree(cx->harena);
+    (void)hipHostFree(cx->hpin);
     cx->ws = cx->harena = nullptr;
-    cx->ws_cap = cx->harena_cap = 0;
+    cx->hpin = nullptr;
+    cx->ws_cap = cx->harena_cap = cx->hpin_cap = 0;
     cx->last_fstat = nullptr;  // pointed into the freed workspace (advisor r4)
     cx->last_fstat_P = 0;
     return GPD_OK;
@@ -1209,7 +1304,11 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
                       const int32_t *fc_of_pixel, const int8_t *state, double omega,
                       const double *xinit, uint32_t flags, int32_t maxfun, gpd_param *out_params,
                       gpd_c64 *out_demod, int64_t ldo, const double *bphi, int32_t n_gpus,
-                      char *errbuf, size_t errlen, int64_t window = 0, bool is_c32 = false) {
+                      char *errbuf, size_t errlen, int64_t window = 0, bool is_c32 = false,
+                      int out_kind = 0) {
+    // out_kind: 0 — out_demod receives ComplexF64 columns straight from the device (pageable
+    // copy); 1 — through the device's pinned staging buffer and the host pool (ComplexF64);
+    // 2 — the same, rounded to ComplexF32 (out_demod then points to gpd_c32 columns)
     const size_t esz = is_c32 ? sizeof(gpd_c32) : sizeof(gpd_c64);  // stored element bytes
     const char *d = (const char *)d_, *fc = (const char *)fc_;
     if (n_samples < 2 || n_pixels < 1 || !t || !d || !fc || !fc_of_pixel || !out_params ||
@@ -1347,10 +1446,35 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
         }
         ok = chk(hipMemcpyAsync(out_params + o0, dpar, nrec * sizeof(Param), hipMemcpyDeviceToHost, s),
                  "D2H params") &&
-             (!out_demod || chk(hipMemcpy2DAsync(out_demod + p0 * ldo + s0, ldo * sizeof(gpd_c64), dout,
-                                                 N * sizeof(c64), N * sizeof(c64), P,
-                                                 hipMemcpyDeviceToHost, s), "D2H out")) &&
-             chk(hipStreamSynchronize(s), "hipStreamSynchronize");
+             (!out_demod || out_kind != 0 ||
+              chk(hipMemcpy2DAsync(out_demod + p0 * ldo + s0, ldo * sizeof(gpd_c64), dout,
+                                   N * sizeof(c64), N * sizeof(c64), P,
+                                   hipMemcpyDeviceToHost, s), "D2H out"));
+        if (ok && out_demod && out_kind != 0) {
+            // staged: one DMA of the P×N demodulated columns into pinned memory, then the host
+            // pool copies them into the caller's columns (ldo), rounding to ComplexF32 for kind 2
+            const size_t bytes = (size_t)P * N * sizeof(c64);
+            if (cx->hpin_cap < bytes) {
+                ok = chk(hipStreamSynchronize(s), "hipStreamSynchronize");
+                if (ok) {
+                    (void)hipHostFree(cx->hpin);
+                    cx->hpin = nullptr;
+                    cx->hpin_cap = 0;
+                    ok = chk(hipHostMalloc((void **)&cx->hpin, bytes, hipHostMallocDefault),
+                             "hipHostMalloc (output staging)");
+                    if (ok) cx->hpin_cap = bytes;
+                }
+            }
+            ok = ok && chk(hipMemcpyAsync(cx->hpin, dout, bytes, hipMemcpyDeviceToHost, s),
+                           "D2H out (staged)") &&
+                 chk(hipStreamSynchronize(s), "hipStreamSynchronize");
+            if (ok) {
+                const size_t des = out_kind == 2 ? sizeof(gpd_c32) : sizeof(gpd_c64);
+                pool_copy_cols((char *)out_demod + ((size_t)p0 * ldo + s0) * des, des, ldo,
+                               cx->hpin, sizeof(c64), N, N, P);
+            }
+        }
+        ok = ok && chk(hipStreamSynchronize(s), "hipStreamSynchronize");
         cleanup();
         if (!ok) return fail(GPD_E_HIP);
     };
@@ -1370,7 +1494,52 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
     return GPD_OK;
 }
 
+// demodulateall over the N×40 idx()-ordered exposure (gpd_demodulateall): the 32 diodes fitted
+// by host_batch with the FC columns 32..39 of the same matrix, their demodulated columns staged
+// into `output`, and the FC columns copied into `output` by the host pool while the device
+// computes (what `output = copy(data)` leaves there, src/Modulation.jl:353).
+static int host_demodulateall(int64_t N, const double *t, const void *data, int64_t ldd,
+                              bool c32, const int8_t *state, const double *xinit, uint32_t flags,
+                              int32_t maxfun, gpd_param *params, void *output, int64_t ldo,
+                              int32_t n_gpus, char *errbuf, size_t errlen) {
+    if (N < 2 || !t || !data || !params || !output || ldd < N || ldo < N) {
+        set_err(errbuf, errlen, "gpd_demodulateall: invalid shapes/pointers (N=%lld)",
+                (long long)N);
+        return GPD_E_ARG;
+    }
+    const size_t esz = c32 ? sizeof(gpd_c32) : sizeof(gpd_c64);
+    // 0-based FC column of diode c among the 8 FC columns: idx(side, telescope, FC) − 33 with
+    // side FT for c < 16, SC otherwise, telescope = (c mod 16) ÷ 4 + 1 (src/Modulation.jl:17-22,388)
+    int32_t fcop[32];
+    for (int c = 0; c < 32; ++c) fcop[c] = (c < 16 ? 0 : 4) + (c % 16) / 4;
+    const char *fc = (const char *)data + (size_t)32 * ldd * esz;
+    std::thread fcopy([&] {
+        pool_copy_cols((char *)output + (size_t)32 * ldo * esz, esz, ldo, fc, esz, ldd, N, 8);
+    });
+    const int r = host_batch(N, 32, t, data, ldd, fc, 8, ldd, fcop, state, 6.283185, xinit, flags,
+                             maxfun, params, (gpd_c64 *)output, ldo, nullptr, n_gpus, errbuf,
+                             errlen, 0, c32, c32 ? 2 : 1);
+    fcopy.join();
+    return r;
+}
+
 extern "C" {
+
+int gpd_demodulateall(int64_t n_samples, const double *t, const gpd_c64 *data, int64_t ldd,
+                      const int8_t *state, const double *xinit, uint32_t flags, int32_t maxfun,
+                      gpd_param *params, gpd_c64 *output, int64_t ldo, int32_t n_gpus,
+                      char *errbuf, size_t errlen) {
+    return host_demodulateall(n_samples, t, data, ldd, false, state, xinit, flags, maxfun, params,
+                              output, ldo, n_gpus, errbuf, errlen);
+}
+
+int gpd_demodulateall_c32(int64_t n_samples, const double *t, const gpd_c32 *data, int64_t ldd,
+                          const int8_t *state, const double *xinit, uint32_t flags,
+                          int32_t maxfun, gpd_param *params, gpd_c32 *output, int64_t ldo,
+                          int32_t n_gpus, char *errbuf, size_t errlen) {
+    return host_demodulateall(n_samples, t, data, ldd, true, state, xinit, flags, maxfun, params,
+                              output, ldo, n_gpus, errbuf, errlen);
+}
 
 int gpd_fit_batch(int64_t n_samples, int64_t n_pixels, const double *t, const gpd_c64 *d,
                   int64_t ldd, const gpd_c64 *fc, int64_t n_fc, int64_t ldfc,

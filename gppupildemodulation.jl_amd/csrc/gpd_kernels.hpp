@@ -185,9 +185,19 @@ __device__ __forceinline__ void drive_fit(F &f, const Problem &pb, double (&x)[2
         x[1] = pb.x1;
     } else {
         double fg[8];
-        for (int k = 0; k < 8; ++k) {
-            double xx[2] = {0.1, c_phi_grid[k]};
-            fg[k] = f(xx);
+        if constexpr (has_multi<F>::value) {  // the 8 grid points at once (same values)
+            double pts[8][2];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                pts[k][0] = 0.1;
+                pts[k][1] = c_phi_grid[k];
+            }
+            f.template multi<8>(pts, fg);
+        } else {
+            for (int k = 0; k < 8; ++k) {
+                double xx[2] = {0.1, c_phi_grid[k]};
+                fg[k] = f(xx);
+            }
         }
         int best = 0;  // findmin: first NaN wins, else first minimum
 #pragma unroll
@@ -210,10 +220,19 @@ __device__ __forceinline__ void drive_fit(F &f, const Problem &pb, double (&x)[2
         const int nf = nw.run(x, 1.0, 1e-3, pb.maxfun, f, fx);
         if (nf >= pb.maxfun) status |= ST_MAXFUN;
         if (pass > 0) break;
-        const double lklval = f(x);
         const double php = x[1] + (x[1] < 0 ? PI_F64 : -PI_F64);
-        double xf[2] = {x[0], php};
-        if (!(lklval > f(xf))) break;  // "bad minima" (src/Modulation.jl:411-414)
+        double lklval, lflip;
+        if constexpr (has_multi<F>::value) {  // lkl(x) and lkl(x[1], ϕπ) at once
+            double pts[2][2] = {{x[0], x[1]}, {x[0], php}}, v[2];
+            f.template multi<2>(pts, v);
+            lklval = v[0];
+            lflip = v[1];
+        } else {
+            lklval = f(x);
+            double xf[2] = {x[0], php};
+            lflip = f(xf);
+        }
+        if (!(lklval > lflip)) break;  // "bad minima" (src/Modulation.jl:411-414)
         status |= ST_REFIT;
         x[1] = php;
     }
@@ -2137,7 +2156,7 @@ __global__ __launch_bounds__(256) void k_moments_win(Problem pb, const double *_
 template <int LPS>
 struct HarmChi2 {
     static_assert(LPS == 1 || LPS == 2 || LPS == 4 || LPS == 8, "lanes per series");
-    static constexpr int NS = 8 / LPS;  // slots per lane
+    static constexpr bool kMulti = LPS > 1;  // independent points in parallel (has_multi)
     const double *__restrict__ mom;
     long long P, k;
     double nvalid, W2, DEN, tailref, qbase, phimax;
@@ -2159,9 +2178,12 @@ struct HarmChi2 {
 
     // Σ_n J_n(b) e^{-jnϕ} M_n for moments M in the layout of k_moments (F0 re/im at rows 0-1,
     // (A,B,C,D)_n at rows 3+4(n-1)..), canonical order (above)
+    template <int LPS_ = LPS>
     __device__ __forceinline__ void combine(const double *__restrict__ m_, long long ld, long long col,
                                             const double (&J)[KH + 2], double cph, double sph,
                                             double &Sr, double &Si) const {
+        constexpr int L = LPS_;  // lanes evaluating this χ² (1: one lane alone)
+        constexpr int NS = 8 / L;
         gdouble *p = (gdouble *)m_ + col;  // row q of this series at p[q·ld]
         double c[9], s[9];
         c[1] = cph;
@@ -2175,19 +2197,19 @@ struct HarmChi2 {
         double vr[NS], vi[NS];
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
-            // slot j's angle components and Bessel factors: compile-time for LPS = 1; for LPS > 1
+            // slot j's angle components and Bessel factors: compile-time for L = 1; for L > 1
             // the slot depends on the lane — captured by compare-and-select against every
             // candidate (no register array indexed at run time, which would go through scratch)
             int m;
             double cn, sn, jq[3];
-            if constexpr (LPS == 1) {
+            if constexpr (L == 1) {
                 m = j + 1;
                 cn = c[m];
                 sn = s[m];
 #pragma unroll
                 for (int q = 0; q < 3; ++q) jq[q] = J[m + 8 * q];
             } else {
-                m = r + LPS * j + 1;
+                m = r + L * j + 1;
                 cn = c[1];
                 sn = s[1];
 #pragma unroll
@@ -2235,27 +2257,27 @@ struct HarmChi2 {
         }
         // the butterfly over the 8 slots: distance 4, 2, 1 (in-lane while the distance spans
         // this lane's slots, then across the group's lanes)
-        if constexpr (LPS <= 4) {
+        if constexpr (L <= 4) {
 #pragma unroll
-            for (int j = 0; j < 4 / LPS; ++j) {
-                vr[j] = vr[j] + vr[j + 4 / LPS];
-                vi[j] = vi[j] + vi[j + 4 / LPS];
+            for (int j = 0; j < 4 / L; ++j) {
+                vr[j] = vr[j] + vr[j + 4 / L];
+                vi[j] = vi[j] + vi[j + 4 / L];
             }
         } else {
             vr[0] = vr[0] + lane_xor<4>(vr[0]);
             vi[0] = vi[0] + lane_xor<4>(vi[0]);
         }
-        if constexpr (LPS <= 2) {
+        if constexpr (L <= 2) {
 #pragma unroll
-            for (int j = 0; j < 2 / LPS; ++j) {
-                vr[j] = vr[j] + vr[j + 2 / LPS];
-                vi[j] = vi[j] + vi[j + 2 / LPS];
+            for (int j = 0; j < 2 / L; ++j) {
+                vr[j] = vr[j] + vr[j + 2 / L];
+                vi[j] = vi[j] + vi[j + 2 / L];
             }
         } else {
             vr[0] = vr[0] + lane_xor<2>(vr[0]);
             vi[0] = vi[0] + lane_xor<2>(vi[0]);
         }
-        if constexpr (LPS == 1) {
+        if constexpr (L == 1) {
             vr[0] = vr[0] + vr[1];
             vi[0] = vi[0] + vi[1];
         } else {
@@ -2277,7 +2299,7 @@ struct HarmChi2 {
     __device__ GPD_FIT_OBJ_ATTR double operator()(const double (&x)[2]) {
         // one inlined copy of eval (the cycle split only brackets it)
         const unsigned long long t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
-        const double v = eval(x);
+        const double v = eval<LPS>(x);
         if (prof) {
             const unsigned long long dt = __builtin_amdgcn_s_memtime() - t0;
             prof_cycles += dt;
@@ -2285,6 +2307,41 @@ struct HarmChi2 {
         }
         return v;
     }
+    // the same χ² evaluated by this lane alone (LPS = 1 form of the canonical arithmetic)
+    __device__ GPD_FIT_OBJ_ATTR double single(const double (&x)[2]) { return eval<1>(x); }
+    // NP independent points: lane r of the group evaluates points r, r + LPS, … alone; every
+    // lane then holds every value (shuffled from its owner), nfev counts NP evaluations and a
+    // fallback anywhere in the group is the group's
+    template <int NP>
+    __device__ __forceinline__ void multi(const double (&pts)[NP][2], double (&vals)[NP]) {
+        constexpr int R = (NP + LPS - 1) / LPS;
+        const int nf0 = nfev;
+        double mine[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const int pi = q * LPS + r;
+            mine[q] = 0.0;
+            if (pi < NP) {
+                double xx[2] = {pts[q * LPS][0], pts[q * LPS][1]};
+#pragma unroll
+                for (int u = 1; u < LPS; ++u) {
+                    if (q * LPS + u < NP) {
+                        const bool hit = r == u;
+                        xx[0] = hit ? pts[q * LPS + u][0] : xx[0];
+                        xx[1] = hit ? pts[q * LPS + u][1] : xx[1];
+                    }
+                }
+                mine[q] = single(xx);
+            }
+        }
+        const int base = ((int)threadIdx.x & 63) & ~(LPS - 1);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) vals[p] = __shfl(mine[p / LPS], base + p % LPS, 64);
+        const unsigned long long bal = __ballot(fallback);
+        fallback = ((bal >> base) & ((1ull << LPS) - 1)) != 0;
+        nfev = nf0 + NP;
+    }
+    template <int LPS_ = LPS>
     __device__ __forceinline__ double eval(const double (&x)[2]) {
         ++nfev;
         if (fallback) return 0.0;
@@ -2306,12 +2363,12 @@ struct HarmChi2 {
         double sph, cph;
         jl_sincos(phi, &sph, &cph);
         double Sr, Si;  // S = Σ w m̄ d
-        combine(mom, P, k, J, cph, sph, Sr, Si);
+        combine<LPS_>(mom, P, k, J, cph, sph, Sr, Si);
         if (offs) {
             // [Σw  Σw m; Σw m̄  Σw|m|²] [c; a] = [Σw d; Σw m̄ d], StaticArrays 2×2 solve as in the
             // exact evaluator; Nχ² = Σw|d|² − Re(c̄ Σw d + ā S) at the solution
             double Gr, Gi;  // Gm = Σ w m̄ = Σ w p̄ e^{-jβ}
-            combine(momG, PG, g, J, cph, sph, Gr, Gi);
+            combine<LPS_>(momG, PG, g, J, cph, sph, Gr, Gi);
             const c64 A11 = {W0, 0.0}, A12 = {Gr, -Gi}, A21 = {Gr, Gi}, A22 = {DEN, 0.0};
             const c64 b1 = {D0r, D0i}, b2 = {Sr, Si};
             const c64 t1 = cmul(A11, A22), t2 = cmul(A12, A21);

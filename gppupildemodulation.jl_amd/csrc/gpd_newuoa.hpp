@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <type_traits>
+
 #include "gpd_jlmath.h"  // OptimPackNextGen is pure Julia: Julia Base cos/sin
 
 namespace gpd {
@@ -66,6 +68,15 @@ GPD_HD void wrc(double (&a)[R][C], int r, int c, double v) {
     for (int j = 0; j < C; ++j)
         if (c == j) a[r][j] = v;
 }
+
+// has_multi<F>: the objective F can evaluate NP independent points at once
+// (f.template multi<NP>(pts, vals), every lane of the fit getting every value) — the harmonic
+// fit's lane groups evaluate them in parallel, each point by one lane with the canonical
+// objective's single-lane form (the same bits as one at a time)
+template <class F, class = void>
+struct has_multi : std::false_type {};
+template <class F>
+struct has_multi<F, std::void_t<decltype(F::kMulti)>> : std::integral_constant<bool, F::kMulti> {};
 
 constexpr double kTwoPi = 6.283185307179586476925286766559;  // 8·atan(1)
 // cos/sin of the fixed trial angles i·dang, dang = kTwoPi/50, of the three angle searches
@@ -933,6 +944,29 @@ struct Newuoa {
         const double reciq = sqrt(0.5) / rhosq;
         double f = 0.0, fbeg = 0.0, fopt = 0.0;
         int kopt = 1;
+        // NPT ≤ 2N + 1: the initial points x_nf = xbase ± rhobeg·e_j depend on no f value, so an
+        // objective with has_multi evaluates all NPT of them at once (the same points, each
+        // x_j = xpt_j + xbase_j as the loop below forms it, the same values)
+        double fpre[NPT];
+        bool pre = false;
+        if constexpr (has_multi<F>::value && NPT <= 2 * N + 1) {
+            if (nftest >= NPT) {
+                double pts[NPT][2];
+#pragma unroll
+                for (int nf = 1; nf <= NPT; ++nf) {
+                    const int nfm = nf - 1;
+#pragma unroll
+                    for (int j = 0; j < N; ++j) {
+                        double v = 0.0;
+                        if (nfm >= 1 && nfm <= N && j == nfm - 1) v = rhobeg;
+                        if (nfm > N && j == nfm - N - 1) v = -rhobeg;
+                        pts[nf - 1][j] = v + xbase[j];
+                    }
+                }
+                fun.template multi<NPT>(pts, fpre);
+                pre = true;
+            }
+        }
 
         // ---------------------------------------- initial interpolation set (NPT points)
         for (int nf = 1; nf <= NPT; ++nf) {
@@ -977,7 +1011,7 @@ struct Newuoa {
                 fx = f;
                 return nf - 1;
             }
-            f = fun(x);
+            f = pre ? fpre[nf - 1] : fun(x);
             wr_(fval, nf - 1, f);
             if (nf == 1) {
                 fbeg = f;

@@ -277,9 +277,12 @@ def demodulateall(timestamp, data, *, init="auto", recenter=True, faintparam=Non
 
     timestamp: (N,) float; data: (N, 40) complex (columns in idx() order, 1..32 diodes,
     33..40 FC).  Returns (output (N, 40) complex, param: list of 32 Modulation records,
-    likelihood: (32,) float).
+    likelihood: (32,) float).  One gpd_demodulateall call: the library fills a fresh
+    column-major output (the demodulated diodes and the FC columns as given), so no host copy
+    of the exposure runs here.  `data` column-major (np.asfortranarray, a Julia Matrix's
+    layout) is passed without a copy; a row-major array is converted first.
     """
-    t = np.asarray(timestamp, dtype=np.float64)
+    t = np.ascontiguousarray(timestamp, dtype=np.float64)
     data = np.asarray(data)
     if not np.iscomplexobj(data):
         raise TypeError("data must be a complex matrix (AbstractMatrix{Complex{T}})")
@@ -292,7 +295,7 @@ def demodulateall(timestamp, data, *, init="auto", recenter=True, faintparam=Non
         raise ValueError("voltage and time must have the same number of lines")
     # (40, N): column k contiguous, like Julia's Matrix (no copy when `data` is column-major,
     # np.asfortranarray — the layout a Julia caller hands over)
-    cols = np.ascontiguousarray(data.T)
+    cols = np.ascontiguousarray(data.T)  # (40, N): no copy when data is column-major
     state = None
     if faintparam is not None:
         if isinstance(faintparam, FaintStates):
@@ -302,22 +305,23 @@ def demodulateall(timestamp, data, *, init="auto", recenter=True, faintparam=Non
             state = np.asarray(faintparam, dtype=np.int8)
             if state.shape != (N,):
                 raise ValueError("faintparam must have one MetState per sample")
+        state = np.ascontiguousarray(state, dtype=np.int8)
     xinit = None
     if not (isinstance(init, str) and init == "auto"):
-        xinit = np.asarray(init, dtype=np.float64)
-    fop = np.array([fc_column_of(c) - 1 for c in range(1, 33)], dtype=np.int32)
-    # output = copy(data): FC columns pass through, eltype of data (src/Modulation.jl:353).  For
-    # complex128 data the library writes the demodulated diodes into its columns 1..32 in place
-    # (one device-to-host copy into memory the copy has touched); complex64 data takes the
-    # Float64 result through a separate array, converted to the data's element type
-    out_cols = cols.copy()
-    inplace = out_cols.dtype == np.complex128
-    params, out = fit_batch(t, cols[:32], cols, fop, state=state, xinit=xinit, recenter=recenter,
-                            fitoffsets=fitoffsets, onlyhigh=onlyhigh, want_output=True,
-                            method=method, n_gpus=n_gpus,
-                            out=out_cols[:32] if inplace else None)
-    if not inplace:
-        out_cols[:32] = out
+        xinit = np.ascontiguousarray(init, dtype=np.float64)
+        if xinit.shape != (2,):
+            raise ValueError("init must be a 2-vector [b, ϕ]")
+    flags = _method_flags(method) | (GPD_RECENTER if recenter else 0) | \
+        (GPD_FIT_OFFSETS if fitoffsets else 0) | (GPD_ONLY_HIGH if onlyhigh else 0)
+    # output = copy(data) with the diodes demodulated (src/Modulation.jl:353, 417-425): a fresh
+    # column-major (N, 40) array of data's element type, every column written by the library
+    out_cols = np.empty((40, N), dtype=cols.dtype)
+    params = np.zeros(32, dtype=PARAM_DTYPE)
+    err = ctypes.create_string_buffer(512)
+    L = load()
+    fn = L.gpd_demodulateall_c32 if cols.dtype == np.complex64 else L.gpd_demodulateall
+    check(fn(N, ptr(t), ptr(cols), N, ptr(state), ptr(xinit), flags, 60, ptr(params),
+             ptr(out_cols), N, int(n_gpus), err, len(err)), err)
     output = out_cols.T  # (N, 40), column-major like the Julia Matrix
     param = []
     for p in params:

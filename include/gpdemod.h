@@ -114,6 +114,34 @@ void gpd_reset_options(void);
 const char *gpd_option_name(int index);
 
 /*
+ * demodulateall itself (src/Modulation.jl:344-435) on the library's side of the boundary: the
+ * exposure as the reference takes it and returns it.
+ *   data, ldd        the N×40 column-major matrix in idx() order (src/Modulation.jl:17-22):
+ *                    columns 0..31 the diodes, 32..39 the fibre couplers; ldd ≥ n_samples
+ *   t, state, xinit, flags, maxfun   as gpd_fit_batch (ω = M_2PI = 6.283185, src/Modulation.jl:11,399)
+ *   params[32]       the 32 diodes' records in idx() order (param, likelihood)
+ *   output, ldo      a second N×40 matrix (ldo ≥ n_samples) that receives what
+ *                    `output = copy(data)` and the diode loop leave in it (:353, :417-425):
+ *                    columns 0..31 the demodulated diodes, 32..39 the FC columns as given.
+ *                    The caller allocates it (Julia `similar(data)`) and need not touch it:
+ *                    the library fills every column — the demodulated ones through a pinned
+ *                    staging buffer and parallel host copies, the FC ones copied while the
+ *                    device computes — so no `copy(data)` of the exposure runs on the caller's
+ *                    side and the first touch of the fresh pages is spread over threads.
+ *   n_gpus           devices (as gpd_fit_batch; one exposure runs on one)
+ * _c32: ComplexF32 data and output (the FITS VOLT precision; Float64 arithmetic, the
+ * demodulated columns rounded to Float32 as Complex{Float32}.(…) does).
+ */
+int gpd_demodulateall(int64_t n_samples, const double *t, const gpd_c64 *data, int64_t ldd,
+                      const int8_t *state, const double *xinit, uint32_t flags, int32_t maxfun,
+                      gpd_param *params, gpd_c64 *output, int64_t ldo, int32_t n_gpus,
+                      char *errbuf, size_t errlen);
+int gpd_demodulateall_c32(int64_t n_samples, const double *t, const gpd_c32 *data, int64_t ldd,
+                          const int8_t *state, const double *xinit, uint32_t flags,
+                          int32_t maxfun, gpd_param *params, gpd_c32 *output, int64_t ldo,
+                          int32_t n_gpus, char *errbuf, size_t errlen);
+
+/*
  * Fit (and optionally demodulate) a batch of series.  Replaces the diode loop of
  * demodulateall (src/Modulation.jl:387-433): per series, the FC phasor
  * exp(im·angle(fc)) (:388), faint power/weight (:391-396, src/Faint.jl:89-100), the 8-point

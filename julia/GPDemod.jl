@@ -103,47 +103,42 @@ function demodulateall_gpu(timestamp::AbstractVector, data::AbstractMatrix{Compl
     length(timestamp) == N || error("voltage and time must have the same number of lines")
     t = Vector{Float64}(timestamp)
     c32 = T === Float32
-    # column k = diode k; a Matrix already in the library's element type is passed as it is
-    # (no conversion copy of the 64 MB exposure)
+    # the exposure as it is (no conversion copy when it already is a Matrix of the library's
+    # element type); ComplexF32 stays Float32 in device memory
     d = c32 ? (data isa Matrix{ComplexF32} ? data : Matrix{ComplexF32}(data)) :
               (data isa Matrix{ComplexF64} ? data : Matrix{ComplexF64}(data))
     state = faint_state_vector(faintparam, t, preswitchdelay, postwitchdelay)
-    fcop = fc_columns()
     flags = UInt32((recenter ? GPD_RECENTER : 0) | (fitoffsets ? GPD_FIT_OFFSETS : 0) |
                    (onlyhigh ? GPD_ONLY_HIGH : 0) | method_flags(method))
     xinit = init isa Symbol ? C_NULL : Vector{Float64}(init)
     params = Vector{GpdParam}(undef, 32)
-    # the reference's output = copy(data) (src/Modulation.jl:353): FC columns 33..40 pass
-    # through.  For ComplexF64 data the library writes the demodulated diodes straight into its
-    # columns 1..32 (out_demod = output, ldo = N): one copy of the exposure into memory that
-    # copy() has already touched, instead of a fresh matrix (page faults on the device-to-host
-    # copy) plus a second copy; ComplexF32 data takes the Float64 result through `demod`.
-    output = copy(data)
-    inplace = !c32 && output isa Matrix{ComplexF64}
-    demod = inplace ? output : Matrix{ComplexF64}(undef, N, 32)
+    # the reference's `output = copy(data)` then the diode loop (src/Modulation.jl:353,
+    # 417-425): one call fills a fresh matrix — the 32 demodulated diodes and the FC columns
+    # 33..40 as given — so the exposure is never copied on this side; ComplexF32 data gets a
+    # ComplexF32 output (Complex{T}.(…) of the Float64 results)
+    output = similar(d)
     err = zeros(UInt8, 512)
-    GC.@preserve t d state xinit params demod err begin
+    GC.@preserve t d state xinit params output err begin
         if c32
-            rc = ccall((:gpd_fit_batch_c32, libgpdemod), Cint,
-                       (Int64, Int64, Ptr{Float64}, Ptr{ComplexF32}, Int64, Ptr{ComplexF32}, Int64,
-                        Int64, Ptr{Int32}, Ptr{Int8}, Float64, Ptr{Float64}, UInt32, Int32,
-                        Ptr{GpdParam}, Ptr{ComplexF64}, Int64, Int32, Ptr{UInt8}, Csize_t),
-                       N, 32, t, d, N, d, 40, N, fcop, state, M_2PI, xinit, flags, 60, params,
-                       demod, N, n_gpus, err, length(err))
+            rc = ccall((:gpd_demodulateall_c32, libgpdemod), Cint,
+                       (Int64, Ptr{Float64}, Ptr{ComplexF32}, Int64, Ptr{Int8}, Ptr{Float64},
+                        UInt32, Int32, Ptr{GpdParam}, Ptr{ComplexF32}, Int64, Int32, Ptr{UInt8},
+                        Csize_t),
+                       N, t, d, N, state, xinit, flags, 60, params, output, N, n_gpus, err,
+                       length(err))
         else
-            rc = ccall((:gpd_fit_batch, libgpdemod), Cint,
-                       (Int64, Int64, Ptr{Float64}, Ptr{ComplexF64}, Int64, Ptr{ComplexF64}, Int64,
-                        Int64, Ptr{Int32}, Ptr{Int8}, Float64, Ptr{Float64}, UInt32, Int32,
-                        Ptr{GpdParam}, Ptr{ComplexF64}, Int64, Int32, Ptr{UInt8}, Csize_t),
-                       N, 32, t, d, N, d, 40, N, fcop, state, M_2PI, xinit, flags, 60, params,
-                       demod, N, n_gpus, err, length(err))
+            rc = ccall((:gpd_demodulateall, libgpdemod), Cint,
+                       (Int64, Ptr{Float64}, Ptr{ComplexF64}, Int64, Ptr{Int8}, Ptr{Float64},
+                        UInt32, Int32, Ptr{GpdParam}, Ptr{ComplexF64}, Int64, Int32, Ptr{UInt8},
+                        Csize_t),
+                       N, t, d, N, state, xinit, flags, 60, params, output, N, n_gpus, err,
+                       length(err))
         end
         gpd_assert_ok(rc, err)
     end
-    # the reference's return types (src/Modulation.jl:353-359, 434): output keeps
-    # Matrix{Complex{T}}, param::Vector{Modulation…{T}}, likelihood::Vector{T}; the library's
-    # Float64 results are converted to T
-    inplace || (output[:, 1:32] .= Complex{T}.(demod))
+    # the reference's return types (src/Modulation.jl:353-359, 434): output::Matrix{Complex{T}},
+    # param::Vector{Modulation…{T}}, likelihood::Vector{T}; the library's Float64 records are
+    # converted to T
     param = fitoffsets ?
         ModulationWithOffsets{T}[ModulationWithOffsets{T}(p.c, p.a, p.b, p.ϕ, M_2PI) for p in params] :
         ModulationNoOffsets{T}[ModulationNoOffsets{T}(p.a, p.b, p.ϕ, M_2PI) for p in params]

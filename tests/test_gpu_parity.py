@@ -374,6 +374,62 @@ def test_demodulateall_one_exposure_full_size(gpu, oracle):
     assert np.max(np.abs(output[:, :32][:, same] - refout[same].T)) <= 1e-9 * np.abs(data).max()
 
 
+def _exposure_matrix(gpu, B, order="F", dtype=np.complex128):
+    """The N×40 idx()-ordered exposure of a 32-series synthetic batch (FC group g of the batch in
+    the idx() FC column of its diodes)."""
+    N = B["t"].size
+    data = np.empty((N, 40), dtype=dtype, order=order)
+    data[:, :32] = B["d"].T
+    fop = np.array([gpu.fc_column_of(c) - 1 for c in range(1, 33)])
+    for g in range(8):
+        cols = np.nonzero(fop == 32 + g)[0]
+        data[:, 32 + g] = B["fc"][B["fc_of_pixel"][cols[0]]]
+    return data, fop
+
+
+@pytest.mark.parametrize("dtype", [np.complex128, np.complex64])
+@pytest.mark.parametrize("faint,fitoffsets", [(False, False), (True, False), (False, True)])
+def test_demodulateall_entry_point(gpu, oracle, dtype, faint, fitoffsets):
+    """gpd_demodulateall (the reference's demodulateall on the library's side, r5): the N×40
+    exposure in, a fresh N×40 output filled by the library — the demodulated diodes through the
+    pinned staging and the host pool, the FC columns copied as given — equals, bit for bit, what
+    the reference's steps give from the batch entry point: output = copy(data) (:353) with the
+    diode columns replaced by gpd_fit_batch's demodulated series (ComplexF32 data: rounded to
+    ComplexF32, Complex{T}.(…)); the records too.  Also with leading dimensions beyond N."""
+    import ctypes
+    N = 7000
+    B = synth.make_batch(N, 32, seed=17, offsets=fitoffsets)
+    data, fop = _exposure_matrix(gpu, B, dtype=dtype)
+    st = faint_states(N, seed=3) if faint else None
+    output, param, lik = gpu.demodulateall(B["t"], data, faintparam=st, fitoffsets=fitoffsets)
+    cols = np.ascontiguousarray(data.T)
+    rec, out = gpu.fit_batch(B["t"], cols[:32], cols, fop, state=st, fitoffsets=fitoffsets,
+                             want_output=True)
+    want = data.copy(order="F")
+    want[:, :32] = out.T.astype(dtype)
+    assert output.dtype == dtype and output.shape == (N, 40)
+    assert output.tobytes(order="F") == want.tobytes(order="F")
+    np.testing.assert_array_equal(lik, rec["chi2"])
+    np.testing.assert_array_equal([p.b for p in param], rec["b"])
+    # the raw C-ABI with ldd, ldo > N
+    L = gpu.load()
+    ld_in, ld_out = N + 5, N + 3
+    big = np.zeros((40, ld_in), dtype=dtype)
+    big[:, :N] = cols
+    outb = np.full((40, ld_out), 7 + 7j, dtype=dtype)
+    par = np.zeros(32, dtype=gpu.PARAM_DTYPE)
+    err = ctypes.create_string_buffer(512)
+    fn = L.gpd_demodulateall_c32 if dtype == np.complex64 else L.gpd_demodulateall
+    flags = gpu.GPD_RECENTER | (gpu.GPD_FIT_OFFSETS if fitoffsets else 0)
+    stp = None if st is None else np.ascontiguousarray(st, dtype=np.int8)
+    gpu._lib.check(fn(N, gpu._lib.ptr(B["t"]), gpu._lib.ptr(big), ld_in, gpu._lib.ptr(stp), None,
+                      flags, 60, gpu._lib.ptr(par), gpu._lib.ptr(outb), ld_out, 1, err, len(err)),
+                   err)
+    assert outb[:, :N].tobytes() == np.ascontiguousarray(want.T).tobytes()
+    assert np.all(outb[:, N:] == 7 + 7j)  # nothing beyond each column's N samples
+    assert par.tobytes() == rec.tobytes()
+
+
 @pytest.mark.parametrize("n_samples", [6000, 100000])
 def test_mixed_precision_moments(gpu, opts, n_samples):
     """Harmonics 17..24 of the production moment kernel run on split-bf16 MFMAs.

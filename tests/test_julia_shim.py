@@ -107,7 +107,7 @@ def test_every_ccall_matches_the_header():
             assert JL2C[jt] == ct, f"{sym} arg {i}: Julia {jt} ↔ C {ct}"
         assert len(args) == len(types), f"{sym}: {len(args)} values for {len(types)} types"
         seen.add(sym)
-    for must in ("gpd_fit_batch", "gpd_fit_batch_c32", "gpd_fit_windows", "gpd_process_volt",
+    for must in ("gpd_demodulateall", "gpd_demodulateall_c32", "gpd_fit_windows", "gpd_process_volt",
                  "gpd_buildstates", "gpd_chi2_batch", "gpd_strerror", "gpd_release"):
         assert must in seen, f"the shim never calls {must}"
 
@@ -125,7 +125,7 @@ def test_gpdparam_layout_and_flags():
         assert int(m.group(1), 16) == int(val, 16), name
 
 
-@pytest.mark.parametrize("sym", ["gpd_fit_batch", "gpd_fit_windows", "gpd_process_volt"])
+@pytest.mark.parametrize("sym", ["gpd_demodulateall", "gpd_fit_windows", "gpd_process_volt"])
 def test_integration_md_snippets_match_the_shim(sym):
     """INTEGRATION.md shows the same ccall type tuples as the committed shim."""
     md = open(os.path.join(ROOT, "INTEGRATION.md")).read()
@@ -158,8 +158,11 @@ def test_return_types_follow_the_reference():
     sig = body.split(")", 1)[0]
     assert "data::AbstractMatrix{Complex{T}}" in sig
     assert re.search(r"where\s*\{T<:AbstractFloat\}", body)
-    assert "output = copy(data)" in body
-    assert re.search(r"output\[:, 1:32\] \.= Complex\{T\}\.\(demod\)", body)
+    # output = copy(data) + the diode loop (src/Modulation.jl:353, 417-425): a fresh matrix of
+    # data's element type that gpd_demodulateall fills completely
+    assert "output = similar(d)" in body
+    assert re.search(r"d = c32 \? \(data isa Matrix\{ComplexF32\}", body)
+    assert "gpd_demodulateall_c32" in body and "Ptr{ComplexF32}, Int64, Int32" in body
     assert "ModulationWithOffsets{T}[" in body and "ModulationNoOffsets{T}[" in body
     assert re.search(r"likelihood = T\[p\.chi2 for p in params\]", body)
     assert re.search(r"return \(output, param, likelihood\)", body)
