@@ -126,18 +126,21 @@ def load():
     L.gpd_last_timings.restype = ctypes.c_int
     L.gpd_last_timings.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                    ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+    # (entry points added in r5: an A/B library of an older revision, GPD_LIB, may lack them)
     for name in ("gpd_demodulateall", "gpd_demodulateall_c32"):
-        getattr(L, name).restype = ctypes.c_int
-        getattr(L, name).argtypes = [I64, V, V, I64, V, V, U32, I32, V, V, I64, I32,
-                                     ctypes.c_char_p, ctypes.c_size_t]
-    L.gpd_set_option.restype = ctypes.c_int
-    L.gpd_set_option.argtypes = [ctypes.c_char_p, I64]
-    L.gpd_get_option.restype = ctypes.c_int
-    L.gpd_get_option.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]
-    L.gpd_reset_options.restype = None
-    L.gpd_reset_options.argtypes = []
-    L.gpd_option_name.restype = ctypes.c_char_p
-    L.gpd_option_name.argtypes = [ctypes.c_int]
+        if hasattr(L, name):
+            getattr(L, name).restype = ctypes.c_int
+            getattr(L, name).argtypes = [I64, V, V, I64, V, V, U32, I32, V, V, I64, I32,
+                                         ctypes.c_char_p, ctypes.c_size_t]
+    if hasattr(L, "gpd_set_option"):
+        L.gpd_set_option.restype = ctypes.c_int
+        L.gpd_set_option.argtypes = [ctypes.c_char_p, I64]
+        L.gpd_get_option.restype = ctypes.c_int
+        L.gpd_get_option.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]
+        L.gpd_reset_options.restype = None
+        L.gpd_reset_options.argtypes = []
+        L.gpd_option_name.restype = ctypes.c_char_p
+        L.gpd_option_name.argtypes = [ctypes.c_int]
     if L.gpd_version() != GPD_ABI_VERSION:
         raise ImportError(f"libgpdemod ABI {L.gpd_version()} != {GPD_ABI_VERSION}")
     _lib = L
