@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <climits>
 #include <condition_variable>
 #include <functional>
@@ -69,6 +70,7 @@ enum OptId {
     O_MOMENTS,       // 0: automatic moment kernel; 1: VALU kernel; 2..7 diagnostics variants
     O_FIT_PROF,      // 1: cycle split of the fit kernels on stderr (diagnostics)
     O_SYNC_DEBUG,    // 1: synchronise after every stage and name the stage that faulted
+    O_HOST_PROF,     // 1: wall-clock split of the host-buffer calls on stderr (diagnostics)
     O_COUNT
 };
 struct OptDef {
@@ -80,9 +82,10 @@ constexpr OptDef kOpt[O_COUNT] = {
     {"exact_g", 0},      {"exact_waves", 0},   {"exact_wgt", 0},     {"exact_fast", 1},
     {"exact_mcache", 1}, {"xspin_test", 0},    {"units", 0},         {"upw", 0},
     {"fit_lanes", 0},    {"fit_lps", 0},       {"fit_wpb", 0},       {"cohorts", 1},       {"harm_min_span", 256}, {"fs_cohort_mb", 4096},
-    {"moments", 0},      {"fit_prof", 0},      {"sync_debug", 0}};
+    {"moments", 0},      {"fit_prof", 0},      {"sync_debug", 0},    {"host_prof", 0}};
 std::atomic<long long> g_opt[O_COUNT] = {{1}, {0}, {0},   {0},    {0}, {0}, {0}, {1}, {1}, {0}, {0},
-                                          {0}, {0}, {0},   {0},    {1}, {256}, {4096}, {0}, {0}, {0}};
+                                          {0}, {0}, {0},   {0},    {1}, {256}, {4096}, {0}, {0}, {0},
+                                          {0}};
 inline long long opt(OptId o) { return g_opt[o].load(std::memory_order_relaxed); }
 int opt_find(const char *name) {
     if (!name) return -1;
@@ -193,7 +196,7 @@ struct Layout {
 // long latency-bound chain; so a small batch gets several lanes per series (the objective's
 // harmonics and the 49-angle searches split across them), a large one one lane per series.
 // lps: the most lanes (≤ 8) that keep the fit within one wave per SIMD; gpw: the series spread
-// over every SIMD; wpb: 4 (a workgroup's waves go to the 4 SIMDs of a CU).  The canonical
+// over every SIMD; wpb: below.  The canonical
 // objective makes the records the same bits for every shape.  Options fit_lps, fit_lanes,
 // fit_wpb override (A/B).
 struct FitShape {
@@ -216,9 +219,12 @@ FitShape fit_shape(long long P, int n_cu) {
     gpw = std::max<long long>(1, std::min<long long>(cap, gpw));
     if (opt(O_FIT_LANES) > 0) gpw = std::min<long long>(cap, opt(O_FIT_LANES));
     f.gpw = (int)gpw;
-    f.wpb = 4;
-    if (opt(O_FIT_WPB) > 0) f.wpb = (int)std::min(4LL, opt(O_FIT_WPB));
     const long long waves = (P + gpw - 1) / gpw;
+    // 4 waves per workgroup once the waves outnumber the CUs with several lanes per series
+    // (C4 rank: 0.90 → 0.86 ms); otherwise 1 — waves sharing a CU slow each other (r5 sweep:
+    // 32 series 0.31 vs 0.52 ms, C3 2.60 vs 2.81 ms)
+    f.wpb = (f.lps > 1 && waves > n_cu) ? 4 : 1;
+    if (opt(O_FIT_WPB) > 0) f.wpb = (int)std::min(4LL, opt(O_FIT_WPB));
     f.wpb = (int)std::max(1LL, std::min<long long>(f.wpb, waves));
     f.grid = (unsigned)((waves + f.wpb - 1) / f.wpb);
     f.lds = (size_t)f.wpb * (size_t)f.gpw * sizeof(Newuoa<2, 5, true, 1>);
@@ -1437,6 +1443,11 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
             cleanup();
             return fail(GPD_E_HIP);
         }
+        const bool hprof = opt(O_HOST_PROF) != 0;
+        auto hnow = [] { return std::chrono::steady_clock::now(); };
+        const auto h0 = hnow();
+        if (hprof) (void)hipStreamSynchronize(s);
+        const auto h1 = hnow();
         int r = pipeline_dev(N, P, dt, dd, N, dfc, nfc, N, dfcop, dst, omega, xinit, flags, maxfun,
                              (gpd_param *)dpar, (gpd_c64 *)dout, N, dbphi, dev, s, errbuf_l,
                              errlen_l, window, is_c32);
@@ -1450,6 +1461,9 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
               chk(hipMemcpy2DAsync(out_demod + p0 * ldo + s0, ldo * sizeof(gpd_c64), dout,
                                    N * sizeof(c64), N * sizeof(c64), P,
                                    hipMemcpyDeviceToHost, s), "D2H out"));
+        if (hprof) (void)hipStreamSynchronize(s);
+        const auto h2 = hnow();
+        auto h3 = h2, h4 = h2;
         if (ok && out_demod && out_kind != 0) {
             // staged: one DMA of the P×N demodulated columns into pinned memory, then the host
             // pool copies them into the caller's columns (ldo), rounding to ComplexF32 for kind 2
@@ -1468,11 +1482,19 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
             ok = ok && chk(hipMemcpyAsync(cx->hpin, dout, bytes, hipMemcpyDeviceToHost, s),
                            "D2H out (staged)") &&
                  chk(hipStreamSynchronize(s), "hipStreamSynchronize");
+            h3 = hnow();
             if (ok) {
                 const size_t des = out_kind == 2 ? sizeof(gpd_c32) : sizeof(gpd_c64);
                 pool_copy_cols((char *)out_demod + ((size_t)p0 * ldo + s0) * des, des, ldo,
                                cx->hpin, sizeof(c64), N, N, P);
             }
+            h4 = hnow();
+        }
+        if (hprof) {
+            auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+            fprintf(stderr, "host_prof dev %d: H2D %.3f ms, pipeline %.3f ms, D2H staged %.3f ms, "
+                    "host copy %.3f ms (pool %d threads)\n", dev, ms(h0, h1), ms(h1, h2),
+                    ms(h2, h3), ms(h3, h4), HostPool::get().size());
         }
         ok = ok && chk(hipStreamSynchronize(s), "hipStreamSynchronize");
         cleanup();
@@ -1514,7 +1536,11 @@ static int host_demodulateall(int64_t N, const double *t, const void *data, int6
     for (int c = 0; c < 32; ++c) fcop[c] = (c < 16 ? 0 : 4) + (c % 16) / 4;
     const char *fc = (const char *)data + (size_t)32 * ldd * esz;
     std::thread fcopy([&] {
+        const auto t0 = std::chrono::steady_clock::now();
         pool_copy_cols((char *)output + (size_t)32 * ldo * esz, esz, ldo, fc, esz, ldd, N, 8);
+        if (opt(O_HOST_PROF))
+            fprintf(stderr, "host_prof FC columns copy %.3f ms\n",
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     });
     const int r = host_batch(N, 32, t, data, ldd, fc, 8, ldd, fcop, state, 6.283185, xinit, flags,
                              maxfun, params, (gpd_c64 *)output, ldo, nullptr, n_gpus, errbuf,
