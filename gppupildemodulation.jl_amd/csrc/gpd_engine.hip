@@ -144,6 +144,7 @@ struct DevCtx {
     // gpd_demodulateall: pinned staging of the demodulated columns (grow-only)
     char *hpin = nullptr;
     size_t hpin_cap = 0;
+    hipEvent_t hpin_ev[4] = {};  // the staged column chunks' arrival (host copy pipelined)
     // the last fit call's faint statistics in the workspace (gpd_last_faint_stats; tests)
     const double *last_fstat = nullptr;
     long long last_fstat_P = 0;
@@ -464,6 +465,23 @@ void pool_copy_cols(char *dst, size_t des, int64_t dld, const char *src, size_t 
             float *dv = (float *)d;
             for (int64_t k = 0; k < 2 * nr; ++k) dv[k] = (float)sv[k];
         }
+    });
+}
+
+// One store per page of ncols columns of rows elements (element size es, leading dimension ld),
+// inside each column's bytes only: the page faults of a fresh destination taken up front, in
+// parallel, rather than inside the copy that follows (which overwrites every byte stored here).
+void pool_touch_cols(char *dst, size_t es, int64_t ld, int64_t rows, int64_t ncols) {
+    constexpr int64_t kPage = 4096;
+    const int64_t per = std::max<int64_t>(1, (int64_t)(1 << 20) / (int64_t)es);
+    const int64_t pieces_per_col = (rows + per - 1) / per;
+    HostPool::get().run((int)(pieces_per_col * ncols), [&](int i) {
+        const int64_t c = i / pieces_per_col, r0 = (i % pieces_per_col) * per;
+        const int64_t nr = std::min(per, rows - r0);
+        volatile char *b = dst + ((size_t)c * ld + r0) * es, *e = b + nr * es;
+        for (volatile char *q = b; q < e;
+             q = (volatile char *)(((uintptr_t)q + kPage) & ~(uintptr_t)(kPage - 1)))
+            *q = 0;
     });
 }
 
@@ -992,7 +1010,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                 k_moments_ws<8><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
             else if (mk == 6)  // ws_mfmaonly
                 k_moments_ws<5><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
-            else if (mk == 7)  // ws_prof {  // cycle split per role (stderr)
+            else if (mk == 7) {  // ws_prof: cycle split per role (stderr)
                 HIP_TRY(prof_reset());
                 k_moments_ws<6><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
                 HIP_TRY(prof_read());
@@ -1426,6 +1444,7 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
         char *dd = A + o_d, *dfc = A + o_fc;
         int32_t *dfcop = (int32_t *)(A + o_fcop);
         Param *dpar = (Param *)(A + o_par);
+        const auto hs = std::chrono::steady_clock::now();
         int8_t *dst = state ? (int8_t *)(A + o_st) : nullptr;
         double *dbphi = bphi ? (double *)(A + o_bphi) : nullptr;
         c64 *dout = out_demod ? (c64 *)(A + o_out) : nullptr;
@@ -1479,22 +1498,43 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
                     if (ok) cx->hpin_cap = bytes;
                 }
             }
-            ok = ok && chk(hipMemcpyAsync(cx->hpin, dout, bytes, hipMemcpyDeviceToHost, s),
-                           "D2H out (staged)") &&
-                 chk(hipStreamSynchronize(s), "hipStreamSynchronize");
+            // the columns come back in up to 4 chunks, an event after each: the pool copies
+            // chunk c while chunk c + 1 is still in flight
+            const int nch = (int)std::min<int64_t>(4, P);
+            for (int c = 0; ok && c < nch; ++c)
+                if (!cx->hpin_ev[c])
+                    ok = chk(hipEventCreateWithFlags(&cx->hpin_ev[c], hipEventDisableTiming),
+                             "hipEventCreate");
+            for (int c = 0; ok && c < nch; ++c) {
+                const int64_t q0 = P * c / nch, q1 = P * (c + 1) / nch;
+                ok = chk(hipMemcpyAsync(cx->hpin + (size_t)q0 * N * sizeof(c64), dout + q0 * N,
+                                        (size_t)(q1 - q0) * N * sizeof(c64), hipMemcpyDeviceToHost,
+                                        s), "D2H out (staged)") &&
+                     chk(hipEventRecord(cx->hpin_ev[c], s), "hipEventRecord");
+            }
+            const size_t des = out_kind == 2 ? sizeof(gpd_c32) : sizeof(gpd_c64);
+            char *dst0 = (char *)out_demod + ((size_t)p0 * ldo + s0) * des;
+            // while the device still computes and copies: the first touch of the caller's
+            // destination columns (a fresh output's page faults — the kernel zeroing each page —
+            // are most of an unpipelined host copy); one store per page, inside the columns only
+            // (never the ldo gaps), each later overwritten by the copy below
+            if (ok) pool_touch_cols(dst0, des, ldo, N, P);
             h3 = hnow();
-            if (ok) {
-                const size_t des = out_kind == 2 ? sizeof(gpd_c32) : sizeof(gpd_c64);
-                pool_copy_cols((char *)out_demod + ((size_t)p0 * ldo + s0) * des, des, ldo,
-                               cx->hpin, sizeof(c64), N, N, P);
+            for (int c = 0; ok && c < nch; ++c) {
+                const int64_t q0 = P * c / nch, q1 = P * (c + 1) / nch;
+                ok = chk(hipEventSynchronize(cx->hpin_ev[c]), "hipEventSynchronize");
+                if (ok)
+                    pool_copy_cols(dst0 + (size_t)q0 * ldo * des, des, ldo,
+                                   cx->hpin + (size_t)q0 * N * sizeof(c64), sizeof(c64), N, N,
+                                   q1 - q0);
             }
             h4 = hnow();
         }
         if (hprof) {
             auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-            fprintf(stderr, "host_prof dev %d: H2D %.3f ms, pipeline %.3f ms, D2H staged %.3f ms, "
-                    "host copy %.3f ms (pool %d threads)\n", dev, ms(h0, h1), ms(h1, h2),
-                    ms(h2, h3), ms(h3, h4), HostPool::get().size());
+            fprintf(stderr, "host_prof dev %d: H2D issue %.3f ms, H2D wait %.3f ms, pipeline %.3f ms, "
+                    "output touch %.3f ms, D2H + host copy %.3f ms (pool %d threads)\n", dev, ms(hs, h0),
+                    ms(h0, h1), ms(h1, h2), ms(h2, h3), ms(h3, h4), HostPool::get().size());
         }
         ok = ok && chk(hipStreamSynchronize(s), "hipStreamSynchronize");
         cleanup();
@@ -1535,6 +1575,7 @@ static int host_demodulateall(int64_t N, const double *t, const void *data, int6
     int32_t fcop[32];
     for (int c = 0; c < 32; ++c) fcop[c] = (c < 16 ? 0 : 4) + (c % 16) / 4;
     const char *fc = (const char *)data + (size_t)32 * ldd * esz;
+    const auto tcall = std::chrono::steady_clock::now();
     std::thread fcopy([&] {
         const auto t0 = std::chrono::steady_clock::now();
         pool_copy_cols((char *)output + (size_t)32 * ldo * esz, esz, ldo, fc, esz, ldd, N, 8);
@@ -1546,6 +1587,9 @@ static int host_demodulateall(int64_t N, const double *t, const void *data, int6
                              maxfun, params, (gpd_c64 *)output, ldo, nullptr, n_gpus, errbuf,
                              errlen, 0, c32, c32 ? 2 : 1);
     fcopy.join();
+    if (opt(O_HOST_PROF))
+        fprintf(stderr, "host_prof demodulateall total %.3f ms\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tcall).count());
     return r;
 }
 

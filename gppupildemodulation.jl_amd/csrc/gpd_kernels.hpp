@@ -1257,7 +1257,11 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             const long long s = s_begin + (long long)it * MM_TS + ss;
             bool sok = s < s_end;
             const long long sl = s < Nm1 ? s : Nm1;
-            c64 *q_out = qs[it & 1];
+            // mm_phys(4(gq + 8r) + j, ss) = q_base + 32r + j: the swizzle (bit 3 of the series)
+            // only touches 4·gq's bits, so the 16 stores share one address and immediate offsets
+            // (written per (r, j), the compiler kept an address register each — the faint variant
+            // spilled them, and every spill reload waited for the tile prefetch: vmcnt(0))
+            c64 *q_out = qs[it & 1] + (ss * MM_ROW + ((4 * gq) ^ ((ss & 1) << 3)));
             if constexpr (FAINT) {
                 const int st = R.st;
                 const bool v = sok && fst_valid(pb.flags, st);
@@ -1292,7 +1296,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
                         q.re = sok ? q.re : 0.0;
                         q.im = sok ? q.im : 0.0;
                     }
-                    q_out[mm_phys(pl, ss)] = q;
+                    q_out[32 * r + j] = q;
                 }
             }
         };

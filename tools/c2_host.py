@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """C2 exposure through the host-buffer drop-in (gpd_demodulateall): where the time of one call
 goes.  Median of `reps` calls each: the fit alone (records only, gpd_fit_batch), demodulateall
-into a fresh output (the reference's semantics: a new matrix per call), the same call into an
+into a fresh output (the reference's semantics: a new matrix per call; once with the previous
+result released inside the timed loop, once with every result kept alive and the release timed
+apart), the same call into an
 output reused across calls (pages already touched), and — for scale — numpy's own
 `data.copy()` of the exposure (what `output = copy(data)` costs on one thread).  Then one call
 with option host_prof = 1 (the library's wall-clock split on stderr).  One JSON line."""
@@ -46,6 +48,14 @@ def main():
     out = {}
     out["fit_only_ms"] = med(lambda: gpd.fit_batch(t, cols[:32], cols, fop), reps)
     out["demodulateall_fresh_ms"] = med(lambda: gpd.demodulateall(t, data), reps)
+    # the same calls with every result kept until the end: the previous result's release
+    # (numpy's munmap of 64 MB of touched pages) then falls outside the timed call
+    kept = []
+    out["demodulateall_fresh_kept_ms"] = med(lambda: kept.append(gpd.demodulateall(t, data)), reps)
+    t0 = time.perf_counter()
+    n_kept = len(kept)
+    kept.clear()
+    out["release_of_one_output_ms"] = round(1e3 * (time.perf_counter() - t0) / n_kept, 3)
     reuse = np.empty((40, N), dtype=np.complex128)
     par = np.zeros(32, dtype=gpd.PARAM_DTYPE)
     import ctypes
