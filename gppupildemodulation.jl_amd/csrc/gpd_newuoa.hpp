@@ -1075,6 +1075,16 @@ struct Newuoa {
         GPD_NW_T1(tinit_, 4);
 
         // ---------------------------------------- iterations
+        // NEWUOB's labels as explicit states, walked so that a wave's fits meet at the objective:
+        // each trip of the outer loop is one evaluation (L290) for every fit still running.
+        // Within a trip a fit first walks L460 / L490 / L100 (trust-region step, geometry point,
+        // ρ reduction — in that order within one pass of the inner loop, so the common paths
+        // take one pass) until it stands at L120 (a step to evaluate), at L290 (L490's final
+        // evaluation) or is done; then the L120 block (VLAG, BETA, BIGLAG/BIGDEN) and the
+        // evaluation run once for all of them together.  The same operations in the same order
+        // as the published goto structure — only the points where diverged fits wait for each
+        // other change (before r5 the fits of a wave reached the objective in different passes
+        // of the compiler's structurised loop, ~3 objective executions per evaluation).
         double rho = rhobeg, delta = rho;
         int idz = 1;
         double diffa = 0.0, diffb = 0.0, diffc = 0.0, ratio = 0.0, crvmin = 0.0;
@@ -1087,306 +1097,335 @@ struct Newuoa {
             xopt[i] = rd2_(xpt, kopt - 1, i);
             xoptsq = xoptsq + xopt[i] * xopt[i];
         }
-    L90:
-        nfsav = nf;
-    L100:
-        knew = 0;
-        {
-            GPD_NW_T0(tt_);
-            trsapp(delta, d, crvmin);
-            GPD_NW_T1(tt_, 0);
-        }
-        dsq = 0.0;
+        enum { S100, S120, S290, S460, S490, SDONE };
+        int st = S100;
+        nfsav = nf;  // L90
+        for (;;) {
+            while (st == S460 || st == S490 || st == S100) {
+                if (st == S460) {  // L460: the point farthest from xopt, if far enough
+                    double distsq = 4.0 * delta * delta;
 #pragma unroll
-        for (int i = 0; i < N; ++i) dsq = dsq + d[i] * d[i];
-        dnorm = fmin(delta, sqrt(dsq));
-        if (dnorm < 0.5 * rho) {
-            knew = -1;
-            delta = 0.1 * delta;
-            ratio = -1.0;
-            if (delta <= 1.5 * rho) delta = rho;
-            if (nf <= nfsav + 2) goto L460;
-            const double temp = 0.125 * crvmin * rho * rho;
-            if (temp <= fmax(fmax(diffa, diffb), diffc)) goto L460;
-            goto L490;
-        }
-    L120:
-        if (dsq <= 1.0e-3 * xoptsq) shift_base(xoptsq, idz);
-        if (knew > 0) {
-            GPD_NW_T0(tt_);
-            biglag(idz, knew, dstep, alpha);
-            GPD_NW_T1(tt_, 1);
-        }
-        // VLAG and BETA for the current D; W(1..NPT) = Wcheck
-        {
-            GPD_NW_T0(tvl_);
+                    for (int k = 0; k < NPT; ++k) {
+                        double sum = 0.0;
 #pragma unroll
-            for (int k = 0; k < NPT; ++k) {
-                double suma = 0.0, sumb = 0.0, sum = 0.0;
-#pragma unroll
-                for (int j = 0; j < N; ++j) {
-                    suma = suma + xpt[k][j] * d[j];
-                    sumb = sumb + xpt[k][j] * xopt[j];
-                    sum = sum + bmat[k][j] * d[j];
-                }
-                w[k] = suma * (0.5 * suma + sumb);
-                vlag[k] = sum;
-            }
-            beta = 0.0;
-#pragma unroll
-            for (int k = 0; k < NPTM; ++k) {
-                double sum = 0.0;
-#pragma unroll
-                for (int i = 0; i < NPT; ++i) sum = sum + zmat[i][k] * w[i];
-                if (k + 1 < idz) {
-                    beta = beta + sum * sum;
-                    sum = -sum;
-                } else {
-                    beta = beta - sum * sum;
-                }
-#pragma unroll
-                for (int i = 0; i < NPT; ++i) vlag[i] = vlag[i] + sum * zmat[i][k];
-            }
-            double bsum = 0.0, dx = 0.0;
-#pragma unroll
-            for (int j = 0; j < N; ++j) {
-                double sum = 0.0;
-#pragma unroll
-                for (int i = 0; i < NPT; ++i) sum = sum + w[i] * bmat[i][j];
-                bsum = bsum + sum * d[j];
-                const int jp = NPT + j;
-#pragma unroll
-                for (int k = 0; k < N; ++k) sum = sum + bmat[jp][k] * d[k];
-                vlag[jp] = sum;
-                bsum = bsum + sum * d[j];
-                dx = dx + d[j] * xopt[j];
-            }
-            beta = dx * dx + dsq * (xoptsq + dx + dx + 0.5 * dsq) + beta - bsum;
-            wr_(vlag, kopt - 1, rd_(vlag, kopt - 1) + 1.0);
-            GPD_NW_T1(tvl_, 5);
-        }
-        if (knew > 0) {
-            const double vk = rd_(vlag, knew - 1);
-            const double temp = 1.0 + alpha * beta / (vk * vk);
-            if (fabs(temp) <= 0.8) {
-                GPD_NW_T0(tt_);
-                bigden(idz, kopt, knew, beta);
-                GPD_NW_T1(tt_, 2);
-            }
-        }
-    L290:
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-            xnew[i] = xopt[i] + d[i];
-            x[i] = xbase[i] + xnew[i];
-        }
-        nf = nf + 1;
-        if (nf > nftest) {
-            nf = nf - 1;
-            goto L530;
-        }
-        f = fun(x);
-        if (knew == -1) goto L530;
-        {
-            vquad = 0.0;
-            int ih = 0;
-#pragma unroll
-            for (int j = 0; j < N; ++j) {
-                vquad = vquad + d[j] * gq[j];
-#pragma unroll
-                for (int i = 0; i <= j; ++i) {
-                    double temp = d[i] * xnew[j] + d[j] * xopt[i];
-                    if (i == j) temp = 0.5 * temp;
-                    vquad = vquad + temp * hq[ih];
-                    ++ih;
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < NPT; ++k) vquad = vquad + pq[k] * w[k];
-        }
-        diff = f - fopt - vquad;
-        diffc = diffb;
-        diffb = diffa;
-        diffa = fabs(diff);
-        if (dnorm > rho) nfsav = nf;
-        {
-            const double fsave = fopt;
-            if (f < fopt) {
-                fopt = f;
-                xoptsq = 0.0;
-#pragma unroll
-                for (int i = 0; i < N; ++i) {
-                    xopt[i] = xnew[i];
-                    xoptsq = xoptsq + xopt[i] * xopt[i];
-                }
-            }
-            const int ksave = knew;
-            if (knew <= 0) {
-                if (vquad >= 0.0) goto L530;  // trust-region step failed to reduce Q
-                ratio = (f - fsave) / vquad;
-                if (ratio <= 0.1) {
-                    delta = 0.5 * dnorm;
-                } else if (ratio <= 0.7) {
-                    delta = fmax(0.5 * delta, dnorm);
-                } else {
-                    delta = fmax(0.5 * delta, dnorm + dnorm);
-                }
-                if (delta <= 1.5 * rho) delta = rho;
-                // point to drop
-                double rs = fmax(0.1 * delta, rho);
-                rs = rs * rs;
-                int ktemp = 0;
-                double detrat = 0.0;
-                if (f >= fsave) {
-                    ktemp = kopt;
-                    detrat = 1.0;
-                }
-#pragma unroll
-                for (int k = 0; k < NPT; ++k) {
-                    double hdiag = 0.0;
-#pragma unroll
-                    for (int j = 0; j < NPTM; ++j) {
-                        double temp = 1.0;
-                        if (j + 1 < idz) temp = -1.0;
-                        hdiag = hdiag + temp * zmat[k][j] * zmat[k][j];
+                        for (int j = 0; j < N; ++j) sum = sum + (xpt[k][j] - xopt[j]) * (xpt[k][j] - xopt[j]);
+                        if (sum > distsq) {
+                            knew = k + 1;
+                            distsq = sum;
+                        }
                     }
-                    double temp = fabs(beta * hdiag + vlag[k] * vlag[k]);
-                    double distsq = 0.0;
-#pragma unroll
-                    for (int j = 0; j < N; ++j)
-                        distsq = distsq + (xpt[k][j] - xopt[j]) * (xpt[k][j] - xopt[j]);
-                    if (distsq > rs) {
-                        const double r = distsq / rs;
-                        temp = temp * (r * r * r);
-                    }
-                    if (temp > detrat && k + 1 != ktemp) {
-                        detrat = temp;
-                        knew = k + 1;
+                    if (knew > 0) {
+                        dstep = fmax(fmin(0.1 * sqrt(distsq), 0.5 * delta), rho);
+                        dsq = dstep * dstep;
+                        st = S120;
+                    } else if (ratio > 0.0) {
+                        st = S100;
+                    } else if (fmax(delta, dnorm) > rho) {
+                        st = S100;
+                    } else {
+                        st = S490;
                     }
                 }
-                if (knew == 0) goto L460;
+                if (st == S490) {  // L490: reduce ρ, or stop
+                    if (rho > rhoend) {
+                        delta = 0.5 * rho;
+                        ratio = rho / rhoend;
+                        if (ratio <= 16.0) {
+                            rho = rhoend;
+                        } else if (ratio <= 250.0) {
+                            rho = sqrt(ratio) * rhoend;
+                        } else {
+                            rho = 0.1 * rho;
+                        }
+                        delta = fmax(delta, rho);
+                        nfsav = nf;  // L90
+                        st = S100;
+                    } else {
+                        st = knew == -1 ? S290 : SDONE;
+                    }
+                }
+                if (st == S100) {  // L100: trust-region step
+                    knew = 0;
+                    {
+                        GPD_NW_T0(tt_);
+                        trsapp(delta, d, crvmin);
+                        GPD_NW_T1(tt_, 0);
+                    }
+                    dsq = 0.0;
+#pragma unroll
+                    for (int i = 0; i < N; ++i) dsq = dsq + d[i] * d[i];
+                    dnorm = fmin(delta, sqrt(dsq));
+                    if (dnorm < 0.5 * rho) {
+                        knew = -1;
+                        delta = 0.1 * delta;
+                        ratio = -1.0;
+                        if (delta <= 1.5 * rho) delta = rho;
+                        if (nf <= nfsav + 2) {
+                            st = S460;
+                        } else {
+                            const double temp = 0.125 * crvmin * rho * rho;
+                            st = temp <= fmax(fmax(diffa, diffb), diffc) ? S460 : S490;
+                        }
+                    } else {
+                        st = S120;
+                    }
+                }
             }
-            // L410: move point knew to xnew and update the model
+            if (st == SDONE) break;
+            if (st == S120) {  // L120
+                if (dsq <= 1.0e-3 * xoptsq) shift_base(xoptsq, idz);
+                if (knew > 0) {
+                    GPD_NW_T0(tt_);
+                    biglag(idz, knew, dstep, alpha);
+                    GPD_NW_T1(tt_, 1);
+                }
+                // VLAG and BETA for the current D; W(1..NPT) = Wcheck
+                {
+                    GPD_NW_T0(tvl_);
+#pragma unroll
+                    for (int k = 0; k < NPT; ++k) {
+                        double suma = 0.0, sumb = 0.0, sum = 0.0;
+#pragma unroll
+                        for (int j = 0; j < N; ++j) {
+                            suma = suma + xpt[k][j] * d[j];
+                            sumb = sumb + xpt[k][j] * xopt[j];
+                            sum = sum + bmat[k][j] * d[j];
+                        }
+                        w[k] = suma * (0.5 * suma + sumb);
+                        vlag[k] = sum;
+                    }
+                    beta = 0.0;
+#pragma unroll
+                    for (int k = 0; k < NPTM; ++k) {
+                        double sum = 0.0;
+#pragma unroll
+                        for (int i = 0; i < NPT; ++i) sum = sum + zmat[i][k] * w[i];
+                        if (k + 1 < idz) {
+                            beta = beta + sum * sum;
+                            sum = -sum;
+                        } else {
+                            beta = beta - sum * sum;
+                        }
+#pragma unroll
+                        for (int i = 0; i < NPT; ++i) vlag[i] = vlag[i] + sum * zmat[i][k];
+                    }
+                    double bsum = 0.0, dx = 0.0;
+#pragma unroll
+                    for (int j = 0; j < N; ++j) {
+                        double sum = 0.0;
+#pragma unroll
+                        for (int i = 0; i < NPT; ++i) sum = sum + w[i] * bmat[i][j];
+                        bsum = bsum + sum * d[j];
+                        const int jp = NPT + j;
+#pragma unroll
+                        for (int k = 0; k < N; ++k) sum = sum + bmat[jp][k] * d[k];
+                        vlag[jp] = sum;
+                        bsum = bsum + sum * d[j];
+                        dx = dx + d[j] * xopt[j];
+                    }
+                    beta = dx * dx + dsq * (xoptsq + dx + dx + 0.5 * dsq) + beta - bsum;
+                    wr_(vlag, kopt - 1, rd_(vlag, kopt - 1) + 1.0);
+                    GPD_NW_T1(tvl_, 5);
+                }
+                if (knew > 0) {
+                    const double vk = rd_(vlag, knew - 1);
+                    const double temp = 1.0 + alpha * beta / (vk * vk);
+                    if (fabs(temp) <= 0.8) {
+                        GPD_NW_T0(tt_);
+                        bigden(idz, kopt, knew, beta);
+                        GPD_NW_T1(tt_, 2);
+                    }
+                }
+            }
+            // L290: evaluate
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                xnew[i] = xopt[i] + d[i];
+                x[i] = xbase[i] + xnew[i];
+            }
+            nf = nf + 1;
+            if (nf > nftest) {
+                nf = nf - 1;
+                break;  // L530
+            }
+            f = fun(x);
+            if (knew == -1) break;  // L530
             {
-                GPD_NW_T0(tt_);
-                update(idz, beta, knew);
-                GPD_NW_T1(tt_, 3);
-            }
-            wr_(fval, knew - 1, f);
-            {
-                GPD_NW_T0(tmu_);
-                const double pqk = rd_(pq, knew - 1);
+                vquad = 0.0;
                 int ih = 0;
 #pragma unroll
-                for (int i = 0; i < N; ++i) {
-                    const double temp = pqk * rd2_(xpt, knew - 1, i);
+                for (int j = 0; j < N; ++j) {
+                    vquad = vquad + d[j] * gq[j];
 #pragma unroll
-                    for (int j = 0; j <= i; ++j) {
-                        hq[ih] = hq[ih] + temp * rd2_(xpt, knew - 1, j);
+                    for (int i = 0; i <= j; ++i) {
+                        double temp = d[i] * xnew[j] + d[j] * xopt[i];
+                        if (i == j) temp = 0.5 * temp;
+                        vquad = vquad + temp * hq[ih];
                         ++ih;
                     }
                 }
-                wr_(pq, knew - 1, 0.0);
 #pragma unroll
-                for (int j = 0; j < NPTM; ++j) {
-                    double temp = diff * rd2_(zmat, knew - 1, j);
-                    if (j + 1 < idz) temp = -temp;
+                for (int k = 0; k < NPT; ++k) vquad = vquad + pq[k] * w[k];
+            }
+            diff = f - fopt - vquad;
+            diffc = diffb;
+            diffb = diffa;
+            diffa = fabs(diff);
+            if (dnorm > rho) nfsav = nf;
+            {
+                const double fsave = fopt;
+                if (f < fopt) {
+                    fopt = f;
+                    xoptsq = 0.0;
 #pragma unroll
-                    for (int k = 0; k < NPT; ++k) pq[k] = pq[k] + temp * zmat[k][j];
-                }
-                double gqsq = 0.0;
-#pragma unroll
-                for (int i = 0; i < N; ++i) {
-                    gq[i] = gq[i] + diff * rd2_(bmat, knew - 1, i);
-                    gqsq = gqsq + gq[i] * gq[i];
-                    wr2_(xpt, knew - 1, i, xnew[i]);
-                }
-                if (ksave == 0 && delta == rho) {
-                    if (fabs(ratio) > 1.0e-2) {
-                        itest = 0;
-                    } else {
-                        const double fk = rd_(fval, kopt - 1);
-#pragma unroll
-                        for (int k = 0; k < NPT; ++k) vlag[k] = fval[k] - fk;
-                        double gisq = 0.0;
-#pragma unroll
-                        for (int i = 0; i < N; ++i) {
-                            double sum = 0.0;
-#pragma unroll
-                            for (int k = 0; k < NPT; ++k) sum = sum + bmat[k][i] * vlag[k];
-                            gisq = gisq + sum * sum;
-                            w[i] = sum;
-                        }
-                        itest = itest + 1;
-                        if (gqsq < 1.0e2 * gisq) itest = 0;
-                        if (itest >= 3) {
-#pragma unroll
-                            for (int i = 0; i < N; ++i) gq[i] = w[i];
-#pragma unroll
-                            for (int ih2 = 0; ih2 < NH; ++ih2) hq[ih2] = 0.0;
-                            double wz[NPTM];
-#pragma unroll
-                            for (int j = 0; j < NPTM; ++j) {
-                                wz[j] = 0.0;
-#pragma unroll
-                                for (int k = 0; k < NPT; ++k) wz[j] = wz[j] + vlag[k] * zmat[k][j];
-                                if (j + 1 < idz) wz[j] = -wz[j];
-                            }
-#pragma unroll
-                            for (int j = 0; j < NPTM; ++j) w[j] = wz[j];
-#pragma unroll
-                            for (int k = 0; k < NPT; ++k) {
-                                pq[k] = 0.0;
-#pragma unroll
-                                for (int j = 0; j < NPTM; ++j) pq[k] = pq[k] + zmat[k][j] * w[j];
-                            }
-                            itest = 0;
-                        }
+                    for (int i = 0; i < N; ++i) {
+                        xopt[i] = xnew[i];
+                        xoptsq = xoptsq + xopt[i] * xopt[i];
                     }
                 }
-                GPD_NW_T1(tmu_, 6);
-            }
-            if (f < fsave) kopt = knew;
-            if (f <= fsave + 0.1 * vquad) goto L100;
-            if (ksave > 0) goto L100;
-        }
-        knew = 0;
-    L460 : {
-        double distsq = 4.0 * delta * delta;
+                const int ksave = knew;
+                if (knew <= 0) {
+                    if (vquad >= 0.0) break;  // L530: trust-region step failed to reduce Q
+                    ratio = (f - fsave) / vquad;
+                    if (ratio <= 0.1) {
+                        delta = 0.5 * dnorm;
+                    } else if (ratio <= 0.7) {
+                        delta = fmax(0.5 * delta, dnorm);
+                    } else {
+                        delta = fmax(0.5 * delta, dnorm + dnorm);
+                    }
+                    if (delta <= 1.5 * rho) delta = rho;
+                    // point to drop
+                    double rs = fmax(0.1 * delta, rho);
+                    rs = rs * rs;
+                    int ktemp = 0;
+                    double detrat = 0.0;
+                    if (f >= fsave) {
+                        ktemp = kopt;
+                        detrat = 1.0;
+                    }
 #pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-            double sum = 0.0;
+                    for (int k = 0; k < NPT; ++k) {
+                        double hdiag = 0.0;
 #pragma unroll
-            for (int j = 0; j < N; ++j) sum = sum + (xpt[k][j] - xopt[j]) * (xpt[k][j] - xopt[j]);
-            if (sum > distsq) {
-                knew = k + 1;
-                distsq = sum;
+                        for (int j = 0; j < NPTM; ++j) {
+                            double temp = 1.0;
+                            if (j + 1 < idz) temp = -1.0;
+                            hdiag = hdiag + temp * zmat[k][j] * zmat[k][j];
+                        }
+                        double temp = fabs(beta * hdiag + vlag[k] * vlag[k]);
+                        double distsq = 0.0;
+#pragma unroll
+                        for (int j = 0; j < N; ++j)
+                            distsq = distsq + (xpt[k][j] - xopt[j]) * (xpt[k][j] - xopt[j]);
+                        if (distsq > rs) {
+                            const double r = distsq / rs;
+                            temp = temp * (r * r * r);
+                        }
+                        if (temp > detrat && k + 1 != ktemp) {
+                            detrat = temp;
+                            knew = k + 1;
+                        }
+                    }
+                    if (knew == 0) {  // L460 with knew = 0
+                        st = S460;
+                        continue;
+                    }
+                }
+                // L410: move point knew to xnew and update the model
+                {
+                    GPD_NW_T0(tt_);
+                    update(idz, beta, knew);
+                    GPD_NW_T1(tt_, 3);
+                }
+                wr_(fval, knew - 1, f);
+                {
+                    GPD_NW_T0(tmu_);
+                    const double pqk = rd_(pq, knew - 1);
+                    int ih = 0;
+#pragma unroll
+                    for (int i = 0; i < N; ++i) {
+                        const double temp = pqk * rd2_(xpt, knew - 1, i);
+#pragma unroll
+                        for (int j = 0; j <= i; ++j) {
+                            hq[ih] = hq[ih] + temp * rd2_(xpt, knew - 1, j);
+                            ++ih;
+                        }
+                    }
+                    wr_(pq, knew - 1, 0.0);
+#pragma unroll
+                    for (int j = 0; j < NPTM; ++j) {
+                        double temp = diff * rd2_(zmat, knew - 1, j);
+                        if (j + 1 < idz) temp = -temp;
+#pragma unroll
+                        for (int k = 0; k < NPT; ++k) pq[k] = pq[k] + temp * zmat[k][j];
+                    }
+                    double gqsq = 0.0;
+#pragma unroll
+                    for (int i = 0; i < N; ++i) {
+                        gq[i] = gq[i] + diff * rd2_(bmat, knew - 1, i);
+                        gqsq = gqsq + gq[i] * gq[i];
+                        wr2_(xpt, knew - 1, i, xnew[i]);
+                    }
+                    if (ksave == 0 && delta == rho) {
+                        if (fabs(ratio) > 1.0e-2) {
+                            itest = 0;
+                        } else {
+                            const double fk = rd_(fval, kopt - 1);
+#pragma unroll
+                            for (int k = 0; k < NPT; ++k) vlag[k] = fval[k] - fk;
+                            double gisq = 0.0;
+#pragma unroll
+                            for (int i = 0; i < N; ++i) {
+                                double sum = 0.0;
+#pragma unroll
+                                for (int k = 0; k < NPT; ++k) sum = sum + bmat[k][i] * vlag[k];
+                                gisq = gisq + sum * sum;
+                                w[i] = sum;
+                            }
+                            itest = itest + 1;
+                            if (gqsq < 1.0e2 * gisq) itest = 0;
+                            if (itest >= 3) {
+#pragma unroll
+                                for (int i = 0; i < N; ++i) gq[i] = w[i];
+#pragma unroll
+                                for (int ih2 = 0; ih2 < NH; ++ih2) hq[ih2] = 0.0;
+                                double wz[NPTM];
+#pragma unroll
+                                for (int j = 0; j < NPTM; ++j) {
+                                    wz[j] = 0.0;
+#pragma unroll
+                                    for (int k = 0; k < NPT; ++k) wz[j] = wz[j] + vlag[k] * zmat[k][j];
+                                    if (j + 1 < idz) wz[j] = -wz[j];
+                                }
+#pragma unroll
+                                for (int j = 0; j < NPTM; ++j) w[j] = wz[j];
+#pragma unroll
+                                for (int k = 0; k < NPT; ++k) {
+                                    pq[k] = 0.0;
+#pragma unroll
+                                    for (int j = 0; j < NPTM; ++j) pq[k] = pq[k] + zmat[k][j] * w[j];
+                                }
+                                itest = 0;
+                            }
+                        }
+                    }
+                    GPD_NW_T1(tmu_, 6);
+                }
+                if (f < fsave) kopt = knew;
+                if (f <= fsave + 0.1 * vquad) {
+                    st = S100;
+                    continue;
+                }
+                if (ksave > 0) {
+                    st = S100;
+                    continue;
+                }
             }
+            knew = 0;
+            st = S460;
         }
-        if (knew > 0) {
-            dstep = fmax(fmin(0.1 * sqrt(distsq), 0.5 * delta), rho);
-            dsq = dstep * dstep;
-            goto L120;
-        }
-    }
-        if (ratio > 0.0) goto L100;
-        if (fmax(delta, dnorm) > rho) goto L100;
-    L490:
-        if (rho > rhoend) {
-            delta = 0.5 * rho;
-            ratio = rho / rhoend;
-            if (ratio <= 16.0) {
-                rho = rhoend;
-            } else if (ratio <= 250.0) {
-                rho = sqrt(ratio) * rhoend;
-            } else {
-                rho = 0.1 * rho;
-            }
-            delta = fmax(delta, rho);
-            goto L90;
-        }
-        if (knew == -1) goto L290;
-    L530:
+        // L530
         finish(x, fopt, f);
         fx = f;
         return nf;
