@@ -71,6 +71,7 @@ enum OptId {
     O_FIT_PROF,      // 1: cycle split of the fit kernels on stderr (diagnostics)
     O_SYNC_DEBUG,    // 1: synchronise after every stage and name the stage that faulted
     O_HOST_PROF,     // 1: wall-clock split of the host-buffer calls on stderr (diagnostics)
+    O_FIT_MCACHE,    // 1: harmonic fit reads the series' moments from LDS where they fit; 0: L2
     O_COUNT
 };
 struct OptDef {
@@ -82,10 +83,11 @@ constexpr OptDef kOpt[O_COUNT] = {
     {"exact_g", 0},      {"exact_waves", 0},   {"exact_wgt", 0},     {"exact_fast", 1},
     {"exact_mcache", 1}, {"xspin_test", 0},    {"units", 0},         {"upw", 0},
     {"fit_lanes", 0},    {"fit_lps", 0},       {"fit_wpb", 0},       {"cohorts", 1},       {"harm_min_span", 256}, {"fs_cohort_mb", 4096},
-    {"moments", 0},      {"fit_prof", 0},      {"sync_debug", 0},    {"host_prof", 0}};
+    {"moments", 0},      {"fit_prof", 0},      {"sync_debug", 0},    {"host_prof", 0},
+    {"fit_mcache", 1}};
 std::atomic<long long> g_opt[O_COUNT] = {{1}, {0}, {0},   {0},    {0}, {0}, {0}, {1}, {1}, {0}, {0},
                                           {0}, {0}, {0},   {0},    {1}, {256}, {4096}, {0}, {0}, {0},
-                                          {0}};
+                                          {0}, {1}};
 inline long long opt(OptId o) { return g_opt[o].load(std::memory_order_relaxed); }
 int opt_find(const char *name) {
     if (!name) return -1;
@@ -202,10 +204,12 @@ struct Layout {
 // fit_wpb override (A/B).
 struct FitShape {
     int lps, gpw, wpb;
+    bool mc;  // the series' moments cached in LDS (k_fit_harmonic<lps, true>)
     unsigned grid;
     size_t lds;
 };
-FitShape fit_shape(long long P, int n_cu) {
+// offs: fitoffsets (the FC columns' moments are cached too)
+FitShape fit_shape(long long P, int n_cu, bool offs) {
     const long long simds = 4LL * std::max(1, n_cu);
     FitShape f{};
     f.lps = 1;
@@ -228,7 +232,13 @@ FitShape fit_shape(long long P, int n_cu) {
     if (opt(O_FIT_WPB) > 0) f.wpb = (int)std::min(4LL, opt(O_FIT_WPB));
     f.wpb = (int)std::max(1LL, std::min<long long>(f.wpb, waves));
     f.grid = (unsigned)((waves + f.wpb - 1) / f.wpb);
-    f.lds = (size_t)f.wpb * (size_t)f.gpw * sizeof(Newuoa<2, 5, true, 1>);
+    const size_t slots = (size_t)f.wpb * (size_t)f.gpw;
+    f.lds = slots * sizeof(Newuoa<2, 5, true, 1>);
+    // the moments in LDS (several lanes per series only: at one lane per series — C3 — the
+    // 64 series of a wave would take 50 KB more per wave, fewer waves per CU); within 128 KB
+    const size_t mlds = slots * (size_t)HARM_ROWS * sizeof(double) * (offs ? 2 : 1);
+    f.mc = f.lps > 1 && opt(O_FIT_MCACHE) != 0 && f.lds + mlds <= 128 * 1024;
+    if (f.mc) f.lds += mlds;
     return f;
 }
 
@@ -247,11 +257,14 @@ hipError_t launch_fit(const FitShape &fs, Problem pb, const Info *info, const do
         kern<<<g, b, fs.lds, s>>>(pb, info, mom, aux, momG, PG, d0, out, raw, list, count);
         e = hipGetLastError();
     };
-    switch (fs.lps) {
-        case 8: go(k_fit_harmonic<8>); break;
-        case 4: go(k_fit_harmonic<4>); break;
-        case 2: go(k_fit_harmonic<2>); break;
-        default: go(k_fit_harmonic<1>); break;
+    switch (fs.lps * 2 + (fs.mc ? 1 : 0)) {
+        case 17: go(k_fit_harmonic<8, true>); break;
+        case 16: go(k_fit_harmonic<8, false>); break;
+        case 9: go(k_fit_harmonic<4, true>); break;
+        case 8: go(k_fit_harmonic<4, false>); break;
+        case 5: go(k_fit_harmonic<2, true>); break;
+        case 4: go(k_fit_harmonic<2, false>); break;
+        default: go(k_fit_harmonic<1, false>); break;
     }
     return e;
 }
@@ -912,7 +925,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             HIP_TRY(hipEventRecord(cx->fork[c], stream));
             HIP_TRY(hipStreamWaitEvent(side, cx->fork[c], 0));
             const int b0 = rec(side);
-            HIP_TRY(launch_fit(fit_shape(n, cx->n_cu), sp, info, mom_c, aux_c, nullptr, n_fc,
+            HIP_TRY(launch_fit(fit_shape(n, cx->n_cu, (sp.flags & F_OFFSETS) != 0), sp, info, mom_c, aux_c, nullptr, n_fc,
                                nullptr, out_c, raw_c, list_c, count_c, side));
             const int b1 = mark_on(side, b0, "fit_harmonic");
             const unsigned xg = (unsigned)std::min<long long>(n, 1024);
@@ -1088,7 +1101,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             HIP_TRY(prof_reset());
             Problem pp = pb;
             pp.flags |= F_PROF;
-            const FitShape fsh = fit_shape(P, cx->n_cu);
+            const FitShape fsh = fit_shape(P, cx->n_cu, (pb.flags & F_OFFSETS) != 0);
             HIP_TRY(launch_fit(fsh, pp, info, mom, aux, momG, n_fc, d0, outp, raw, list, count,
                                stream));
             HIP_TRY(prof_read());
@@ -1099,19 +1112,20 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             const unsigned long long *zn = prof_h + PROF_NW;
             fprintf(stderr, "fit_prof newuoa per series: trsapp %.3g biglag %.3g bigden %.3g "
                     "update %.3g init %.3g vlag/beta %.3g model-update %.3g cycles (lps %d, "
-                    "series per wave %d, waves per workgroup %d)\n",
+                    "series per wave %d, waves per workgroup %d, moments in LDS %d)\n",
                     (double)zn[0] / P, (double)zn[1] / P, (double)zn[2] / P, (double)zn[3] / P,
                     (double)zn[4] / P, (double)zn[5] / P, (double)zn[6] / P, fsh.lps, fsh.gpw,
-                    fsh.wpb);
+                    fsh.wpb, (int)fsh.mc);
             const double nw = (double)((P + fsh.gpw - 1) / fsh.gpw);  // waves
             fprintf(stderr, "fit_prof per wave: objective %.3g trsapp %.3g biglag %.3g update %.3g "
-                    "init %.3g vlag/beta %.3g model-update %.3g cycles, whole fit (max lane) "
-                    "n/a\n", (double)z[4] / nw, (double)zn[8] / nw, (double)zn[9] / nw,
-                    (double)zn[11] / nw, (double)zn[12] / nw, (double)zn[13] / nw,
-                    (double)zn[14] / nw);
+                    "init %.3g vlag/beta %.3g model-update %.3g cycles; whole fit mean %.3g max %.3g "
+                    "cycles over %llu waves\n", (double)z[4] / nw, (double)zn[8] / nw,
+                    (double)zn[9] / nw, (double)zn[11] / nw, (double)zn[12] / nw,
+                    (double)zn[13] / nw, (double)zn[14] / nw, (double)z[5] / (double)(z[7] ? z[7] : 1),
+                    (double)z[6], (unsigned long long)z[7]);
 #endif
         } else {
-            HIP_TRY(launch_fit(fit_shape(P, cx->n_cu), pb, info, mom, aux, momG, n_fc, d0, outp,
+            HIP_TRY(launch_fit(fit_shape(P, cx->n_cu, (pb.flags & F_OFFSETS) != 0), pb, info, mom, aux, momG, n_fc, d0, outp,
                                raw, list, count, stream));
         }
         mark("fit_harmonic");

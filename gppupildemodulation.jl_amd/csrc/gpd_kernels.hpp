@@ -2144,6 +2144,173 @@ __global__ __launch_bounds__(256) void k_moments_win(Problem pb, const double *_
 #endif
 
 
+// Where the moments of the series are read (r5).  HarmG: the moment array in global memory,
+// row q of column col at p[q·ld + col] (through a global-address-space pointer: a generic one
+// makes every wait drain all outstanding loads).  HarmL: the series' 99 rows copied once into
+// LDS by the fit (k_fit_harmonic<LPS, true>), row q at p[q] — an evaluation then waits ~100
+// cycles per batch of reads instead of an L2 round trip (the global form's loads arrive in 5
+// dependent batches per evaluation, 3-5 k cycles of the objective's time).
+struct HarmG {
+    typedef const __attribute__((address_space(1))) double gdouble;
+    const double *p;
+    long long ld, col;
+    __device__ __forceinline__ double operator[](int q) const {
+        return ((gdouble *)p)[(long long)q * ld + col];
+    }
+};
+struct HarmL {
+    const __attribute__((address_space(3))) double *p;
+    __device__ __forceinline__ double operator[](int q) const { return p[q]; }
+};
+constexpr int HARM_ROWS = 3 + 4 * KH;  // rows of a series' moments (F0 re/im, Q2, (A,B,C,D)_n)
+
+// Σ_n J_n(b) e^{-jnϕ} M_n for moments M in the layout of k_moments (F0 re/im at rows 0-1,
+// (A,B,C,D)_n at rows 3+4(n-1)..), canonical order (above), by the L lanes of a group (L = 1:
+// one lane alone; r: the lane's index in its group)
+template <int L, class M>
+__device__ __forceinline__ void harm_combine(const M &m, int r, const double (&J)[KH + 2],
+                                             double cph, double sph, double &Sr, double &Si) {
+    constexpr int NS = 8 / L;
+    double c[9], s[9];
+    c[1] = cph;
+    s[1] = sph;
+#pragma unroll
+    for (int q = 2; q <= 8; ++q) {
+        c[q] = c[q - 1] * cph - s[q - 1] * sph;
+        s[q] = s[q - 1] * cph + c[q - 1] * sph;
+    }
+    const double c8 = c[8], s8 = s[8];
+    double vr[NS], vi[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        // slot j's angle components and Bessel factors: compile-time for L = 1; for L > 1
+        // the slot depends on the lane — captured by compare-and-select against every
+        // candidate (no register array indexed at run time, which would go through scratch)
+        int mi;
+        double cn, sn, jq[3];
+        if constexpr (L == 1) {
+            mi = j + 1;
+            cn = c[mi];
+            sn = s[mi];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) jq[q] = J[mi + 8 * q];
+        } else {
+            mi = r + L * j + 1;
+            cn = c[1];
+            sn = s[1];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) jq[q] = J[1 + 8 * q];
+#pragma unroll
+            for (int mm = 2; mm <= 8; ++mm) {
+                const bool hit = mi == mm;
+                cn = hit ? c[mm] : cn;
+                sn = hit ? s[mm] : sn;
+#pragma unroll
+                for (int q = 0; q < 3; ++q) jq[q] = hit ? J[mm + 8 * q] : jq[q];
+            }
+        }
+        // odd n: the even form with (A', B', C', D') = (B, A, −D, −C) gives fma(B, cn, C sn)
+        // and −fma(D, cn, A sn), bit for bit (negation and ×(±1) are exact)
+        const bool odd = (mi & 1) != 0;
+        const int oA = odd ? 1 : 0, oB = odd ? 0 : 1, oC = odd ? 3 : 2, oD = odd ? 2 : 3;
+        const double sg = odd ? -1.0 : 1.0;
+        double pr = 0.0, pi = 0.0;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int n = mi + 8 * q;
+            if (q > 0) {
+                const double c2 = cn * c8 - sn * s8;
+                const double s2 = sn * c8 + cn * s8;
+                cn = c2;
+                sn = s2;
+            }
+            const int rw = 3 + 4 * (n - 1);
+            const double A = m[rw + oA], B = m[rw + oB];
+            const double C = sg * m[rw + oC], D = sg * m[rw + oD];
+            const double tr = fma(A, cn, -(D * sn));
+            const double ti = fma(C, cn, -(B * sn));
+            const double j2 = 2.0 * jq[q];
+            if (q == 0) {
+                pr = j2 * tr;
+                pi = j2 * ti;
+            } else {
+                pr = fma(j2, tr, pr);
+                pi = fma(j2, ti, pi);
+            }
+        }
+        vr[j] = pr;
+        vi[j] = pi;
+    }
+    // the butterfly over the 8 slots: distance 4, 2, 1 (in-lane while the distance spans
+    // this lane's slots, then across the group's lanes)
+    if constexpr (L <= 4) {
+#pragma unroll
+        for (int j = 0; j < 4 / L; ++j) {
+            vr[j] = vr[j] + vr[j + 4 / L];
+            vi[j] = vi[j] + vi[j + 4 / L];
+        }
+    } else {
+        vr[0] = vr[0] + lane_xor<4>(vr[0]);
+        vi[0] = vi[0] + lane_xor<4>(vi[0]);
+    }
+    if constexpr (L <= 2) {
+#pragma unroll
+        for (int j = 0; j < 2 / L; ++j) {
+            vr[j] = vr[j] + vr[j + 2 / L];
+            vi[j] = vi[j] + vi[j + 2 / L];
+        }
+    } else {
+        vr[0] = vr[0] + lane_xor<2>(vr[0]);
+        vi[0] = vi[0] + lane_xor<2>(vi[0]);
+    }
+    if constexpr (L == 1) {
+        vr[0] = vr[0] + vr[1];
+        vi[0] = vi[0] + vi[1];
+    } else {
+        vr[0] = vr[0] + lane_xor<1>(vr[0]);
+        vi[0] = vi[0] + lane_xor<1>(vi[0]);
+    }
+    Sr = J[0] * m[0] + vr[0];
+    Si = J[0] * m[1] + vi[0];
+}
+
+// The objective's heavy part, out of line (one copy per (L, source) whatever NEWUOA's call sites)
+// with everything it reads passed by value: the Bessel factors, the safe-range checks, sin/cos
+// of the phase and the sums S = Σ w m̄ d (and G = Σ w m̄ for fitoffsets).  bad: the truncated
+// expansion is not exact at this point (→ exact evaluator).
+struct HarmS {
+    double Sr, Si, Gr, Gi;
+    int bad;
+};
+// (OFFS a template parameter: the second combine in the same body raises the one-lane form's
+// registers past 256 — spills in every evaluation of C3's fit)
+template <int L, class M, bool OFFS>
+__device__ __attribute__((noinline)) HarmS harm_core(double b, double phi, M m, M mg, int r,
+                                                     double tailref, double qbase, double phimax) {
+    HarmS o;
+    o.Sr = o.Si = o.Gr = o.Gi = 0.0;
+    o.bad = 0;
+    double J[KH + 2];
+    bessel_j<KH + 1>(b, J);
+    if (!(fabs(b) < 0.45 * KH) || fabs(J[KH + 1]) > tailref) {
+        o.bad = 1;
+        return o;
+    }
+    if (qbase != 0.0) {
+        if (!(fabs(phi) <= phimax)) {  // fl(x + ϕ) may leave the binade: exact evaluator
+            o.bad = 1;
+            return o;
+        }
+        phi = (qbase + phi) - qbase;  // θ = fl(x + ϕ) = x + ϕ_q (one binade)
+    }
+    double sph, cph;
+    jl_sincos(phi, &sph, &cph);
+    harm_combine<L>(m, r, J, cph, sph, o.Sr, o.Si);
+    if constexpr (OFFS) harm_combine<L>(mg, r, J, cph, sph, o.Gr, o.Gi);  // Gm = Σ w m̄ = Σ w p̄ e^{-jβ}
+    else (void)mg;
+    return o;
+}
+
 // χ²(b,ϕ) from the moments of one series, evaluated by a group of LPS consecutive lanes of a
 // wave (LPS ∈ {1, 2, 4, 8}; sub-lane r = lane mod LPS).  The arithmetic is canonical — the
 // same operations in the same order whatever LPS is (r5), so that the records do not depend on
@@ -2157,151 +2324,27 @@ __global__ __launch_bounds__(256) void k_moments_win(Problem pb, const double *_
 // cross-lane exchange, with LPS = 1 every level is in-lane.  (Before r5: one lane per series, the
 // 24 harmonics in one sequential recurrence and fma chain — a different rounding of the same
 // sum, within the harmonic evaluator's stated χ² error.)
-template <int LPS>
+// M: where the moments are read (HarmG / HarmL above); the functor itself is inlined into the
+// fit, so its fields stay in registers.
+template <int LPS, class M = HarmG>
 struct HarmChi2 {
     static_assert(LPS == 1 || LPS == 2 || LPS == 4 || LPS == 8, "lanes per series");
     static constexpr bool kMulti = LPS > 1;  // independent points in parallel (has_multi)
-    const double *__restrict__ mom;
-    long long P, k;
+    M src, srcG;  // the series' moments; fitoffsets: those of its FC phasor (momG)
     double nvalid, W2, DEN, tailref, qbase, phimax;
     double a_re, a_im;
     int nfev;
     int r;  // sub-lane of the group (0 for LPS = 1)
     bool fallback;
-    // fitoffsets (ModulationWithOffsets, src/Modulation.jl:174-192): moments G of the series' FC
-    // phasor (momG[m][g], PG columns), Σw and Σw d
+    // fitoffsets (ModulationWithOffsets, src/Modulation.jl:174-192): Σw and Σw d
     bool offs;
-    const double *__restrict__ momG;
-    long long PG, g;
     double W0, D0r, D0i, c_re, c_im;
 
-    // The moments are read through a global-address-space pointer: reached through this
-    // out-of-line functor, a plain pointer is generic, and flat loads both cost more and make
-    // every wait drain all outstanding loads (flat counts on vmcnt and lgkmcnt).
-    typedef const __attribute__((address_space(1))) double gdouble;
-
-    // Σ_n J_n(b) e^{-jnϕ} M_n for moments M in the layout of k_moments (F0 re/im at rows 0-1,
-    // (A,B,C,D)_n at rows 3+4(n-1)..), canonical order (above)
-    template <int LPS_ = LPS>
-    __device__ __forceinline__ void combine(const double *__restrict__ m_, long long ld, long long col,
-                                            const double (&J)[KH + 2], double cph, double sph,
-                                            double &Sr, double &Si) const {
-        constexpr int L = LPS_;  // lanes evaluating this χ² (1: one lane alone)
-        constexpr int NS = 8 / L;
-        gdouble *p = (gdouble *)m_ + col;  // row q of this series at p[q·ld]
-        double c[9], s[9];
-        c[1] = cph;
-        s[1] = sph;
-#pragma unroll
-        for (int m = 2; m <= 8; ++m) {
-            c[m] = c[m - 1] * cph - s[m - 1] * sph;
-            s[m] = s[m - 1] * cph + c[m - 1] * sph;
-        }
-        const double c8 = c[8], s8 = s[8];
-        double vr[NS], vi[NS];
-#pragma unroll
-        for (int j = 0; j < NS; ++j) {
-            // slot j's angle components and Bessel factors: compile-time for L = 1; for L > 1
-            // the slot depends on the lane — captured by compare-and-select against every
-            // candidate (no register array indexed at run time, which would go through scratch)
-            int m;
-            double cn, sn, jq[3];
-            if constexpr (L == 1) {
-                m = j + 1;
-                cn = c[m];
-                sn = s[m];
-#pragma unroll
-                for (int q = 0; q < 3; ++q) jq[q] = J[m + 8 * q];
-            } else {
-                m = r + L * j + 1;
-                cn = c[1];
-                sn = s[1];
-#pragma unroll
-                for (int q = 0; q < 3; ++q) jq[q] = J[1 + 8 * q];
-#pragma unroll
-                for (int mm = 2; mm <= 8; ++mm) {
-                    const bool hit = m == mm;
-                    cn = hit ? c[mm] : cn;
-                    sn = hit ? s[mm] : sn;
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) jq[q] = hit ? J[mm + 8 * q] : jq[q];
-                }
-            }
-            // odd n: the even form with (A', B', C', D') = (B, A, −D, −C) gives fma(B, cn, C sn)
-            // and −fma(D, cn, A sn), bit for bit (negation and ×(±1) are exact)
-            const bool odd = (m & 1) != 0;
-            const int oA = odd ? 1 : 0, oB = odd ? 0 : 1, oC = odd ? 3 : 2, oD = odd ? 2 : 3;
-            const double sg = odd ? -1.0 : 1.0;
-            double pr = 0.0, pi = 0.0;
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                const int n = m + 8 * q;
-                if (q > 0) {
-                    const double c2 = cn * c8 - sn * s8;
-                    const double s2 = sn * c8 + cn * s8;
-                    cn = c2;
-                    sn = s2;
-                }
-                gdouble *rw = p + (long long)(3 + 4 * (n - 1)) * ld;
-                const double A = rw[oA * ld], B = rw[oB * ld];
-                const double C = sg * rw[oC * ld], D = sg * rw[oD * ld];
-                const double tr = fma(A, cn, -(D * sn));
-                const double ti = fma(C, cn, -(B * sn));
-                const double j2 = 2.0 * jq[q];
-                if (q == 0) {
-                    pr = j2 * tr;
-                    pi = j2 * ti;
-                } else {
-                    pr = fma(j2, tr, pr);
-                    pi = fma(j2, ti, pi);
-                }
-            }
-            vr[j] = pr;
-            vi[j] = pi;
-        }
-        // the butterfly over the 8 slots: distance 4, 2, 1 (in-lane while the distance spans
-        // this lane's slots, then across the group's lanes)
-        if constexpr (L <= 4) {
-#pragma unroll
-            for (int j = 0; j < 4 / L; ++j) {
-                vr[j] = vr[j] + vr[j + 4 / L];
-                vi[j] = vi[j] + vi[j + 4 / L];
-            }
-        } else {
-            vr[0] = vr[0] + lane_xor<4>(vr[0]);
-            vi[0] = vi[0] + lane_xor<4>(vi[0]);
-        }
-        if constexpr (L <= 2) {
-#pragma unroll
-            for (int j = 0; j < 2 / L; ++j) {
-                vr[j] = vr[j] + vr[j + 2 / L];
-                vi[j] = vi[j] + vi[j + 2 / L];
-            }
-        } else {
-            vr[0] = vr[0] + lane_xor<2>(vr[0]);
-            vi[0] = vi[0] + lane_xor<2>(vi[0]);
-        }
-        if constexpr (L == 1) {
-            vr[0] = vr[0] + vr[1];
-            vi[0] = vi[0] + vi[1];
-        } else {
-            vr[0] = vr[0] + lane_xor<1>(vr[0]);
-            vi[0] = vi[0] + lane_xor<1>(vi[0]);
-        }
-        Sr = J[0] * p[0] + vr[0];
-        Si = J[0] * p[ld] + vi[0];
-    }
-
-    // one out-of-line copy: NEWUOA calls the objective from several sites, and each inlined
-    // copy of the Bessel recurrence + 24-harmonic sum adds its own live registers
     unsigned long long prof_cycles, prof_wave;  // lane-level / wave-level (first active lane)
     bool prof;
 
-#ifndef GPD_FIT_OBJ_ATTR
-#define GPD_FIT_OBJ_ATTR __attribute__((noinline))
-#endif
-    __device__ GPD_FIT_OBJ_ATTR double operator()(const double (&x)[2]) {
-        // one inlined copy of eval (the cycle split only brackets it)
+    __device__ __forceinline__ double operator()(const double (&x)[2]) {
+        // the cycle split brackets the evaluation
         const unsigned long long t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
         const double v = eval<LPS>(x);
         if (prof) {
@@ -2312,7 +2355,7 @@ struct HarmChi2 {
         return v;
     }
     // the same χ² evaluated by this lane alone (LPS = 1 form of the canonical arithmetic)
-    __device__ GPD_FIT_OBJ_ATTR double single(const double (&x)[2]) { return eval<1>(x); }
+    __device__ __forceinline__ double single(const double (&x)[2]) { return eval<1>(x); }
     // NP independent points: lane r of the group evaluates points r, r + LPS, … alone; every
     // lane then holds every value (shuffled from its owner), nfev counts NP evaluations and a
     // fallback anywhere in the group is the group's
@@ -2349,30 +2392,17 @@ struct HarmChi2 {
     __device__ __forceinline__ double eval(const double (&x)[2]) {
         ++nfev;
         if (fallback) return 0.0;
-        const double b = x[0];
-        double phi = x[1];
-        double J[KH + 2];
-        bessel_j<KH + 1>(b, J);
-        if (!(fabs(b) < 0.45 * KH) || fabs(J[KH + 1]) > tailref) {
+        const HarmS h = offs ? harm_core<LPS_, M, true>(x[0], x[1], src, srcG, r, tailref, qbase, phimax)
+                             : harm_core<LPS_, M, false>(x[0], x[1], src, srcG, r, tailref, qbase, phimax);
+        if (h.bad) {
             fallback = true;  // truncated expansion not exact here → exact evaluator
             return 0.0;
         }
-        if (qbase != 0.0) {
-            if (!(fabs(phi) <= phimax)) {  // fl(x + ϕ) may leave the binade: exact evaluator
-                fallback = true;
-                return 0.0;
-            }
-            phi = (qbase + phi) - qbase;  // θ = fl(x + ϕ) = x + ϕ_q (one binade)
-        }
-        double sph, cph;
-        jl_sincos(phi, &sph, &cph);
-        double Sr, Si;  // S = Σ w m̄ d
-        combine<LPS_>(mom, P, k, J, cph, sph, Sr, Si);
+        const double Sr = h.Sr, Si = h.Si;  // S = Σ w m̄ d
         if (offs) {
             // [Σw  Σw m; Σw m̄  Σw|m|²] [c; a] = [Σw d; Σw m̄ d], StaticArrays 2×2 solve as in the
             // exact evaluator; Nχ² = Σw|d|² − Re(c̄ Σw d + ā S) at the solution
-            double Gr, Gi;  // Gm = Σ w m̄ = Σ w p̄ e^{-jβ}
-            combine<LPS_>(momG, PG, g, J, cph, sph, Gr, Gi);
+            const double Gr = h.Gr, Gi = h.Gi;
             const c64 A11 = {W0, 0.0}, A12 = {Gr, -Gi}, A21 = {Gr, Gi}, A22 = {DEN, 0.0};
             const c64 b1 = {D0r, D0i}, b2 = {Sr, Si};
             const c64 t1 = cmul(A11, A22), t2 = cmul(A12, A21);
@@ -2397,30 +2427,29 @@ struct HarmChi2 {
 
 // k_fit_harmonic: lane = series.  Series whose NEWUOA probes leave the expansion's safe
 // range are appended to `list` for the exact evaluator.
-// Offsets fields of the objective (fitoffsets, non-faint): G moments of the FC columns and
-// Σ d of the series.
+// Offsets fields of the objective (fitoffsets, non-faint): Σw and Σ d of the series (the G
+// moments of its FC column are the caller's srcG).
 template <class F>
 __device__ __forceinline__ void harm_offsets(F &f, const Problem &pb, long long k,
-                                             const double *__restrict__ momG, long long PG,
                                              const double *__restrict__ d0) {
     f.offs = (pb.flags & F_OFFSETS) != 0;
     f.c_re = f.c_im = 0.0;
     if (!f.offs) return;
-    f.momG = momG;
-    f.PG = PG;
-    f.g = pb.fcop[k];
     f.W0 = f.nvalid;  // Σ w (w ≡ 1)
     f.D0r = d0[2 * k];
     f.D0i = d0[2 * k + 1];
 }
 
-// k_fit_harmonic<LPS>: a group of LPS lanes per series (the canonical objective above and
+// k_fit_harmonic<LPS, MC>: a group of LPS lanes per series (the canonical objective above and
 // NEWUOA's trial-angle searches split across the group; NEWUOA itself runs replicated on the
 // group's lanes, its state shared in LDS), pb.fit_lanes series per wave, blockDim.x / 64 waves
 // per workgroup (a workgroup's waves are placed on different SIMDs of one CU).  Dynamic LDS:
-// one NEWUOA state (71 doubles, odd 8-byte stride) per series of the workgroup.  Series whose
-// NEWUOA probes leave the expansion's safe range are appended to `list` for the exact evaluator.
-template <int LPS>
+// one NEWUOA state (71 doubles, odd 8-byte stride) per series of the workgroup, then with MC the
+// series' moments (HARM_ROWS doubles per series, odd stride; fitoffsets: then those of their FC
+// columns), copied in by the group's lanes before the fit — the objective reads them there
+// (HarmL).  Series whose NEWUOA probes leave the expansion's safe range are appended to `list`
+// for the exact evaluator.
+template <int LPS, bool MC>
 __global__ __launch_bounds__(256, 1) void k_fit_harmonic(Problem pb, const Info *__restrict__ info,
                                                          const double *__restrict__ mom,
                                                          const double *__restrict__ aux,
@@ -2431,6 +2460,8 @@ __global__ __launch_bounds__(256, 1) void k_fit_harmonic(Problem pb, const Info 
 #if GPD_OWNS(GPD_U_FITH)
 {
     typedef Newuoa<2, 5, true, LPS> NW;
+    typedef __attribute__((address_space(3))) double ldouble;
+    typedef typename std::conditional<MC, HarmL, HarmG>::type Src;
     extern __shared__ __attribute__((aligned(16))) double fit_lds[];
     const int lane = (int)threadIdx.x & 63, wv = (int)threadIdx.x >> 6;
     const int gpw = pb.fit_lanes > 0 ? pb.fit_lanes : 64 / LPS;  // series per wave
@@ -2438,7 +2469,8 @@ __global__ __launch_bounds__(256, 1) void k_fit_harmonic(Problem pb, const Info 
     if (grp >= gpw) return;
     const long long k = ((long long)blockIdx.x * (blockDim.x >> 6) + wv) * gpw + grp;
     if (k >= pb.P) return;
-    NW &nw = ((NW *)fit_lds)[wv * gpw + grp];
+    const int slot = wv * gpw + grp;
+    NW &nw = ((NW *)fit_lds)[slot];
     const Info in = *info;
     const Span sp = span_of(pb, k);
     // harmonic path unusable for these timestamps, or a short (last) window: exact fit
@@ -2446,10 +2478,7 @@ __global__ __launch_bounds__(256, 1) void k_fit_harmonic(Problem pb, const Info 
         if (r == 0) list[atomicAdd(count, 1)] = (int)k;
         return;
     }
-    HarmChi2<LPS> f;
-    f.mom = mom;
-    f.P = pb.P;
-    f.k = k;
+    HarmChi2<LPS, Src> f;
     f.r = r;
     f.nvalid = aux[4 * k + 3];
     f.W2 = aux[4 * k + 0];
@@ -2462,7 +2491,28 @@ __global__ __launch_bounds__(256, 1) void k_fit_harmonic(Problem pb, const Info 
     f.a_re = f.a_im = 0.0;
     f.nfev = 0;
     f.fallback = false;
-    harm_offsets(f, pb, k, momG, PG, d0);
+    harm_offsets(f, pb, k, d0);
+    const long long g = f.offs ? (long long)pb.fcop[k] : 0;
+    if constexpr (MC) {
+        const int nsl = (int)(blockDim.x >> 6) * gpw;  // series slots of the workgroup
+        ldouble *cache = (ldouble *)((char *)fit_lds + (size_t)nsl * sizeof(NW));
+        ldouble *cs = cache + (size_t)slot * HARM_ROWS;
+        for (int q = r; q < HARM_ROWS; q += LPS) cs[q] = mom[(long long)q * pb.P + k];
+        f.src.p = cs;
+        f.srcG.p = cs;
+        if (f.offs) {
+            ldouble *cg = cache + (size_t)(nsl + slot) * HARM_ROWS;
+            for (int q = r; q < HARM_ROWS; q += LPS) cg[q] = momG[(long long)q * PG + g];
+            f.srcG.p = cg;
+        }
+        // the group's lanes read each other's rows: one wave, LDS in issue order
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        f.src = HarmG{mom, pb.P, k};
+        f.srcG = f.offs ? HarmG{momG, PG, g} : f.src;
+    }
     f.prof = (pb.flags & F_PROF) != 0;
     f.prof_cycles = f.prof_wave = 0;
     const unsigned long long tfit = f.prof ? __builtin_amdgcn_s_memtime() : 0;
@@ -2473,6 +2523,16 @@ __global__ __launch_bounds__(256, 1) void k_fit_harmonic(Problem pb, const Info 
     for (int q = 0; q < 16; ++q) nw.prof_[q] = 0;
 #endif
     drive_fit(f, pb, x, status, nw);
+#ifdef GPD_DIAG
+    if (f.prof) {  // the wave's fit time (its lanes meet again here): mean and max over waves
+        const unsigned long long tw = __builtin_amdgcn_s_memtime() - tfit;
+        if ((int)threadIdx.x == __builtin_amdgcn_readfirstlane((int)threadIdx.x)) {
+            atomicAdd(&pb.prof[PROF_FIT + 5], tw);
+            atomicMax(&pb.prof[PROF_FIT + 6], tw);
+            atomicAdd(&pb.prof[PROF_FIT + 7], 1ull);
+        }
+    }
+#endif
     const double chi2 = f(x);  // likelihood[idx] = lkl(x) (src/Modulation.jl:416)
     if (f.prof && r == 0) {
         atomicAdd(&pb.prof[PROF_FIT + 0], f.prof_cycles);
@@ -3483,9 +3543,6 @@ __global__ __launch_bounds__(64) void k_chi2_harmonic(Problem pb, const Info *__
     const Info in = *info;
     HarmChi2<1> f;
     f.r = 0;
-    f.mom = mom;
-    f.P = pb.P;
-    f.k = k;
     f.nvalid = aux[4 * k + 3];
     f.W2 = aux[4 * k + 0];
     f.DEN = aux[4 * k + 1];
@@ -3496,7 +3553,9 @@ __global__ __launch_bounds__(64) void k_chi2_harmonic(Problem pb, const Info *__
     f.nfev = 0;
     f.fallback = in.mode == 2;
     f.prof = false;
-    harm_offsets(f, pb, k, momG, PG, d0);
+    harm_offsets(f, pb, k, d0);
+    f.src = HarmG{mom, pb.P, k};
+    f.srcG = f.offs ? HarmG{momG, PG, (long long)pb.fcop[k]} : f.src;
     double x[2] = {bphi[2 * k], bphi[2 * k + 1]};
     const double chi2 = f(x);
     Param p;

@@ -5,6 +5,8 @@
 
 namespace gpd {
 __attribute__((used)) void *const k_fit_harmonic_units[] = {
-    (void *)&k_fit_harmonic<1>, (void *)&k_fit_harmonic<2>, (void *)&k_fit_harmonic<4>,
-    (void *)&k_fit_harmonic<8>};
+    (void *)&k_fit_harmonic<1, false>, (void *)&k_fit_harmonic<2, false>,
+    (void *)&k_fit_harmonic<4, false>, (void *)&k_fit_harmonic<8, false>,
+    (void *)&k_fit_harmonic<2, true>,  (void *)&k_fit_harmonic<4, true>,
+    (void *)&k_fit_harmonic<8, true>};
 }  // namespace gpd
