@@ -449,17 +449,36 @@ def c2_block(gpd, t, d, fc, args, log, reps=5):
             ts.append(time.perf_counter() - t1)
         return round(1e3 * float(np.median(ts)), 3), gpd.timings(0)
 
+    # demodulateall returns a fresh N x 40 output per call (as the reference does): its pages
+    # are faulted inside the call; the previous result's release (numpy unmapping 64 MB the
+    # library's copy threads touched) is the caller's garbage collection, timed apart — each
+    # call's result is kept until the timed calls are over
+    def med_kept(fn):
+        keep = [fn()]
+        ts = []
+        for _ in range(reps):
+            t1 = time.perf_counter()
+            keep.append(fn())
+            ts.append(time.perf_counter() - t1)
+        n = len(keep)
+        t1 = time.perf_counter()
+        keep.clear()
+        rel = (time.perf_counter() - t1) / n
+        return round(1e3 * float(np.median(ts)), 3), gpd.timings(0), round(1e3 * rel, 3)
+
     cases = {}
     ms, k = med(lambda: gpd.fit_batch(th, cols[:32], cols, fop))
     cases["fit_only"] = {"host_call_ms": ms, "what": "gpd_fit_batch, records only"}
     kern = k
-    ms, k = med(lambda: gpd.demodulateall(th, data))
-    cases["demodulateall"] = {"host_call_ms": ms,
+    ms, k, rel = med_kept(lambda: gpd.demodulateall(th, data))
+    cases["demodulateall"] = {"host_call_ms": ms, "release_of_the_output_ms": rel,
                               "what": "output = copy(data) with the 32 demodulated columns "
-                                      "written in place, records, likelihood"}
-    ms, k = med(lambda: gpd.demodulateall(th, data, fitoffsets=True))
+                                      "written in place, records, likelihood (a fresh output "
+                                      "per call; its release by the caller timed apart)"}
+    ms, k, rel = med_kept(lambda: gpd.demodulateall(th, data, fitoffsets=True))
     cases["demodulateall_fitoffsets"] = {
-        "host_call_ms": ms, "kernels_ms": {a: round(b, 3) for a, b in k.items()},
+        "host_call_ms": ms, "release_of_the_output_ms": rel,
+        "kernels_ms": {a: round(b, 3) for a, b in k.items()},
         "what": "--center fit (ModulationWithOffsets): the exact evaluator by default"}
     nwin = gpd.window_length(th, 1.0)
     out = cols.copy()

@@ -1043,16 +1043,19 @@ __device__ __forceinline__ bool fst_valid(unsigned flags, int st) {
 // fma-formed |q|² by v_rsq_f64 and one Goldschmidt correction (≤ 1 ulp; no rescaling — |q|²
 // stays far from the subnormal and overflow ranges for metrology voltages; 0 → 0, Inf → NaN).
 // The statistics are a restatement with a stated tolerance (oracle: faint_stats_fused in
-// demod_oracle.c forms the same sums from Julia's hypot), not a bit-for-bit one.
+// demod_oracle.c forms the same sums from Julia's hypot), not a bit-for-bit one.  r5: 0 → 0
+// through rsq of max(|q|², DBL_MIN) (g = 0·y stays 0 through the corrections) instead of a
+// compare and two selects — the same bits for every |q|² ≥ DBL_MIN (the hardware v_sqrt_f64
+// would be cheaper still but is ~2^-25 relative: tools/probes/sqrt_ulp.hip).
 __device__ __forceinline__ double fs_abs(double re, double im) {
     const double r2 = fma(re, re, im * im);
-    const double y = __builtin_amdgcn_rsq(r2);
+    const double y = __builtin_amdgcn_rsq(fmax(r2, 0x1p-1022));
     double g = r2 * y, h = 0.5 * y;
     const double r = fma(-g, h, 0.5);
     g = fma(g, r, g);
     h = fma(h, r, h);
     g = fma(fma(-g, g, r2), h, g);
-    return r2 == 0.0 ? 0.0 : g;
+    return g;
 }
 
 // One complex element of storage type TS (c64: 16 B, c32: 8 B) through a buffer descriptor;
@@ -1253,28 +1256,15 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             T2 = __builtin_bit_cast(double2,
                                     __builtin_amdgcn_raw_buffer_load_b128(trs, vo + 8192, 0, 0));
         };
-        auto stage_q = [&](const WsRegs<TS> &R, int it, auto gen, auto partial) __attribute__((always_inline)) {
+        // masked: zero the q of samples outside the tile's state (FAINT) or past the chunk end
+        auto stage_q = [&](const WsRegs<TS> &R, int it, auto gen, auto masked, bool sok) __attribute__((always_inline)) {
             const long long s = s_begin + (long long)it * MM_TS + ss;
-            bool sok = s < s_end;
             const long long sl = s < Nm1 ? s : Nm1;
             // mm_phys(4(gq + 8r) + j, ss) = q_base + 32r + j: the swizzle (bit 3 of the series)
             // only touches 4·gq's bits, so the 16 stores share one address and immediate offsets
             // (written per (r, j), the compiler kept an address register each — the faint variant
             // spilled them, and every spill reload waited for the tile prefetch: vmcnt(0))
             c64 *q_out = qs[it & 1] + (ss * MM_ROW + ((4 * gq) ^ ((ss & 1) << 3)));
-            if constexpr (FAINT) {
-                const int st = R.st;
-                const bool v = sok && fst_valid(pb.flags, st);
-                // lanes l and l + 32 hold the same sample: bits 0..31 are the tile's samples
-                const unsigned b32 = (unsigned)__builtin_amdgcn_ballot_w64(v);
-                const int ds = b32 ? __builtin_amdgcn_readlane(st, __builtin_ctz(b32)) : -1;
-                sok = v && st == ds;
-                const unsigned okm = (unsigned)__builtin_amdgcn_ballot_w64(sok);
-                if (ptid == 0) {
-                    tds[it & 1] = ds;
-                    tmk[it & 1] = okm;
-                }
-            }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const c64 ph = unit_phasor(widen(R.f[r]));
@@ -1292,7 +1282,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
                         q.re = fma(pj.re, dv.re, pj.im * dv.im);
                         q.im = fma(pj.re, dv.im, -(pj.im * dv.re));
                     }
-                    if (FAINT || decltype(partial)::value) {  // rows beyond P read as 0 already
+                    if (decltype(masked)::value) {  // rows beyond P read as 0 already
                         q.re = sok ? q.re : 0.0;
                         q.im = sok ? q.im : 0.0;
                     }
@@ -1303,11 +1293,30 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
         auto stage = [&](const WsRegs<TS> &R, int it, auto gen) __attribute__((always_inline)) {
             if (it >= ntiles) return;
             if constexpr (DBG == 5) return;
+            const long long s = s_begin + (long long)it * MM_TS + ss;
+            bool sok = s < s_end;
             // only a chunk's last tile can be partial (chunks are whole tiles, N may not be)
-            if (s_begin + (long long)(it + 1) * MM_TS <= s_end)  // uniform
-                stage_q(R, it, gen, BoolTag<false>{});
+            bool whole = s_begin + (long long)(it + 1) * MM_TS <= s_end;  // uniform
+            if constexpr (FAINT) {
+                const int st = R.st;
+                const bool v = sok && fst_valid(pb.flags, st);
+                // lanes l and l + 32 hold the same sample: bits 0..31 are the tile's samples
+                const unsigned b32 = (unsigned)__builtin_amdgcn_ballot_w64(v);
+                const int ds = b32 ? __builtin_amdgcn_readlane(st, __builtin_ctz(b32)) : -1;
+                sok = v && st == ds;
+                const unsigned okm = (unsigned)__builtin_amdgcn_ballot_w64(sok);
+                if (ptid == 0) {
+                    tds[it & 1] = ds;
+                    tmk[it & 1] = okm;
+                }
+                // every sample of the tile valid and of one state (most tiles of a faint
+                // series: states change only at the few shutter switches) — nothing to mask
+                whole = okm == 0xffffffffu;
+            }
+            if (whole)
+                stage_q(R, it, gen, BoolTag<false>{}, sok);
             else
-                stage_q(R, it, gen, BoolTag<true>{});
+                stage_q(R, it, gen, BoolTag<true>{}, sok);
             double2 *tsb = (double2 *)ts[it & 1] + ptid;
             tsb[0] = T0;
             tsb[256] = T1;
