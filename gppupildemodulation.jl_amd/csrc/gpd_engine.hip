@@ -999,6 +999,13 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             }
             if (faint && is_c32 && tmix)  // faint series: the producer/consumer kernel, state-split
                 k_moments_ws<0, false, c32, 2, true, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, smask, fsp, fcnt, dhdr);
+#ifdef GPD_DIAG
+            // timing variants of the faint kernel (results invalid), diagnostics build only
+            else if (faint && tmix && mk == 9)
+                k_moments_ws<9, false, c64, 2, true, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, smask, fsp, fcnt, dhdr);
+            else if (faint && tmix && mk == 10)
+                k_moments_ws<10, false, c64, 2, true, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, smask, fsp, fcnt, dhdr);
+#endif
             else if (faint && tmix)
                 k_moments_ws<0, false, c64, 2, true, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, smask, fsp, fcnt, dhdr);
             else if (faint && is_c32)

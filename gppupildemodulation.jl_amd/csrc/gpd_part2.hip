@@ -18,6 +18,8 @@ __attribute__((used)) void *const k_moments_ws_c64_units[] = {
 #ifdef GPD_DIAG
     (void *)&k_moments_ws<1>, (void *)&k_moments_ws<2>, (void *)&k_moments_ws<5>,
     (void *)&k_moments_ws<6>, (void *)&k_moments_ws<7>, (void *)&k_moments_ws<8>,
+    (void *)&k_moments_ws<9, false, c64, 2, true, true>,   // faint without the fused statistics
+    (void *)&k_moments_ws<10, false, c64, 2, true, true>,  // faint, producers without masking
 #endif
 };
 #else
