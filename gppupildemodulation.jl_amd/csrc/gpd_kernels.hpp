@@ -1097,7 +1097,8 @@ struct WsRegs {
 
 // DBG (timing experiments only, results invalid): 1 = consumers skip the MFMA phase,
 // 7 = consumers skip the F0/Σ|q|² VALU, 8 = producers stage d without forming q = p̄ d,
-// 2 = producers skip the global loads, 5 = producers only keep the barrier cadence.
+// 2 = producers skip the global loads, 5 = producers only keep the barrier cadence;
+// FAINT: 9 = no fused statistics, 10 = no masking of the staged q.
 // UNIT: the series are FC columns and d ≡ 1, i.e. the moments G_n = Σ p̄ e^{-jnx} of the
 // unit phasors (harmonic fitoffsets: Σ w m = conj(Σ_n J_n(b) e^{-jnϕ} G_n)).
 // MIX (production): harmonics 1..16 on the f64 MFMAs (2 column tiles), harmonics 17..24 on
@@ -1313,7 +1314,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
                 // series: states change only at the few shutter switches) — nothing to mask
                 whole = okm == 0xffffffffu;
             }
-            if (whole)
+            if (whole || DBG == 10)  // (DBG 10: timing only, masks dropped)
                 stage_q(R, it, gen, BoolTag<false>{}, sok);
             else
                 stage_q(R, it, gen, BoolTag<true>{}, sok);
@@ -1351,7 +1352,7 @@ __global__ __launch_bounds__(512, 1) void k_moments_ws(Problem pb, const double 
             fs_n = 0;
         };
         auto fs_tile = [&](int i) __attribute__((always_inline)) {
-            if constexpr (FAINT && DBG == 0) {
+            if constexpr (FAINT && (DBG == 0 || DBG == 10)) {
                 const int ds = __builtin_amdgcn_readfirstlane(tds[i & 1]);
                 const unsigned mk = (unsigned)__builtin_amdgcn_readfirstlane((int)tmk[i & 1]);
                 if (ds >= 0 && ds != fs_cs) {  // uniform
