@@ -176,6 +176,26 @@ def test_series_per_fit_wave_does_not_change_records(gpu, opts):
     assert fallbacks > 0
 
 
+def test_fit_moment_source_does_not_change_records(gpu, opts):
+    """With several lanes per series the harmonic fit reads each series' moments (and, with
+    fitoffsets, its FC column's) from a copy in LDS (option fit_mcache, default 1) instead of
+    L2: the same values, so the same records, for every multi-lane shape, with and without
+    fitoffsets (r5)."""
+    N, P = 20_000, 64
+    B = synth.make_batch(N, P, seed=5, b_range=(0.3, 4.0))
+    args = (B["t"], B["d"], B["fc"], B["fc_of_pixel"])
+    for offs in (False, True):
+        for lps, lanes, wpb in ((2, 8, 1), (4, 3, 2), (4, 16, 4), (8, 1, 1), (8, 8, 4)):
+            gpu.reset_options()
+            opts("fit_lps", lps)
+            opts("fit_lanes", lanes)
+            opts("fit_wpb", wpb)
+            a = gpu.fit_batch(*args, method="harmonic", fitoffsets=offs)
+            opts("fit_mcache", 0)
+            b = gpu.fit_batch(*args, method="harmonic", fitoffsets=offs)
+            _same(a, b)
+
+
 def test_faint_state_pointer_alignment(gpu):
     """The state-split faint moments read each tile's 32 state bytes in 16-B loads only when the
     caller's state array is 16-B aligned (k_faint_defer); a state view at an odd byte offset
