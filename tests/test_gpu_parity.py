@@ -251,6 +251,34 @@ def test_faint_matches_oracle(gpu, oracle, method, onlyhigh):
     print(assert_fit_parity(got, ref, pert, label=f"faint/{method}/onlyhigh={onlyhigh}"))
 
 
+@pytest.mark.parametrize("method", ["exact", "harmonic"])
+@pytest.mark.parametrize("onlyhigh", [False, True])
+def test_faint_excluded_samples_do_not_reach_the_fit(gpu, method, onlyhigh):
+    """demodulateall fits only the valid samples (src/Modulation.jl:373-382: TRANSIENT always
+    dropped, and with onlyhigh everything but HIGH/NORMAL): NaN data and NaN FC samples at
+    excluded samples must change nothing — the same records bit for bit as the same exposure
+    with finite values there (the moment pass masks or skips them, the statistics and the exact
+    evaluator never read them as valid)."""
+    B, st = faint_batch(6000, 32, seed=31)
+    excluded = st == -1
+    if onlyhigh:
+        excluded |= ~np.isin(st, (2, 3))
+    idx = np.flatnonzero(excluded)
+    assert idx.size > 100
+    ref = fit(gpu, B, state=st, method=method, onlyhigh=onlyhigh)
+    Bn = dict(B)
+    Bn["d"] = B["d"].copy()
+    Bn["fc"] = B["fc"].copy()
+    rng = np.random.default_rng(7)
+    hit = rng.choice(idx, size=min(200, idx.size), replace=False)
+    Bn["d"][:, hit] = complex(np.nan, np.nan)
+    Bn["fc"][:, hit[::3]] = complex(np.nan, 0.0)
+    got = fit(gpu, Bn, state=st, method=method, onlyhigh=onlyhigh)
+    assert not np.any(np.isnan(ref["chi2"]))
+    for k in ("c", "a", "b", "phi", "chi2", "nfev", "status"):
+        assert np.array_equal(got[k], ref[k]), k
+
+
 def test_faint_single_sample_state_gives_nan(gpu, oracle):
     """var of a 1-sample state is NaN → NaN weights → NaN fit (src/Faint.jl:97)."""
     B = synth.make_batch(2000, 4, seed=2)
