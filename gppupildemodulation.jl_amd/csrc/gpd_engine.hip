@@ -72,8 +72,6 @@ enum OptId {
     O_SYNC_DEBUG,    // 1: synchronise after every stage and name the stage that faulted
     O_HOST_PROF,     // 1: wall-clock split of the host-buffer calls on stderr (diagnostics)
     O_FIT_MCACHE,    // 1: harmonic fit reads the series' moments from LDS where they fit; 0: L2
-    O_FIT_DEFER,     // 1: π-flip re-fits of the harmonic fit in a second launch; 0: in place
-    O_FIT_WPC,       // 0: automatic; n: at most n harmonic-fit waves per CU (LDS reserved, A/B)
     O_COUNT
 };
 struct OptDef {
@@ -86,10 +84,10 @@ constexpr OptDef kOpt[O_COUNT] = {
     {"exact_mcache", 1}, {"xspin_test", 0},    {"units", 0},         {"upw", 0},
     {"fit_lanes", 0},    {"fit_lps", 0},       {"fit_wpb", 0},       {"cohorts", 1},       {"harm_min_span", 256}, {"fs_cohort_mb", 4096},
     {"moments", 0},      {"fit_prof", 0},      {"sync_debug", 0},    {"host_prof", 0},
-    {"fit_mcache", 1},   {"fit_defer", 1},     {"fit_wpc", 0}};
+    {"fit_mcache", 1}};
 std::atomic<long long> g_opt[O_COUNT] = {{1}, {0}, {0},   {0},    {0}, {0}, {0}, {1}, {1}, {0}, {0},
                                           {0}, {0}, {0},   {0},    {1}, {256}, {4096}, {0}, {0}, {0},
-                                          {0}, {1}, {1}, {0}};
+                                          {0}, {1}};
 inline long long opt(OptId o) { return g_opt[o].load(std::memory_order_relaxed); }
 int opt_find(const char *name) {
     if (!name) return -1;
@@ -171,7 +169,7 @@ size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
 struct Layout {
     size_t info, prof, tab, part, mom, aux, fstat, raw, list, phbuf, partG, momG, auxG, fcid, d0,
-        mcache, xtot, xcnt, fsx, fsc, xr32, refit, total;
+        mcache, xtot, xcnt, fsx, fsc, xr32, total;
     long long mstride;  // model-cache elements per exact-path workgroup (0: no cache)
     int nch;            // sample chunks of the moment grid (grid.y)
     long long chunk;    // samples per chunk (a whole number of units)
@@ -241,60 +239,32 @@ FitShape fit_shape(long long P, int n_cu, bool offs) {
     const size_t mlds = slots * (size_t)HARM_ROWS * sizeof(double) * (offs ? 2 : 1);
     f.mc = f.lps > 1 && opt(O_FIT_MCACHE) != 0 && f.lds + mlds <= 128 * 1024;
     if (f.mc) f.lds += mlds;
-    if (opt(O_FIT_WPC) > 0) {  // A/B: at most n waves per CU, by reserving LDS
-        const long long wg = std::max(1LL, opt(O_FIT_WPC) / f.wpb);  // workgroups per CU
-        const size_t need = (size_t)160 * 1024 / (size_t)(wg + 1) + 2048;
-        if (f.lds < need) f.lds = need;
-    }
     return f;
 }
 
-// The harmonic fit in shape fs.  With option fit_defer (default) and at least kDeferMin series,
-// a series whose first NEWUOA run lands in a "bad minimum" (src/Modulation.jl:411-414) leaves
-// its π-flip re-fit to a second launch over the listed re-fits at several lanes per series: in
-// place, such a series doubles its wave's time and, when that wave runs last, the kernel's
-// (~5 re-fits per 1e5 synthetic series; C3 2.24 → 2.17 ms).  The second launch costs ~0.03 ms
-// when the list is empty, so a small batch, unlikely to hold a re-fit, keeps it in place.  Same
-// operations, same records.  *rcount is zeroed by the caller.
-constexpr long long kDeferMin = 2048;
 hipError_t launch_fit(const FitShape &fs, Problem pb, const Info *info, const double *mom,
                       const double *aux, const double *momG, long long PG, const double *d0,
-                      Param *out, double *raw, int *list, int *count, Refit *refit, int *rcount,
-                      int n_cu, hipStream_t s) {
+                      Param *out, double *raw, int *list, int *count, hipStream_t s) {
+    pb.fit_lanes = fs.gpw;
+    const dim3 g(fs.grid), b(64 * fs.wpb);
     hipError_t e = hipSuccess;
-    auto go = [&](const FitShape &sh, Problem p, auto kern) {
-        p.fit_lanes = sh.gpw;
-        if (sh.lds > 48 * 1024) {  // beyond the default dynamic-LDS limit (C3: 4 × 64 states)
+    auto go = [&](auto kern) {
+        if (fs.lds > 48 * 1024) {  // beyond the default dynamic-LDS limit (C3: 4 × 64 states)
             e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)sh.lds);
+                                    (int)fs.lds);
             if (e != hipSuccess) return;
         }
-        kern<<<dim3(sh.grid), dim3(64 * sh.wpb), sh.lds, s>>>(p, info, mom, aux, momG, PG, d0, out,
-                                                              raw, list, count, refit, rcount);
+        kern<<<g, b, fs.lds, s>>>(pb, info, mom, aux, momG, PG, d0, out, raw, list, count);
         e = hipGetLastError();
     };
-    auto shape = [&](const FitShape &sh, const Problem &p) {
-        switch (sh.lps * 2 + (sh.mc ? 1 : 0)) {
-            case 17: go(sh, p, k_fit_harmonic<8, true>); break;
-            case 16: go(sh, p, k_fit_harmonic<8, false>); break;
-            case 9: go(sh, p, k_fit_harmonic<4, true>); break;
-            case 8: go(sh, p, k_fit_harmonic<4, false>); break;
-            case 5: go(sh, p, k_fit_harmonic<2, true>); break;
-            case 4: go(sh, p, k_fit_harmonic<2, false>); break;
-            default: go(sh, p, k_fit_harmonic<1, false>); break;
-        }
-    };
-    const bool defer = opt(O_FIT_DEFER) != 0 && refit != nullptr && pb.P >= kDeferMin;
-    if (defer) pb.flags |= F_REFIT_DEFER;
-    shape(fs, pb);
-    if (defer && e == hipSuccess) {
-        // the listed re-fits (count on the device): one round of several-lane groups for up to
-        // 4·n_cu of them, grid-stride beyond
-        Problem pr = pb;
-        pr.flags = (pb.flags & ~F_REFIT_DEFER) | F_REFIT_RUN;
-        shape(fit_shape(std::min<long long>(pb.P, 4LL * std::max(1, n_cu)), n_cu,
-                        (pb.flags & F_OFFSETS) != 0),
-              pr);
+    switch (fs.lps * 2 + (fs.mc ? 1 : 0)) {
+        case 17: go(k_fit_harmonic<8, true>); break;
+        case 16: go(k_fit_harmonic<8, false>); break;
+        case 9: go(k_fit_harmonic<4, true>); break;
+        case 8: go(k_fit_harmonic<4, false>); break;
+        case 5: go(k_fit_harmonic<2, true>); break;
+        case 4: go(k_fit_harmonic<2, false>); break;
+        default: go(k_fit_harmonic<1, false>); break;
     }
     return e;
 }
@@ -372,9 +342,7 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     L.aux = take((size_t)P * 4 * sizeof(double));
     L.fstat = take(faint ? (size_t)P * 16 * sizeof(double) : 0);
     L.raw = take((size_t)P * 2 * sizeof(double));
-    // + per-cohort fallback and re-fit counters
-    L.list = take((size_t)(P + 64 + 2 * kMaxCohorts) * sizeof(int));
-    L.refit = take(harmonic ? (size_t)P * sizeof(Refit) : 0);  // deferred π-flip re-fits
+    L.list = take((size_t)(P + 64 + kMaxCohorts) * sizeof(int));  // + per-cohort counters
     L.phbuf = take(phbuf ? (size_t)n_fc * N * sizeof(c64) : 0);
     // harmonic fitoffsets: G moments of the FC columns (same chunking), Σ d per series
     L.partG = take(harm_offs ? (size_t)nch * NMOM * n_fc * sizeof(double) : 0);
@@ -749,8 +717,6 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     double *raw = (double *)(ws + L.raw);
     int *list = (int *)(ws + L.list);
     int *count = list + P;
-    int *rcount = count + 1;  // deferred π-flip re-fits (launch_fit)
-    Refit *refit = (Refit *)(ws + L.refit);
     c64 *ph = (c64 *)(ws + L.phbuf);
 
     Problem pb;
@@ -824,7 +790,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         k_prepare_part<<<np, 256, 0, stream>>>(pb, pp);
         k_prepare_fin<<<1, 256, 0, stream>>>(pp, (int)np, info);
     }
-    HIP_TRY(hipMemsetAsync(count, 0, 2 * sizeof(int), stream));  // fallbacks, re-fits
+    HIP_TRY(hipMemsetAsync(count, 0, sizeof(int), stream));
     mark("prepare");
     // Pipelined harmonic path (whole-exposure series, fits only, without fitoffsets): the
     // series are cut into cohorts; cohort c's statistics, moment pass and reduction run on the
@@ -887,8 +853,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         else
             k_table<<<(unsigned)((N + 255) / 256), 256, 0, stream>>>(t, N, omega, tab);
         mark("table");
-        int *ccount = list + P + 64;  // one fallback and one re-fit counter per cohort
-        HIP_TRY(hipMemsetAsync(ccount, 0, 2 * kMaxCohorts * sizeof(int), stream));
+        int *ccount = list + P + 64;  // one fallback counter per cohort
+        HIP_TRY(hipMemsetAsync(ccount, 0, kMaxCohorts * sizeof(int), stream));
         const bool fs1 = L.fs1 && fse != 2;
         const long long step = ((P + cohorts - 1) / cohorts + MM_PIX - 1) / MM_PIX * MM_PIX;
         int c = 0;
@@ -960,8 +926,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             HIP_TRY(hipStreamWaitEvent(side, cx->fork[c], 0));
             const int b0 = rec(side);
             HIP_TRY(launch_fit(fit_shape(n, cx->n_cu, (sp.flags & F_OFFSETS) != 0), sp, info, mom_c, aux_c, nullptr, n_fc,
-                               nullptr, out_c, raw_c, list_c, count_c, refit, ccount + kMaxCohorts + c,
-                               cx->n_cu, side));
+                               nullptr, out_c, raw_c, list_c, count_c, side));
             const int b1 = mark_on(side, b0, "fit_harmonic");
             const unsigned xg = (unsigned)std::min<long long>(n, 1024);
             if (faint)
@@ -1145,7 +1110,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             pp.flags |= F_PROF;
             const FitShape fsh = fit_shape(P, cx->n_cu, (pb.flags & F_OFFSETS) != 0);
             HIP_TRY(launch_fit(fsh, pp, info, mom, aux, momG, n_fc, d0, outp, raw, list, count,
-                               refit, rcount, cx->n_cu, stream));
+                               stream));
             HIP_TRY(prof_read());
             const unsigned long long *z = prof_h + PROF_FIT;
             fprintf(stderr, "fit_prof per series: objective %.3g cycles, whole fit %.3g, evals %.3g\n",
@@ -1174,7 +1139,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
 #endif
         } else {
             HIP_TRY(launch_fit(fit_shape(P, cx->n_cu, (pb.flags & F_OFFSETS) != 0), pb, info, mom, aux, momG, n_fc, d0, outp,
-                               raw, list, count, refit, rcount, cx->n_cu, stream));
+                               raw, list, count, stream));
         }
         mark("fit_harmonic");
         // fallback: series whose fit left the expansion's safe range, re-fitted exactly

@@ -60,21 +60,11 @@ constexpr uint32_t F_PROF = 0x80000000u;  // internal: k_fit_harmonic cycle spli
 constexpr uint32_t F_XSPIN_TEST = 0x40000000u;
 // internal (A/B, tests): the exact evaluator's general load path even where FAST applies
 constexpr uint32_t F_NOFAST = 0x20000000u;
-// internal (k_fit_harmonic, launch_fit): a series whose first NEWUOA run lands in a "bad
-// minimum" hands its π-flip re-fit to a second launch (F_REFIT_DEFER), which runs the listed
-// re-fits (F_REFIT_RUN) — the same operations, so the same records
-constexpr uint32_t F_REFIT_DEFER = 0x10000000u, F_REFIT_RUN = 0x08000000u;
-// a deferred π-flip re-fit: the series, its flipped point and what its first run carried
-struct Refit {
-    double x0, x1;
-    int k, status, nfev, fallback;
-};
 // Diagnostic cycle counters (options fit_prof, moments = 7: ws_prof) live in the workspace, reached
 // through Problem::prof: [0..3] fit split (objective, whole fit, evals, exact exchange),
-// [8..15] moment-kernel roles,
-// [16..31] NEWUOA phases (diagnostics build: lane- and wave-level); diagnostics build also
-// [PROF_WV + 4 w ..]: harmonic-fit wave w's start and end (s_memrealtime, 100 MHz), its lanes'
-// largest evaluation count and its hardware id (HW_ID | XCC_ID << 32)
+// [8..15] moment-kernel roles, [16..31] NEWUOA phases (diagnostics build: lane- and wave-level);
+// diagnostics build also [PROF_WV + 4 w ..]: harmonic-fit wave w's start and end (s_memrealtime,
+// 100 MHz), its lanes' largest evaluation count and its hardware id (HW_ID | XCC_ID << 32)
 #ifdef GPD_DIAG
 constexpr int PROF_FIT = 0, PROF_WS = 8, PROF_NW = 16, PROF_WV = 40, PROF_WV_MAX = 4096,
               PROF_LEN = PROF_WV + 4 * PROF_WV_MAX;
@@ -194,16 +184,10 @@ __device__ __forceinline__ c64 fc_phasor(c64 z) { return cisj(jl_atan2(z.im, z.r
 
 // ---------------------------------------------------------------------------------------
 // Driver shared by both evaluators (src/Modulation.jl:402-416).  F: double operator()(double(&)[2])
-// With F_REFIT_DEFER the π-flip re-fit is not run here: drive_fit returns true with x at the
-// flipped point and status carrying ST_REFIT, and the caller lists the series; with
-// F_REFIT_RUN x and status arrive so, and only the re-fit runs.
 template <class F, class NW>
-__device__ __forceinline__ bool drive_fit(F &f, const Problem &pb, double (&x)[2], int &status,
+__device__ __forceinline__ void drive_fit(F &f, const Problem &pb, double (&x)[2], int &status,
                                           NW &nw) {
-    const bool rerun = (pb.flags & F_REFIT_RUN) != 0;
-    if (rerun) {
-        // x arrives at the flipped point
-    } else if (pb.has_xinit) {
+    if (pb.has_xinit) {
         x[0] = pb.x0;
         x[1] = pb.x1;
     } else {
@@ -239,7 +223,7 @@ __device__ __forceinline__ bool drive_fit(F &f, const Problem &pb, double (&x)[2
     // — one call site of run() in a two-pass loop, so the inlined NEWUOA exists once in the
     // kernel's code (r4: the harmonic fit kernel 19.5 k → ~10 k instructions, against a 64 KB
     // instruction cache shared by two CUs), the same operations in the same order
-    for (int pass = rerun ? 1 : 0;; ++pass) {
+    for (int pass = 0;; ++pass) {
         const int nf = nw.run(x, 1.0, 1e-3, pb.maxfun, f, fx);
         if (nf >= pb.maxfun) status |= ST_MAXFUN;
         if (pass > 0) break;
@@ -258,9 +242,7 @@ __device__ __forceinline__ bool drive_fit(F &f, const Problem &pb, double (&x)[2
         if (!(lklval > lflip)) break;  // "bad minima" (src/Modulation.jl:411-414)
         status |= ST_REFIT;
         x[1] = php;
-        if (pb.flags & F_REFIT_DEFER) return true;
     }
-    return false;
 }
 
 template <class F>
@@ -2491,8 +2473,7 @@ __global__ __launch_bounds__(256, 1) void k_fit_harmonic(Problem pb, const Info 
                                                          const double *__restrict__ momG, long long PG,
                                                          const double *__restrict__ d0,
                                                          Param *__restrict__ out, double *__restrict__ raw,
-                                                         int *__restrict__ list, int *__restrict__ count,
-                                                         Refit *__restrict__ refit, int *__restrict__ rcount)
+                                                         int *__restrict__ list, int *__restrict__ count)
 #if GPD_OWNS(GPD_U_FITH)
 {
     typedef Newuoa<2, 5, true, LPS> NW;
@@ -2503,129 +2484,101 @@ __global__ __launch_bounds__(256, 1) void k_fit_harmonic(Problem pb, const Info 
     const int gpw = pb.fit_lanes > 0 ? pb.fit_lanes : 64 / LPS;  // series per wave
     const int grp = lane / LPS, r = lane & (LPS - 1);
     if (grp >= gpw) return;
+    const long long k = ((long long)blockIdx.x * (blockDim.x >> 6) + wv) * gpw + grp;
+    if (k >= pb.P) return;
     const int slot = wv * gpw + grp;
     NW &nw = ((NW *)fit_lds)[slot];
     const Info in = *info;
-    // F_REFIT_RUN: the listed π-flip re-fits, grid-stride; otherwise this group's one series
-    const bool rerun = (pb.flags & F_REFIT_RUN) != 0;
-    const long long e0 = ((long long)blockIdx.x * (blockDim.x >> 6) + wv) * gpw + grp;
-    const long long ecap = (long long)gridDim.x * (blockDim.x >> 6) * gpw;
-    const long long nre = rerun ? (long long)*rcount : 0;
-    for (long long e = e0;; e += ecap) {
-        if (rerun ? e >= nre : (e > e0 || e >= pb.P)) break;
-        const long long k = rerun ? (long long)refit[e].k : e;
-        const Span sp = span_of(pb, k);
-        // harmonic path unusable for these timestamps, or a short (last) window: exact fit
-        if (in.mode == 2 || sp.s1 - sp.s0 < pb.harm_min) {
-            if (r == 0) list[atomicAdd(count, 1)] = (int)k;
-            continue;
-        }
-        HarmChi2<LPS, Src> f;
-        f.r = r;
-        f.nvalid = aux[4 * k + 3];
-        f.W2 = aux[4 * k + 0];
-        f.DEN = aux[4 * k + 1];
-        const double Q2 = aux[4 * k + 2];
-        // tail bound: |Σ_{|n|>K} J_n e^{-jnϕ} F_n| ≤ 2|J_{K+1}| sqrt(N Σ|q|²) ≤ 1e-16 sqrt(W2·DEN)
-        f.tailref = 0.5e-16 * sqrt(f.W2 * f.DEN) / sqrt(f.nvalid * Q2);
-        f.qbase = in.mode == 1 ? in.qbase : 0.0;
-        f.phimax = in.phimax;
-        f.a_re = f.a_im = 0.0;
-        f.nfev = 0;
-        f.fallback = false;
-        harm_offsets(f, pb, k, d0);
-        const long long g = f.offs ? (long long)pb.fcop[k] : 0;
-        if constexpr (MC) {
-            const int nsl = (int)(blockDim.x >> 6) * gpw;  // series slots of the workgroup
-            ldouble *cache = (ldouble *)((char *)fit_lds + (size_t)nsl * sizeof(NW));
-            ldouble *cs = cache + (size_t)slot * HARM_ROWS;
-            for (int q = r; q < HARM_ROWS; q += LPS) cs[q] = mom[(long long)q * pb.P + k];
-            f.src.p = cs;
-            f.srcG.p = cs;
-            if (f.offs) {
-                ldouble *cg = cache + (size_t)(nsl + slot) * HARM_ROWS;
-                for (int q = r; q < HARM_ROWS; q += LPS) cg[q] = momG[(long long)q * PG + g];
-                f.srcG.p = cg;
-            }
-            // the group's lanes read each other's rows: one wave, LDS in issue order
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        } else {
-            f.src = HarmG{mom, pb.P, k};
-            f.srcG = f.offs ? HarmG{momG, PG, g} : f.src;
-        }
-        f.prof = (pb.flags & F_PROF) != 0;
-        f.prof_cycles = f.prof_wave = 0;
-        const unsigned long long tfit = f.prof ? __builtin_amdgcn_s_memtime() : 0;
-        double x[2];
-        int status = 0;
-        if (rerun) {  // what the series' first run carried
-            const Refit re = refit[e];
-            x[0] = re.x0;
-            x[1] = re.x1;
-            status = re.status;
-            f.nfev = re.nfev;
-            f.fallback = re.fallback != 0;
-        }
-#ifdef GPD_DIAG
-        const unsigned long long rt0 = f.prof ? __builtin_amdgcn_s_memrealtime() : 0;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) nw.prof_[q] = 0;
-#endif
-        const bool deferred = drive_fit(f, pb, x, status, nw);
-#ifdef GPD_DIAG
-        if (f.prof && !rerun) {  // the wave's fit time (its lanes meet again here): mean and max over waves
-            const unsigned long long tw = __builtin_amdgcn_s_memtime() - tfit;
-            const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
-            const long long wid = (long long)blockIdx.x * (blockDim.x >> 6) + wv;
-            unsigned long long *wrec = pb.prof + PROF_WV + 4 * wid;
-            if ((int)threadIdx.x == __builtin_amdgcn_readfirstlane((int)threadIdx.x)) {
-                atomicAdd(&pb.prof[PROF_FIT + 5], tw);
-                atomicMax(&pb.prof[PROF_FIT + 6], tw);
-                atomicAdd(&pb.prof[PROF_FIT + 7], 1ull);
-                if (wid < PROF_WV_MAX) {  // the wave's timeline record (vector atomics)
-                    atomicMax(&wrec[0], rt0);
-                    atomicMax(&wrec[1], rt1);
-                    const unsigned long long hw = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
-                    const unsigned long long xcc = (unsigned)__builtin_amdgcn_s_getreg(20 | (31 << 11));
-                    atomicMax(&wrec[3], hw | (xcc << 32));
-                }
-            }
-            if (r == 0 && wid < PROF_WV_MAX) atomicMax(&wrec[2], (unsigned long long)f.nfev);
-        }
-#endif
-        if (deferred) {  // the re-fit from the flipped point runs in the second launch
-            if (r == 0) {
-                Refit re;
-                re.x0 = x[0];
-                re.x1 = x[1];
-                re.k = (int)k;
-                re.status = status;
-                re.nfev = f.nfev;
-                re.fallback = f.fallback ? 1 : 0;
-                refit[atomicAdd(rcount, 1)] = re;
-            }
-            continue;
-        }
-        const double chi2 = f(x);  // likelihood[idx] = lkl(x) (src/Modulation.jl:416)
-        if (f.prof && r == 0) {
-            atomicAdd(&pb.prof[PROF_FIT + 0], f.prof_cycles);
-            atomicAdd(&pb.prof[PROF_FIT + 1], __builtin_amdgcn_s_memtime() - tfit);
-            atomicAdd(&pb.prof[PROF_FIT + 2], (unsigned long long)f.nfev);
-#ifdef GPD_DIAG
-#pragma unroll
-            for (int q = 0; q < 16; ++q) atomicAdd(&pb.prof[PROF_NW + q], nw.prof_[q]);
-            atomicAdd(&pb.prof[PROF_FIT + 4], f.prof_wave);
-#endif
-        }
-        if (r != 0) continue;
-        if (f.fallback) {
-            list[atomicAdd(count, 1)] = (int)k;
-            continue;
-        }
-        store_param(out, raw, k, f.c_re, f.c_im, f.a_re, f.a_im, x[0], x[1], chi2, f.nfev, status);
+    const Span sp = span_of(pb, k);
+    // harmonic path unusable for these timestamps, or a short (last) window: exact fit
+    if (in.mode == 2 || sp.s1 - sp.s0 < pb.harm_min) {
+        if (r == 0) list[atomicAdd(count, 1)] = (int)k;
+        return;
     }
+    HarmChi2<LPS, Src> f;
+    f.r = r;
+    f.nvalid = aux[4 * k + 3];
+    f.W2 = aux[4 * k + 0];
+    f.DEN = aux[4 * k + 1];
+    const double Q2 = aux[4 * k + 2];
+    // tail bound: |Σ_{|n|>K} J_n e^{-jnϕ} F_n| ≤ 2|J_{K+1}| sqrt(N Σ|q|²) ≤ 1e-16 sqrt(W2·DEN)
+    f.tailref = 0.5e-16 * sqrt(f.W2 * f.DEN) / sqrt(f.nvalid * Q2);
+    f.qbase = in.mode == 1 ? in.qbase : 0.0;
+    f.phimax = in.phimax;
+    f.a_re = f.a_im = 0.0;
+    f.nfev = 0;
+    f.fallback = false;
+    harm_offsets(f, pb, k, d0);
+    const long long g = f.offs ? (long long)pb.fcop[k] : 0;
+    if constexpr (MC) {
+        const int nsl = (int)(blockDim.x >> 6) * gpw;  // series slots of the workgroup
+        ldouble *cache = (ldouble *)((char *)fit_lds + (size_t)nsl * sizeof(NW));
+        ldouble *cs = cache + (size_t)slot * HARM_ROWS;
+        for (int q = r; q < HARM_ROWS; q += LPS) cs[q] = mom[(long long)q * pb.P + k];
+        f.src.p = cs;
+        f.srcG.p = cs;
+        if (f.offs) {
+            ldouble *cg = cache + (size_t)(nsl + slot) * HARM_ROWS;
+            for (int q = r; q < HARM_ROWS; q += LPS) cg[q] = momG[(long long)q * PG + g];
+            f.srcG.p = cg;
+        }
+        // the group's lanes read each other's rows: one wave, LDS in issue order
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        f.src = HarmG{mom, pb.P, k};
+        f.srcG = f.offs ? HarmG{momG, PG, g} : f.src;
+    }
+    f.prof = (pb.flags & F_PROF) != 0;
+    f.prof_cycles = f.prof_wave = 0;
+    const unsigned long long tfit = f.prof ? __builtin_amdgcn_s_memtime() : 0;
+    double x[2];
+    int status = 0;
+#ifdef GPD_DIAG
+    const unsigned long long rt0 = f.prof ? __builtin_amdgcn_s_memrealtime() : 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) nw.prof_[q] = 0;
+#endif
+    drive_fit(f, pb, x, status, nw);
+#ifdef GPD_DIAG
+    if (f.prof) {  // the wave's fit time (its lanes meet again here): mean and max over waves
+        const unsigned long long tw = __builtin_amdgcn_s_memtime() - tfit;
+        const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
+        const long long wid = (long long)blockIdx.x * (blockDim.x >> 6) + wv;
+        unsigned long long *wrec = pb.prof + PROF_WV + 4 * wid;
+        if ((int)threadIdx.x == __builtin_amdgcn_readfirstlane((int)threadIdx.x)) {
+            atomicAdd(&pb.prof[PROF_FIT + 5], tw);
+            atomicMax(&pb.prof[PROF_FIT + 6], tw);
+            atomicAdd(&pb.prof[PROF_FIT + 7], 1ull);
+            if (wid < PROF_WV_MAX) {  // the wave's timeline record (vector atomics)
+                atomicMax(&wrec[0], rt0);
+                atomicMax(&wrec[1], rt1);
+                const unsigned long long hw = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+                const unsigned long long xcc = (unsigned)__builtin_amdgcn_s_getreg(20 | (31 << 11));
+                atomicMax(&wrec[3], hw | (xcc << 32));
+            }
+        }
+        if (r == 0 && wid < PROF_WV_MAX) atomicMax(&wrec[2], (unsigned long long)f.nfev);
+    }
+#endif
+    const double chi2 = f(x);  // likelihood[idx] = lkl(x) (src/Modulation.jl:416)
+    if (f.prof && r == 0) {
+        atomicAdd(&pb.prof[PROF_FIT + 0], f.prof_cycles);
+        atomicAdd(&pb.prof[PROF_FIT + 1], __builtin_amdgcn_s_memtime() - tfit);
+        atomicAdd(&pb.prof[PROF_FIT + 2], (unsigned long long)f.nfev);
+#ifdef GPD_DIAG
+#pragma unroll
+        for (int q = 0; q < 16; ++q) atomicAdd(&pb.prof[PROF_NW + q], nw.prof_[q]);
+        atomicAdd(&pb.prof[PROF_FIT + 4], f.prof_wave);
+#endif
+    }
+    if (r != 0) return;
+    if (f.fallback) {
+        list[atomicAdd(count, 1)] = (int)k;
+        return;
+    }
+    store_param(out, raw, k, f.c_re, f.c_im, f.a_re, f.a_im, x[0], x[1], chi2, f.nfev, status);
 }
 #else
 ;
