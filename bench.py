@@ -63,6 +63,8 @@ def parse():
                          "for the 1e5 x 1e5 headline shape, 0 otherwise)")
     ap.add_argument("--no-c5", action="store_true",
                     help="skip the C5 block (faint exposure: GPU step + CPU oracle sample)")
+    ap.add_argument("--no-c5-sweep", action="store_true",
+                    help="skip the C5 Float32 storage / arithmetic tolerance sweep")
     ap.add_argument("--c5-cpu-pixels", type=int, default=256,
                     help="series of the C5 exposure in its CPU-oracle sample")
     ap.add_argument("--no-ceiling", action="store_true",
@@ -539,11 +541,14 @@ def c5_block(gpd, L, dev, sptr, args, log):
     params = torch.empty((P, 64), dtype=torch.uint8, device=dev)
     err = ctypes.create_string_buffer(512)
 
-    def call(method):
-        gpd._lib.check(L.gpd_fit_batch_dev(N, P, t.data_ptr(), d.data_ptr(), N, fc.data_ptr(), G,
-                                           N, fcop.data_ptr(), std.data_ptr(), gpd.M_2PI, None,
-                                           gpd.GPD_RECENTER | method, 60, params.data_ptr(),
-                                           None, N, dev.index, sptr, err, len(err)), err)
+    def call(method, dd=None, ff=None):
+        c32 = dd is not None
+        fn = L.gpd_fit_batch_c32_dev if c32 else L.gpd_fit_batch_dev
+        dd, ff = (dd, ff) if c32 else (d, fc)
+        gpd._lib.check(fn(N, P, t.data_ptr(), dd.data_ptr(), N, ff.data_ptr(), G,
+                          N, fcop.data_ptr(), std.data_ptr(), gpd.M_2PI, None,
+                          gpd.GPD_RECENTER | method, 60, params.data_ptr(),
+                          None, N, dev.index, sptr, err, len(err)), err)
 
     for _ in range(2):
         call(0)
@@ -577,6 +582,14 @@ def c5_block(gpd, L, dev, sptr, args, log):
     ems = 1e3 * (time.perf_counter() - t0) / 2
     out["gpu_exact"] = {"ms_per_step": round(ems, 2), "complex_samples_per_s": P * N / (ems * 1e-3),
                         "kernels_ms": {k: round(float(v), 3) for k, v in gpd.timings(dev.index).items()}}
+    par_exact = params.cpu().numpy().reshape(-1).view(rec).copy()
+    if not args.no_c5_sweep:
+        sw = c5_fp32_sweep(gpd, call, params, d, fc, dev, P, N,
+                           {"f64_harmonic": par, "f64_exact": par_exact}, log)
+        sw["rows"]["f64_harmonic"] = {"ms": round(ms, 3)}
+        sw["rows"]["f64_exact"] = {"ms": round(ems, 2)}
+        sw["fp32_arith_speedup_over_f64_exact"] = round(ems / sw["rows"]["fp32"]["ms"], 3)
+        out["fp32_sweep"] = sw
     if args.no_cpu or args.c5_cpu_pixels <= 0:
         return out
     # the sample: the first k series through the oracle, and the GPU's exact evaluator on them
@@ -611,6 +624,68 @@ def c5_block(gpd, L, dev, sptr, args, log):
                             "harmonic_within_1e-6": f"{int((e <= 1e-6).sum())}/{k}",
                             "harmonic_max_dev": float(e.max())}
     return out
+
+
+def c5_fp32_sweep(gpd, call, params, d, fc, dev, P, N, ref, log):
+    """BASELINE configs[4]'s fp32-vs-fp64 tolerance sweep on the C5 exposure, on this build
+    (verdict r5 item 3; tools/c5_sweep.py's pairs and summaries).  Rows, each against the Float64
+    records of the same evaluator:
+      c32_harmonic / c32_exact  ComplexF32 STORAGE (the FITS VOLT precision, d and FC rounded to
+                                Float32 and kept so in HBM; Float64 arithmetic) — gpd_fit_batch_c32_dev
+      fp32 / c32_fp32           Float32 ARITHMETIC (GPD_FP32: the exact evaluator's per-sample
+                                θ, sin, sincos, phasor, model and residual in Float32; sums and
+                                NEWUOA in Float64) on the Float64 and on the ComplexF32 data,
+                                against the Float64 exact evaluator
+    plus harmonic vs exact in Float64 (the scale of evaluator-level differences).  Columns: the
+    fraction of series within 1e-3 … 1e-8 and the max, for b (relative), ϕ and arg a (radians),
+    |a| (relative) and all four together; each row's time (one warm call, then one timed call,
+    wall clock around the device call)."""
+    import numpy as np
+    import torch
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from c5_sweep import summarise
+
+    rec = gpd.PARAM_DTYPE
+    d32, fc32 = d.float(), fc.float()
+    rows = {}
+    res = dict(ref)
+
+    def timed(key, method, c32):
+        args = (d32, fc32) if c32 else ()
+        call(method, *args)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        call(method, *args)
+        torch.cuda.synchronize(dev)
+        ms = 1e3 * (time.perf_counter() - t0)
+        res[key] = params.cpu().numpy().reshape(-1).view(rec).copy()
+        rows[key] = {"ms": round(ms, 2),
+                     "fallback": int(np.count_nonzero(res[key]["status"] & gpd.GPD_ST_FALLBACK)),
+                     "nan": int(np.count_nonzero(res[key]["status"] & gpd.GPD_ST_NAN))}
+        log(f"C5 sweep {key}: {ms:.1f} ms")
+
+    timed("c32_harmonic", 0, True)
+    timed("c32_exact", gpd.GPD_METHOD_EXACT, True)
+    timed("fp32", gpd.GPD_FP32, False)
+    timed("c32_fp32", gpd.GPD_FP32, True)
+    del d32, fc32
+    torch.cuda.empty_cache()
+    pairs = {"c32_storage_harmonic_vs_f64_harmonic": ("c32_harmonic", "f64_harmonic"),
+             "c32_storage_exact_vs_f64_exact": ("c32_exact", "f64_exact"),
+             "fp32_arith_vs_f64_exact": ("fp32", "f64_exact"),
+             "fp32_arith_c32_data_vs_f64_exact": ("c32_fp32", "f64_exact"),
+             "f64_harmonic_vs_f64_exact": ("f64_harmonic", "f64_exact")}
+    table = {}
+    for name, (a, b) in pairs.items():
+        s = summarise(res[a], res[b])
+        table[name] = {"within": s["all_params"]["within"], "max": s["all_params"]["max"],
+                       "per_param": {k: {"max": v["max"], "within": v["within"]}
+                                     for k, v in s.items() if k != "all_params"}}
+    return {"series": P, "samples": N, "rows": rows, "pairs": table,
+            "note": "ComplexF32 storage = Float32 data, Float64 engine (both evaluators); "
+                    "Float32 arithmetic = GPD_FP32 exact evaluator; deviations per series of b "
+                    "(relative), ϕ / arg a (radians, mod 2π), |a| (relative)"}
 
 
 def traffic_from_profiles(P, N, storage="c64"):

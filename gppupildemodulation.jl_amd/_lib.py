@@ -63,6 +63,20 @@ class GpdError(RuntimeError):
 _lib = None
 
 
+def _warn_legacy_env():
+    """The library reads no environment variable (r5); the GPD_* variables earlier rounds' A/B
+    scripts set (GPD_MOMENTS, GPD_FIT_PROF, GPD_COHORTS, …) now do nothing.  Say so once, so a run
+    that sets one does not silently measure the default path (advisor r5).  GPD_LIB (library
+    variant) and GPD_OPTS (options_from_env, the A/B tools) are still read on the Python side."""
+    import warnings
+    legacy = sorted(k for k in os.environ
+                    if k.startswith("GPD_") and k not in ("GPD_LIB", "GPD_OPTS"))
+    if legacy:
+        warnings.warn(f"environment variables {legacy} are ignored: the library reads no "
+                      "environment; set options with gpd_set_option / GPD_OPTS=name=value,… "
+                      "(tools) instead", RuntimeWarning, stacklevel=3)
+
+
 def load():
     """Load libgpdemod.so (built in-tree by __graft_entry__.build() / build.py)."""
     global _lib
@@ -72,6 +86,7 @@ def load():
         raise ImportError(
             f"{LIB_PATH} not found: the HIP extension is not built "
             "(run `python -c 'import __graft_entry__ as g; g.build()'`). No CPU fallback exists.")
+    _warn_legacy_env()
     L = ctypes.CDLL(LIB_PATH)
     V, I64, I32, U32, D = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_double
     L.gpd_version.restype = ctypes.c_int

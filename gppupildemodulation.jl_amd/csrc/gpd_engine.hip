@@ -17,6 +17,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -72,6 +73,7 @@ enum OptId {
     O_SYNC_DEBUG,    // 1: synchronise after every stage and name the stage that faulted
     O_HOST_PROF,     // 1: wall-clock split of the host-buffer calls on stderr (diagnostics)
     O_FIT_MCACHE,    // 1: harmonic fit reads the series' moments from LDS where they fit; 0: L2
+    O_STAGE_PINNED,  // 1: demodulated columns staged through a pinned ring; 0: pageable ring (tests)
     O_COUNT
 };
 struct OptDef {
@@ -84,10 +86,10 @@ constexpr OptDef kOpt[O_COUNT] = {
     {"exact_mcache", 1}, {"xspin_test", 0},    {"units", 0},         {"upw", 0},
     {"fit_lanes", 0},    {"fit_lps", 0},       {"fit_wpb", 0},       {"cohorts", 1},       {"harm_min_span", 256}, {"fs_cohort_mb", 4096},
     {"moments", 0},      {"fit_prof", 0},      {"sync_debug", 0},    {"host_prof", 0},
-    {"fit_mcache", 1}};
+    {"fit_mcache", 1},   {"stage_pinned", 1}};
 std::atomic<long long> g_opt[O_COUNT] = {{1}, {0}, {0},   {0},    {0}, {0}, {0}, {1}, {1}, {0}, {0},
                                           {0}, {0}, {0},   {0},    {1}, {256}, {4096}, {0}, {0}, {0},
-                                          {0}, {1}};
+                                          {0}, {1}, {1}};
 inline long long opt(OptId o) { return g_opt[o].load(std::memory_order_relaxed); }
 int opt_find(const char *name) {
     if (!name) return -1;
@@ -143,10 +145,12 @@ struct DevCtx {
     char *harena = nullptr;
     size_t harena_cap = 0;
     hipStream_t hstream = nullptr;
-    // gpd_demodulateall: pinned staging of the demodulated columns (grow-only)
+    // gpd_demodulateall: staging ring of the demodulated columns — kStageSlots slots of
+    // kStageSlotBytes, pinned (hipHostMalloc) or, if that fails or option stage_pinned = 0,
+    // pageable (malloc); a bounded allocation whatever the exposure's length
     char *hpin = nullptr;
-    size_t hpin_cap = 0;
-    hipEvent_t hpin_ev[4] = {};  // the staged column chunks' arrival (host copy pipelined)
+    bool hpin_pinned = false, hpin_nopin = false;
+    hipEvent_t hpin_ev[4] = {};  // each slot's chunk has arrived (host copy pipelined)
     // the last fit call's faint statistics in the workspace (gpd_last_faint_stats; tests)
     const double *last_fstat = nullptr;
     long long last_fstat_P = 0;
@@ -498,6 +502,73 @@ void pool_touch_cols(char *dst, size_t es, int64_t ld, int64_t rows, int64_t nco
     });
 }
 
+// Copy the elements [e0, e1) of a P×N ComplexF64 matrix with contiguous columns (ld N), held
+// contiguously at src, into the caller's columns (dst: element size des, leading dimension dld;
+// des = 8 rounds to ComplexF32 as pool_copy_cols), in pieces of about 1 MB within columns.
+void pool_copy_range(char *dst, size_t des, int64_t dld, const char *src, int64_t N, int64_t e0,
+                     int64_t e1) {
+    constexpr size_t ses = 16;
+    const int64_t per = (int64_t)(1 << 20) / (int64_t)ses;
+    struct Piece {
+        int64_t col, r0, nr, off;  // off: element offset in src
+    };
+    std::vector<Piece> pcs;
+    for (int64_t c = e0 / N; c * N < e1; ++c) {
+        const int64_t r0 = std::max<int64_t>(0, e0 - c * N), r1 = std::min<int64_t>(N, e1 - c * N);
+        for (int64_t r = r0; r < r1; r += per)
+            pcs.push_back({c, r, std::min(per, r1 - r), c * N + r - e0});
+    }
+    HostPool::get().run((int)pcs.size(), [&](int i) {
+        const Piece &q = pcs[i];
+        const char *sp = src + (size_t)q.off * ses;
+        char *d = dst + ((size_t)q.col * dld + q.r0) * des;
+        if (des == ses) {
+            std::memcpy(d, sp, (size_t)q.nr * ses);
+        } else {
+            const double *sv = (const double *)sp;
+            float *dv = (float *)d;
+            for (int64_t k = 0; k < 2 * q.nr; ++k) dv[k] = (float)sv[k];
+        }
+    });
+}
+
+// The output staging ring of a device (host_batch, out_kind 1/2): kStageSlots × kStageSlotBytes
+// (64 MB) whatever the exposure's length (advisor r5: the whole P×N×16 B used to be pinned,
+// grow-only).  Pinned (hipHostMalloc) by default; if that fails — or with option stage_pinned = 0
+// — pageable memory (hipMemcpyAsync into it returns once the bytes are staged: the same bytes,
+// less overlap), and a failed pinned allocation is not retried on every call.
+constexpr int kStageSlots = 4;
+constexpr size_t kStageSlotBytes = (size_t)16 << 20;
+
+void free_stage(DevCtx *cx) {
+    if (cx->hpin) {
+        if (cx->hpin_pinned)
+            (void)hipHostFree(cx->hpin);
+        else
+            std::free(cx->hpin);
+    }
+    cx->hpin = nullptr;
+    cx->hpin_pinned = false;
+}
+
+bool ensure_stage(DevCtx *cx) {
+    const bool want_pin = opt(O_STAGE_PINNED) != 0 && !cx->hpin_nopin;
+    if (cx->hpin && cx->hpin_pinned == want_pin) return true;
+    free_stage(cx);
+    const size_t bytes = (size_t)kStageSlots * kStageSlotBytes;
+    if (want_pin) {
+        if (hipHostMalloc((void **)&cx->hpin, bytes, hipHostMallocDefault) == hipSuccess) {
+            cx->hpin_pinned = true;
+            return true;
+        }
+        (void)hipGetLastError();
+        cx->hpin = nullptr;
+        cx->hpin_nopin = true;
+    }
+    cx->hpin = (char *)std::malloc(bytes);
+    return cx->hpin != nullptr;
+}
+
 const char *kErrStr[] = {"ok", "invalid argument", "HIP runtime error", "no HIP device",
                          "out of device memory", "harmonic method unsafe for these timestamps"};
 
@@ -558,10 +629,9 @@ int gpd_release(int device) {
     if (cx->done) (void)hipEventSynchronize(cx->done);
     (void)hipFree(cx->ws);
     (void)hipFree(cx->harena);
-    (void)hipHostFree(cx->hpin);
+    free_stage(cx);
     cx->ws = cx->harena = nullptr;
-    cx->hpin = nullptr;
-    cx->ws_cap = cx->harena_cap = cx->hpin_cap = 0;
+    cx->ws_cap = cx->harena_cap = 0;
     cx->last_fstat = nullptr;  // pointed into the freed workspace (advisor r4)
     cx->last_fstat_P = 0;
     return GPD_OK;
@@ -929,6 +999,8 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                                nullptr, out_c, raw_c, list_c, count_c, side));
             const int b1 = mark_on(side, b0, "fit_harmonic");
             const unsigned xg = (unsigned)std::min<long long>(n, 1024);
+            if (fused)  // the fallback series' two-pass statistics (as above, one cohort)
+                k_faint_stats_list<<<xg, 256, 0, side>>>(sp, list_c, count_c, fs_c);
             if (faint)
                 k_fit_exact<true, false, false><<<xg, EXACT_WG, 0, side>>>(
                     sp, info, nullptr, fs_c, list_c, count_c, out_c, raw_c, ST_FALLBACK);
@@ -1142,7 +1214,13 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                                raw, list, count, stream));
         }
         mark("fit_harmonic");
-        // fallback: series whose fit left the expansion's safe range, re-fitted exactly
+        // fallback: series whose fit left the expansion's safe range, re-fitted exactly — faint
+        // ones with the two-pass statistics of the listed series (the oracle's bits), not the
+        // fused ones the harmonic fit used
+        if (fused) {
+            k_faint_stats_list<<<exact_grid, 256, 0, stream>>>(pb, list, count, fstat);
+            mark("fallback_stats");
+        }
         if (faint)
             k_fit_exact<true, false, false><<<exact_grid, EXACT_WG, 0, stream>>>(
                 pb, info, nullptr, fstat, list, count, outp, raw, ST_FALLBACK);
@@ -1511,34 +1589,35 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
         const auto h2 = hnow();
         auto h3 = h2, h4 = h2;
         if (ok && out_demod && out_kind != 0) {
-            // staged: one DMA of the P×N demodulated columns into pinned memory, then the host
-            // pool copies them into the caller's columns (ldo), rounding to ComplexF32 for kind 2
-            const size_t bytes = (size_t)P * N * sizeof(c64);
-            if (cx->hpin_cap < bytes) {
-                ok = chk(hipStreamSynchronize(s), "hipStreamSynchronize");
-                if (ok) {
-                    (void)hipHostFree(cx->hpin);
-                    cx->hpin = nullptr;
-                    cx->hpin_cap = 0;
-                    ok = chk(hipHostMalloc((void **)&cx->hpin, bytes, hipHostMallocDefault),
-                             "hipHostMalloc (output staging)");
-                    if (ok) cx->hpin_cap = bytes;
-                }
-            }
-            // the columns come back in up to 4 chunks, an event after each: the pool copies
-            // chunk c while chunk c + 1 is still in flight
-            const int nch = (int)std::min<int64_t>(4, P);
-            for (int c = 0; ok && c < nch; ++c)
+            // staged: the P×N demodulated columns (contiguous on the device) come back in chunks
+            // through the device's staging ring — chunk c into slot c mod kStageSlots, an event
+            // after each; the host pool copies chunk c into the caller's columns (ldo; rounded to
+            // ComplexF32 for kind 2) while chunks c + 1 … are in flight, then the slot takes
+            // chunk c + kStageSlots.  At least 4 chunks (C2: 4 × 12.8 MB), at most one slot each.
+            const int64_t total = P * N;  // c64 elements
+            const int64_t per_slot = (int64_t)(kStageSlotBytes / sizeof(c64));
+            const int64_t nch = std::max<int64_t>(std::min<int64_t>(4, total),
+                                                  (total + per_slot - 1) / per_slot);
+            ok = ensure_stage(cx);
+            if (!ok) set_err(errbuf_l, errlen_l, "output staging ring: out of host memory");
+            for (int c = 0; ok && c < kStageSlots; ++c)
                 if (!cx->hpin_ev[c])
                     ok = chk(hipEventCreateWithFlags(&cx->hpin_ev[c], hipEventDisableTiming),
                              "hipEventCreate");
-            for (int c = 0; ok && c < nch; ++c) {
-                const int64_t q0 = P * c / nch, q1 = P * (c + 1) / nch;
-                ok = chk(hipMemcpyAsync(cx->hpin + (size_t)q0 * N * sizeof(c64), dout + q0 * N,
-                                        (size_t)(q1 - q0) * N * sizeof(c64), hipMemcpyDeviceToHost,
-                                        s), "D2H out (staged)") &&
-                     chk(hipEventRecord(cx->hpin_ev[c], s), "hipEventRecord");
-            }
+            auto chunk = [&](int64_t c, int64_t &e0, int64_t &e1) {
+                e0 = total * c / nch;
+                e1 = total * (c + 1) / nch;
+            };
+            auto issue = [&](int64_t c) {
+                int64_t e0, e1;
+                chunk(c, e0, e1);
+                const int sl = (int)(c % kStageSlots);
+                return chk(hipMemcpyAsync(cx->hpin + (size_t)sl * kStageSlotBytes, dout + e0,
+                                          (size_t)(e1 - e0) * sizeof(c64), hipMemcpyDeviceToHost,
+                                          s), "D2H out (staged)") &&
+                       chk(hipEventRecord(cx->hpin_ev[sl], s), "hipEventRecord");
+            };
+            for (int64_t c = 0; ok && c < std::min<int64_t>(nch, kStageSlots); ++c) ok = issue(c);
             const size_t des = out_kind == 2 ? sizeof(gpd_c32) : sizeof(gpd_c64);
             char *dst0 = (char *)out_demod + ((size_t)p0 * ldo + s0) * des;
             // while the device still computes and copies: the first touch of the caller's
@@ -1547,13 +1626,15 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
             // (never the ldo gaps), each later overwritten by the copy below
             if (ok) pool_touch_cols(dst0, des, ldo, N, P);
             h3 = hnow();
-            for (int c = 0; ok && c < nch; ++c) {
-                const int64_t q0 = P * c / nch, q1 = P * (c + 1) / nch;
-                ok = chk(hipEventSynchronize(cx->hpin_ev[c]), "hipEventSynchronize");
+            for (int64_t c = 0; ok && c < nch; ++c) {
+                const int sl = (int)(c % kStageSlots);
+                int64_t e0, e1;
+                chunk(c, e0, e1);
+                ok = chk(hipEventSynchronize(cx->hpin_ev[sl]), "hipEventSynchronize");
                 if (ok)
-                    pool_copy_cols(dst0 + (size_t)q0 * ldo * des, des, ldo,
-                                   cx->hpin + (size_t)q0 * N * sizeof(c64), sizeof(c64), N, N,
-                                   q1 - q0);
+                    pool_copy_range(dst0, des, ldo, cx->hpin + (size_t)sl * kStageSlotBytes, N,
+                                    e0, e1);
+                if (ok && c + kStageSlots < nch) ok = issue(c + kStageSlots);
             }
             h4 = hnow();
         }
@@ -1597,6 +1678,17 @@ static int host_demodulateall(int64_t N, const double *t, const void *data, int6
         return GPD_E_ARG;
     }
     const size_t esz = c32 ? sizeof(gpd_c32) : sizeof(gpd_c64);
+    // output must not overlap data (advisor r5): the FC columns are copied from data into output
+    // and the diode columns read by the H2D copies while output's pages are touched and written
+    {
+        const uintptr_t d0 = (uintptr_t)data, d1 = d0 + ((size_t)39 * ldd + N) * esz;
+        const uintptr_t o0 = (uintptr_t)output, o1 = o0 + ((size_t)39 * ldo + N) * esz;
+        if (d0 < o1 && o0 < d1) {
+            set_err(errbuf, errlen, "gpd_demodulateall: output overlaps data (output = copy(data) "
+                    "is a fresh array)");
+            return GPD_E_ARG;
+        }
+    }
     // 0-based FC column of diode c among the 8 FC columns: idx(side, telescope, FC) − 33 with
     // side FT for c < 16, SC otherwise, telescope = (c mod 16) ÷ 4 + 1 (src/Modulation.jl:17-22,388)
     int32_t fcop[32];

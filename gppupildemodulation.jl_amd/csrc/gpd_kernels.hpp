@@ -494,11 +494,44 @@ __global__ __launch_bounds__(256) void k_table_mix(const double *__restrict__ t,
 // src/Faint.jl:89-100) over the valid samples, plus Σ|d|² per state.  One workgroup per series;
 // sums in the canonical order CR8 (8 block sweeps of 256 strided slots, the oracle's gsum), so m
 // and w are the oracle's bits.  out[k*16 + ...]: m[5] | w[5] | W2 | DEN | Q2 (state = code + 1).
+__device__ __forceinline__ void faint_stats_one(const Problem &pb, long long k,
+                                                double *__restrict__ out, double *lds);
+
 __global__ __launch_bounds__(256) void k_faint_stats(Problem pb, double *__restrict__ out)
 #if GPD_OWNS(GPD_U_ENGINE)
 {
     __shared__ double lds[4 * 15];
-    const long long k = blockIdx.x;
+    faint_stats_one(pb, blockIdx.x, out, lds);
+}
+#else
+;
+#endif
+
+// k_faint_stats over the harmonic fit's fallback list (series list[0 .. *count)): the faint
+// series the exact evaluator re-fits get compute_mean_var_power's two-pass statistics — the
+// oracle's bits — in place of the moment pass's fused ones (m ≤ 1e-14, w ≤ 1e-13 off), so a
+// GPD_ST_FALLBACK record is the oracle's bit for bit like any exact record.  The list is read
+// on the device (no host round trip); with no fallback the launch only reads the count.
+__global__ __launch_bounds__(256) void k_faint_stats_list(Problem pb, const int *__restrict__ list,
+                                                          const int *__restrict__ count,
+                                                          double *__restrict__ out)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
+    __shared__ double lds[4 * 15];
+    const long long total = *count;
+    for (long long j = blockIdx.x; j < total; j += gridDim.x) {
+        faint_stats_one(pb, list[j], out, lds);
+        __syncthreads();  // lds is reused by the next listed series
+    }
+}
+#else
+;
+#endif
+
+__device__ __forceinline__ void faint_stats_one(const Problem &pb, long long k,
+                                                double *__restrict__ out, double *lds)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
     const Span sp = span_of(pb, k);  // per window: compute_mean_var_power on state[I] (:205)
     const long long doff = sp.col * pb.ldd;
     // the loads of U consecutive samples of a slot (2048 apart) are issued together

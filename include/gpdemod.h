@@ -105,8 +105,8 @@ int gpd_release(int device);
  * call.  Names and defaults (INTEGRATION.md lists them): mix 1, faint_stats 0, faint_side 0,
  * fake_gpus 0, exact_g 0, exact_waves 0, exact_wgt 0, exact_fast 1, exact_mcache 1,
  * xspin_test 0, units 0, upw 0, fit_lanes 0, fit_lps 0, fit_wpb 0, cohorts 1, harm_min_span 256, fs_cohort_mb 4096,
- * moments 0, fit_prof 0, sync_debug 0, host_prof 0, fit_mcache 1 (0 = automatic where a count is
- * meant).
+ * moments 0, fit_prof 0, sync_debug 0, host_prof 0, fit_mcache 1, stage_pinned 1 (0 = automatic
+ * where a count is meant).
  * gpd_set_option / gpd_get_option: GPD_OK, or GPD_E_ARG for an unknown name.
  * gpd_option_name(i): the i-th option's name, NULL past the last. */
 int gpd_set_option(const char *name, int64_t value);
@@ -125,10 +125,12 @@ const char *gpd_option_name(int index);
  *                    `output = copy(data)` and the diode loop leave in it (:353, :417-425):
  *                    columns 0..31 the demodulated diodes, 32..39 the FC columns as given.
  *                    The caller allocates it (Julia `similar(data)`) and need not touch it:
- *                    the library fills every column — the demodulated ones through a pinned
- *                    staging buffer and parallel host copies, the FC ones copied while the
- *                    device computes — so no `copy(data)` of the exposure runs on the caller's
- *                    side and the first touch of the fresh pages is spread over threads.
+ *                    the library fills every column — the demodulated ones through a bounded
+ *                    staging ring (4 × 16 MB per device, pinned; pageable if pinning fails) and
+ *                    parallel host copies, the FC ones copied while the device computes — so no
+ *                    `copy(data)` of the exposure runs on the caller's side and the first touch
+ *                    of the fresh pages is spread over threads.  output must not overlap data
+ *                    (GPD_E_ARG): it is a fresh array, as `copy(data)` is.
  *   n_gpus           devices (as gpd_fit_batch; one exposure runs on one)
  * _c32: ComplexF32 data and output (the FITS VOLT precision; Float64 arithmetic, the
  * demodulated columns rounded to Float32 as Complex{Float32}.(…) does).
@@ -312,10 +314,10 @@ int gpd_buildstates_dev(int64_t n_samples, const double *t, int64_t n1, const do
  * — computed by the kernels of the exact evaluator (method EXACT, and the harmonic path with
  * option faint_stats = 1|2), bit for bit the oracle's two-pass restatement.  The default
  * whole-exposure harmonic path forms these statistics inside its moment pass (one pass,
- * shifted sums per state: m within 1e-14, w within 1e-13 relative of these values) and its
- * exact re-fit of FALLBACK series uses those, so faint GPD_ST_FALLBACK records are within that
- * tolerance of the oracle rather than its bits (tests/test_gpu_parity.py
- * ::test_faint_large_b_fallback_statistics).
+ * shifted sums per state: m within 1e-14, w within 1e-13 relative of these values) for the
+ * harmonic fit; the series it hands to the exact evaluator (GPD_ST_FALLBACK) get these two-pass
+ * statistics first, so every exact record — method EXACT and fallback — is the oracle's bit for
+ * bit (tests/test_gpu_parity.py::test_faint_large_b_fallback_statistics).
  * out[10k + c] = m and out[10k + 5 + c] = w of MetState code c − 1 (c = 0 TRANSIENT … 4 HIGH;
  * NaN for a state without samples, w NaN for a 1-sample state, as Julia's 0/0).  Synchronous.
  */
@@ -354,8 +356,9 @@ int gpd_last_timings(int device, const char **names, double *ms, int cap);
 /* Faint statistics of the last fit call on `device` (test hook): the first n_series records of
  * 16 doubles each — m of MetState code c − 1 at [16k + c] (c = 0 TRANSIENT … 4 HIGH), w at
  * [16k + 5 + c], then Σw|d|², Σw m² n, Σ(w m)²|d|² at [16k + 10 … 12] — as the fit used them
- * (the fused statistics of the state-split moment pass for whole-exposure harmonic fits, the
- * separate kernels otherwise).  Waits for that call.  GPD_E_ARG if it had no faint series. */
+ * (the fused statistics of the state-split moment pass for whole-exposure harmonic fits — the
+ * two-pass ones for the series re-fitted by the exact fallback —, the separate kernels
+ * otherwise).  Waits for that call.  GPD_E_ARG if it had no faint series. */
 int gpd_last_faint_stats(int device, double *out, int64_t n_series);
 
 #ifdef __cplusplus

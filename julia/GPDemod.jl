@@ -143,6 +143,15 @@ function demodulateall_gpu(timestamp::AbstractVector, data::AbstractMatrix{Compl
         ModulationWithOffsets{T}[ModulationWithOffsets{T}(p.c, p.a, p.b, p.ϕ, M_2PI) for p in params] :
         ModulationNoOffsets{T}[ModulationNoOffsets{T}(p.a, p.b, p.ϕ, M_2PI) for p in params]
     likelihood = T[p.chi2 for p in params]
+    # eltype(output) == eltype(data) for every T (advisor r5): Float32/Float64 data came back in
+    # its own type; any other T (Float16, BigFloat, …) went through ComplexF64, so it gets the
+    # reference's `output = copy(data)` with the 32 demodulated columns converted into it — the
+    # FC columns 33..40 keep their own precision
+    if !(T === Float32 || T === Float64)
+        out = copy(data)
+        out[:, 1:32] .= Complex{T}.(view(output, :, 1:32))
+        output = out
+    end
     return (output, param, likelihood)
 end
 

@@ -52,7 +52,8 @@ def test_options_api_and_no_environment(gpd):
                 "xspin_test": 0, "units": 0, "upw": 0, "fit_lanes": 0, "fit_lps": 0,
                 "fit_wpb": 0, "cohorts": 1,
                 "harm_min_span": 256, "fs_cohort_mb": 4096, "moments": 0, "fit_prof": 0,
-                "sync_debug": 0, "host_prof": 0, "fit_mcache": 1}
+                "sync_debug": 0, "host_prof": 0, "fit_mcache": 1,
+                "stage_pinned": 1}
     gpd.reset_options()
     assert gpd.option_names() == list(defaults)
     assert {k: gpd.get_option(k) for k in defaults} == defaults
@@ -97,6 +98,22 @@ def test_window_arguments_rejected(gpd):
         assert rc == -1, (window, flags)
     with pytest.raises(ValueError):
         gpd.fit_windows(B["t"], B["d"], B["fc"], B["fc_of_pixel"], 0)
+
+
+def test_demodulateall_rejects_output_overlapping_data(gpd):
+    """output must not overlap data (advisor r5): output = copy(data) is a fresh array; an
+    aliased or overlapping output is GPD_E_ARG before any device work, for both storage types."""
+    L = gpd.load()
+    N = 64
+    t = np.arange(N) * 0.002
+    err = ctypes.create_string_buffer(512)
+    par = np.zeros(32, dtype=gpd.PARAM_DTYPE)
+    for dt, fn in ((np.complex128, L.gpd_demodulateall), (np.complex64, L.gpd_demodulateall_c32)):
+        buf = np.zeros((41, N), dtype=dt)
+        for out in (buf[:40], buf[1:41]):  # the same matrix; one shifted by a column
+            rc = fn(N, t.ctypes.data, buf[:40].ctypes.data, N, None, None, 0, 60,
+                    par.ctypes.data, out.ctypes.data, N, 1, err, len(err))
+            assert rc == -1 and b"overlaps" in err.value, (dt, rc, err.value)
 
 
 def test_window_tables_broadcast(gpd):

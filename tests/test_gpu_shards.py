@@ -63,6 +63,59 @@ def test_fit_windows_shards_bit_identical(gpu, opts, window):
         np.testing.assert_array_equal(out, ref_out)
 
 
+def _exposure(gpu, N, seed):
+    B = synth.make_batch(N, 32, seed=seed)
+    data = np.empty((40, N), dtype=np.complex128)
+    data[:32] = B["d"]
+    fop = np.array([gpu.fc_column_of(c) - 1 for c in range(1, 33)])
+    for g in range(8):
+        data[32 + g] = B["fc"][B["fc_of_pixel"][np.nonzero(fop == 32 + g)[0][0]]]
+    return B["t"], data.T
+
+
+@pytest.mark.parametrize("storage", ["c64", "c32"])
+def test_demodulateall_shards_bit_identical(gpu, opts, storage):
+    """gpd_demodulateall over 2, 3 and 8 shards (advisor r5): each shard writes its slice of the
+    32 demodulated columns through the staging ring (shards on one device take turns), the FC
+    columns are copied beside them — output (every column, FC included), records and likelihood
+    equal the 1-device call's bits, for ComplexF64 and ComplexF32 exposures."""
+    opts("fake_gpus", 1)
+    t, data = _exposure(gpu, 20_011, 64)
+    if storage == "c32":
+        data = np.asfortranarray(data.astype(np.complex64))
+    out1, par1, lk1 = gpu.demodulateall(t, data)
+    assert out1.dtype == data.dtype
+    np.testing.assert_array_equal(out1[:, 32:], data[:, 32:])
+    for g in (2, 3, 8):
+        out, par, lk = gpu.demodulateall(t, data, n_gpus=g)
+        np.testing.assert_array_equal(out, out1)
+        np.testing.assert_array_equal(lk, lk1)
+        assert [(p.a, p.b, p.ϕ) for p in par] == [(p.a, p.b, p.ϕ) for p in par1]
+
+
+def test_demodulateall_pageable_staging_and_long_exposure(gpu, opts):
+    """The staging ring is bounded (4 × 16 MB per device, advisor r5): an exposure whose
+    demodulated columns exceed it (32 × 200 000 × 16 B = 102 MB: 7 chunks through 4 slots) gives
+    the same output as the fit-batch path; and the pageable ring — what runs when pinning fails
+    (option stage_pinned = 0 forces it) — gives the same bytes as the pinned one."""
+    t, data = _exposure(gpu, 200_000, 65)
+    out, par, lk = gpu.demodulateall(t, data)
+    cols = np.ascontiguousarray(data.T)
+    fop = np.array([gpu.fc_column_of(c) - 1 for c in range(1, 33)], dtype=np.int32)
+    ref, ref_out = gpu.fit_batch(t, cols[:32], cols, fop, want_output=True)
+    np.testing.assert_array_equal(out[:, :32].T, ref_out)
+    np.testing.assert_array_equal(lk, ref["chi2"])
+    opts("stage_pinned", 0)
+    out2, _, lk2 = gpu.demodulateall(t, data)
+    np.testing.assert_array_equal(out2, out)
+    np.testing.assert_array_equal(lk2, lk)
+    d32 = np.asfortranarray(data.astype(np.complex64))
+    o32, _, _ = gpu.demodulateall(t, d32)
+    opts("stage_pinned", 1)
+    o32p, _, _ = gpu.demodulateall(t, d32)
+    np.testing.assert_array_equal(o32, o32p)
+
+
 def test_records_independent_of_batch_and_grid(gpu, opts):
     """A series' harmonic record does not depend on the other series of its batch (a sub-batch
     starting mid-workgroup) nor on the moment grid (units per workgroup 1, 2, 3, 7)."""

@@ -166,6 +166,26 @@ def test_return_types_follow_the_reference():
     assert "ModulationWithOffsets{T}[" in body and "ModulationNoOffsets{T}[" in body
     assert re.search(r"likelihood = T\[p\.chi2 for p in params\]", body)
     assert re.search(r"return \(output, param, likelihood\)", body)
+    # eltype(output) == eltype(data) for every T (advisor r5): the library returns ComplexF32 or
+    # ComplexF64 columns; for any other T (Float16, BigFloat) the shim must hand back
+    # copy(data) with the demodulated columns converted into it.  Julia is absent here, so the
+    # element type each branch leaves in `output` is traced from the source:
+    conv = re.search(r"if !\(T === Float32 \|\| T === Float64\)\s*\n\s*out = copy\(data\)\s*\n"
+                     r"\s*out\[:, 1:32\] \.= Complex\{T\}\.\(view\(output, :, 1:32\)\)\s*\n"
+                     r"\s*output = out\s*\n\s*end", body)
+    assert conv, "non-Float32/Float64 element types must get copy(data) back"
+    assert body.index("output = similar(d)") < conv.start() < body.index("return (output")
+
+    def traced_eltype(T):  # the shim's branches, as written above
+        c32 = T == "Float32"
+        d = "ComplexF32" if c32 else "ComplexF64"
+        out = d  # output = similar(d)
+        if T not in ("Float32", "Float64"):
+            out = f"Complex{{{T}}}"  # copy(data)
+        return out
+    for T, want in (("Float16", "Complex{Float16}"), ("Float32", "ComplexF32"),
+                    ("Float64", "ComplexF64"), ("BigFloat", "Complex{BigFloat}")):
+        assert traced_eltype(T) == want, T
     # the χ² functor returns T as lkl does (src/Modulation.jl:318-326)
     body = _function_body(src, "chi2_gpu")
     assert "data::AbstractMatrix{Complex{T}}" in body

@@ -1,7 +1,9 @@
 #!/usr/bin/env bash
-# A/B of library builds / env knobs on one box, interleaved rounds (box-to-box spread is ~6 %,
-# so only same-box comparisons count).  Usage: tools/ab_bench.sh <tag> <rounds> <bench args> -- <variant>...
-# A variant is "name:ENV=val,ENV2=val" ("base:" = no env); GPD_LIB=old loads libgpdemod_old.so.
+# A/B of library builds on one box, interleaved rounds (box-to-box spread is ~6 %, so only
+# same-box comparisons count).  Usage: tools/ab_bench.sh <tag> <rounds> <bench args> -- <variant>...
+# A variant is "name:GPD_LIB=x" ("base:" = the release library); GPD_LIB=old loads
+# libgpdemod_old.so.  The library reads no environment variable and bench.py applies no options,
+# so a build variant (build.py --variant) is the only knob here.
 set -euo pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 TAG=$1; ROUNDS=$2; shift 2
