@@ -178,7 +178,7 @@ def check(rc: int, errbuf=None):
 
 
 LIBM_FN = {"sin": 0, "cos": 1, "sincos": 2, "atan": 3, "atan2": 4, "hypot": 5, "rem_pio2": 6, "hypot_nb": 7,
-           "sin_sel": 8, "sincos_sel": 9}
+           "sin_sel": 8, "sincos_sel": 9, "sin_ph_shift": 10}
 
 
 def libm_eval(fn: str, x, y=None, device: int = 0):

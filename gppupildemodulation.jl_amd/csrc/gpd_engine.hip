@@ -181,7 +181,8 @@ struct Layout {
     long long unit_len; // samples per unit
     size_t smask, dlist, fixp, ftab;  // faint state-split moments (k_moments_ws<FAINT>)
     size_t fsp, fcnt, fixs;           // fused faint statistics (k_moments_ws<FAINT> producers)
-    size_t prep;                      // k_prepare_part's partial (count, min, max) per workgroup
+    size_t prep;                      // k_prepare_part's partial (count, min, max, bad) per workgroup
+    size_t pht;                       // exact path: Payne–Hanek table of fl(ω t) (k_ph_table)
     bool fs1;           // faint statistics in one pass (k_faint_p1/p2/fin), cohorts of fs_pc
     long long fs_pc;    // series per cohort
     int fs_mmax;        // samples per thread and part: ⌈N/2048⌉
@@ -322,7 +323,7 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     const long long nch = U;  // partial-moment sets (units)
     L.info = take(sizeof(Info));
     L.prof = take(PROF_LEN * sizeof(unsigned long long));  // diagnostic counters
-    L.prep = take((size_t)((N + PREP_PER - 1) / PREP_PER) * 3 * sizeof(double));  // k_prepare_part
+    L.prep = take((size_t)((N + PREP_PER - 1) / PREP_PER) * 4 * sizeof(double));  // k_prepare_part
     // cos/sin table, padded to whole MM_TS-sample tiles (k_table_mix fills the padding)
     L.tab = take(harmonic ? (size_t)((N + MM_TS - 1) / MM_TS * MM_TS) * 2 * KH * sizeof(double) : 0);
     // windowed series: k_moments_win writes mom directly (no partial moments)
@@ -377,6 +378,7 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     L.fsx = take(L.fs1 ? (size_t)L.fs_pc * FS_G * L.fs_mmax * 256 * sizeof(double) : 0);
     L.fsc = take(L.fs1 ? (size_t)L.fs_pc * FS_G * (FS_NV + 8) * sizeof(double) : 0);
     L.xr32 = take(fp32 ? (size_t)N * sizeof(float) : 0);  // F_FP32 phase table
+    L.pht = take(!harmonic && !fp32 ? (size_t)N * 3 * sizeof(uint64_t) : 0);
     L.total = off;
     return L;
 }
@@ -814,6 +816,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     pb.prof = (unsigned long long *)(ws + L.prof);
     pb.fit_lanes = 0;
     pb.xr32 = fp32 ? (const float *)(ws + L.xr32) : nullptr;
+    pb.pht = nullptr;
     Param *outp = (Param *)out_params;
 
     int nt = 0, ne = 0;
@@ -908,6 +911,10 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     int *dbsum = dhdr + 6;
     const unsigned defer_blocks = (unsigned)(((N + MM_TS - 1) / MM_TS + 1023) / 1024);
     auto faint_defer = [&]() {
+        if ((N + MM_TS - 1) / MM_TS <= kDeferOneTiles) {  // one workgroup, one launch (r6)
+            k_faint_defer_one<<<1, 1024, 0, stream>>>(pb, dlist, dhdr);
+            return;
+        }
         k_faint_defer_count<<<defer_blocks, 1024, 0, stream>>>(pb, dbsum);
         k_faint_defer_list<<<defer_blocks, 1024, 0, stream>>>(pb, dbsum, dlist, dhdr);
     };
@@ -964,7 +971,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                 k_fix_table<<<ftab_grid, 256, 0, stream>>>(pb, dlist, dhdr, ftab);
                 mark("faint_defer");
             }
-            if (faint) k_moments_fix<<<dim3((unsigned)n, FST_SLOTS), 256, 0, stream>>>(sp, dlist, dhdr, ftab, fix_c, fixs_c);
+            if (faint) k_moments_fix<<<(unsigned)n, 256, 0, stream>>>(sp, dlist, dhdr, ftab, fix_c, fixs_c);
             if (faint && is_c32 && tm)
                 k_moments_ws<0, false, c32, 2, true, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, smask, fsp_c, fcnt, dhdr);
             else if (faint && tm)
@@ -1066,7 +1073,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             if (faint) {  // the deferred samples of the state-split pass (usually none)
                 faint_defer();
                 k_fix_table<<<ftab_grid, 256, 0, stream>>>(pb, dlist, dhdr, ftab);
-                k_moments_fix<<<dim3((unsigned)P, FST_SLOTS), 256, 0, stream>>>(pb, dlist, dhdr, ftab, fixp, fixs);
+                k_moments_fix<<<(unsigned)P, 256, 0, stream>>>(pb, dlist, dhdr, ftab, fixp, fixs);
                 mark("faint_defer");
             }
             if (faint && is_c32 && tmix)  // faint series: the producer/consumer kernel, state-split
@@ -1217,18 +1224,21 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         // fallback: series whose fit left the expansion's safe range, re-fitted exactly — faint
         // ones with the two-pass statistics of the listed series (the oracle's bits), not the
         // fused ones the harmonic fit used
+        // (one workgroup per CU walks the list — one round of the exact fit's one-workgroup-
+        // per-CU occupancy; an empty list costs the launch of n_cu workgroups, not of 1024)
+        const unsigned fb_grid = (unsigned)std::min<long long>(P, std::max(1, cx->n_cu));
         if (fused) {
-            k_faint_stats_list<<<exact_grid, 256, 0, stream>>>(pb, list, count, fstat);
+            k_faint_stats_list<<<fb_grid, 256, 0, stream>>>(pb, list, count, fstat);
             mark("fallback_stats");
         }
         if (faint)
-            k_fit_exact<true, false, false><<<exact_grid, EXACT_WG, 0, stream>>>(
+            k_fit_exact<true, false, false><<<fb_grid, EXACT_WG, 0, stream>>>(
                 pb, info, nullptr, fstat, list, count, outp, raw, ST_FALLBACK);
         else if (harm_offs)
-            k_fit_exact<false, true, false><<<exact_grid, EXACT_WG, 0, stream>>>(
+            k_fit_exact<false, true, false><<<fb_grid, EXACT_WG, 0, stream>>>(
                 pb, info, nullptr, fstat, list, count, outp, raw, ST_FALLBACK);
         else
-            k_fit_exact<false, false, false><<<exact_grid, EXACT_WG, 0, stream>>>(
+            k_fit_exact<false, false, false><<<fb_grid, EXACT_WG, 0, stream>>>(
                 pb, info, nullptr, fstat, list, count, outp, raw, ST_FALLBACK);
         mark("fit_fallback");
         if (harm_offs) {
@@ -1239,6 +1249,14 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         if (fp32) {
             k_phase32<<<(unsigned)((N + 255) / 256), 256, 0, stream>>>(t, N, omega, (float *)pb.xr32);
             mark("phase32");
+        } else {
+            // the Payne–Hanek table of fl(ω t) (r6): the one-wave-per-SIMD fits read it in place
+            // of t when every phase lies in one binade of the Payne–Hanek regime (MJD-scale
+            // timestamps; ExactChi2 PHT) — built for every exact call, 24 B per sample
+            uint64_t *pht = (uint64_t *)(ws + L.pht);
+            k_ph_table<<<(unsigned)((N + 255) / 256), 256, 0, stream>>>(t, N, omega, pht);
+            pb.pht = pht;
+            mark("ph_table");
         }
         if (phbuf) {
             dim3 g((unsigned)std::min<long long>((N + 255) / 256, 256), (unsigned)n_fc);
@@ -1905,9 +1923,20 @@ int gpd_process_volt(int64_t n_samples, const double *t, const float *volt, int6
 int gpd_libm_eval(int fn, int64_t n, const double *x, const double *y, double *out, int device) {
     char *errbuf = nullptr;
     size_t errlen = 0;
-    if (fn < 0 || fn > 9 || n < 0 || (n > 0 && (!x || !out)) ||
-        ((fn == 4 || fn == 5 || fn == 7) && n > 0 && !y))
+    if (fn < 0 || fn > 10 || n < 0 || (n > 0 && (!x || !out)) ||
+        ((fn == 4 || fn == 5 || fn == 7 || fn == 10) && n > 0 && !y))
         return GPD_E_ARG;
+    // fn 10: jl_sin(fl(x[i] + y[0])) through the Payne–Hanek table and shift; the shift of the
+    // whole x range is formed here on the host (the same jlm_ph_shift) and handed to the device
+    uint64_t shift[4] = {0, 0, 0, 0};
+    if (fn == 10 && n > 0) {
+        double xmin = x[0], xmax = x[0];
+        for (int64_t i = 1; i < n; ++i) {
+            xmin = std::min(xmin, x[i]);
+            xmax = std::max(xmax, x[i]);
+        }
+        shift[3] = (uint64_t)jlm_ph_shift(xmin, xmax, y[0], &shift[0], &shift[1], &shift[2]);
+    }
     const int ndev = gpd_device_count();
     if (ndev <= 0) return GPD_E_NODEV;
     if (device < 0 || device >= ndev) return GPD_E_ARG;
@@ -1921,14 +1950,16 @@ int gpd_libm_eval(int fn, int64_t n, const double *x, const double *y, double *o
         (void)hipFree(dout);
     };
     if (hipMalloc(&dx, n * sizeof(double)) != hipSuccess ||
-        hipMalloc(&dy, n * sizeof(double)) != hipSuccess ||
+        hipMalloc(&dy, std::max<int64_t>(n, 4) * sizeof(double)) != hipSuccess ||
         hipMalloc(&dout, n * width * sizeof(double)) != hipSuccess) {
         release();
         (void)hipGetLastError();
         return GPD_E_OOM;
     }
     hipError_t e = hipMemcpy(dx, x, n * sizeof(double), hipMemcpyHostToDevice);
-    if (e == hipSuccess)
+    if (e == hipSuccess && fn == 10)
+        e = hipMemcpy(dy, shift, sizeof shift, hipMemcpyHostToDevice);  // dy holds ≥ 4 words
+    else if (e == hipSuccess)
         e = hipMemcpy(dy, y ? y : x, n * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) {
         k_libm<<<(unsigned)((n + 255) / 256), 256>>>(fn, n, dx, dy, dout);

@@ -380,14 +380,9 @@ JLM_FN void jlm_ph_words(int e, uint64_t *a1, uint64_t *a2, uint64_t *a3) {
 }
 JLM_FN int jlm_biased_exponent(double x) { return (int)((jlm_bits(x) >> 52) & 0x7ffu); }
 /* jlm_paynehanek on x's binade words; regime |x| ≥ 2^20·π/2, finite */
-JLM_FN int jlm_paynehanek_w(double x, uint64_t a1, uint64_t a2, uint64_t a3, double *yhi,
-                            double *ylo) {
-    const uint64_t X = (jlm_bits(x) & 0x000fffffffffffffull) | (1ull << 52);
-    const jlm_u128 w1 = (jlm_u128)(X * a1) << 64;
-    const jlm_u128 w2 = (jlm_u128)X * a2;
-    const jlm_u128 w3 = ((jlm_u128)X * a3) >> 64;
-    const jlm_u128 wp = w1 + w2 + w3;
-    const jlm_u128 w = __builtin_signbit(x) ? (jlm_u128)0 - wp : wp;
+/* Payne–Hanek after the product: wp = the 128-bit fraction of |x|·(2/π)/4 (mod 1), neg = x < 0 */
+JLM_FN int jlm_ph_tail(jlm_u128 wp, int neg, double *yhi, double *ylo) {
+    const jlm_u128 w = neg ? (jlm_u128)0 - wp : wp;
     const int q = (int)(((int64_t)(uint64_t)(w >> 125) + 1) >> 1);
     const jlm_i128 f = (jlm_i128)(w << 2);
     double zhi, zlo;
@@ -398,6 +393,14 @@ JLM_FN int jlm_paynehanek_w(double x, uint64_t a1, uint64_t a2, uint64_t a3, dou
     *yhi = yh;
     *ylo = (((zhi * pio2_hi - yh) + zhi * pio2_lo) + zlo * pio2_hi) + zlo * pio2_lo;
     return q;
+}
+JLM_FN int jlm_paynehanek_w(double x, uint64_t a1, uint64_t a2, uint64_t a3, double *yhi,
+                            double *ylo) {
+    const uint64_t X = (jlm_bits(x) & 0x000fffffffffffffull) | (1ull << 52);
+    const jlm_u128 w1 = (jlm_u128)(X * a1) << 64;
+    const jlm_u128 w2 = (jlm_u128)X * a2;
+    const jlm_u128 w3 = ((jlm_u128)X * a3) >> 64;
+    return jlm_ph_tail(w1 + w2 + w3, __builtin_signbit(x), yhi, ylo);
 }
 JLM_FN int jlm_paynehanek_nb(double x, double *yhi, double *ylo) {
     uint64_t a1, a2, a3;
@@ -464,6 +467,67 @@ JLM_FN double jl_sin_ph_w(double x, uint64_t a1, uint64_t a2, uint64_t a3) {
     const int n = jlm_paynehanek_w(x, a1, a2, a3, &hi, &lo);
     return jlm_sin_quadrant(n, hi, lo);
 }
+/* ---- Payne–Hanek of θ = fl(x + ϕ) from a per-sample precomputation of x (r6) -------------
+ * The exact evaluator's sin(θ) for MJD-scale phases: x = fl(ω t) is fixed per sample and every
+ * evaluation adds one ϕ.  When every x lies in one binade e (mantissa X ∈ [2^52, 2^53), ulp
+ * u = 2^(e−1075)) and r = ϕ/u is not a half-integer, θ = x + δ·u with δ = rint(r) for every x
+ * (fl(x + ϕ) is the multiple of u nearest x + ϕ) as long as X + δ stays inside the binade — so θ's
+ * mantissa is X + δ and Payne–Hanek's products are linear in it:
+ *   (X+δ)·a1 mod 2^64 = X·a1 + δ·a1,   (X+δ)·a2 = X·a2 + δ·a2,
+ *   ⌊(X+δ)·a3 / 2^64⌋ = ⌊X·a3 / 2^64⌋ + ⌊δ·a3 / 2^64⌋ + carry(X·a3 mod 2^64 + δ·a3 mod 2^64)
+ * (all mod 2^128; ⌊·⌋ of the signed δ·a3 is an arithmetic shift).  The table holds per sample
+ * W = (X·a1 mod 2^64)·2^64 + X·a2 + ⌊X·a3 / 2^64⌋ and A3 = X·a3 mod 2^64; an evaluation forms
+ * K = δ·a1·2^64 + δ·a2 + ⌊δ·a3 / 2^64⌋ and D3 = δ·a3 mod 2^64 once; then per sample
+ *   w(θ) = W + K + [A3 + D3 ≥ 2^64]   — the 128-bit word jlm_paynehanek_w computes for θ,
+ * bit for bit, with two 64-bit adds in place of three 64×64-bit products. */
+JLM_FN void jlm_ph_table_entry(double x, uint64_t *wlo, uint64_t *whi, uint64_t *a3lo) {
+    uint64_t a1, a2, a3;
+    jlm_ph_words(jlm_biased_exponent(x), &a1, &a2, &a3);
+    const uint64_t X = (jlm_bits(x) & 0x000fffffffffffffull) | (1ull << 52);
+    const jlm_u128 p3 = (jlm_u128)X * a3;
+    const jlm_u128 W = ((jlm_u128)(X * a1) << 64) + (jlm_u128)X * a2 + (p3 >> 64);
+    *wlo = (uint64_t)W;
+    *whi = (uint64_t)(W >> 64);
+    *a3lo = (uint64_t)p3;
+}
+/* the per-evaluation shift for xmin ≤ every x ≤ xmax (one binade, Payne–Hanek regime, positive):
+ * 1 and (K, D3) when the table applies to θ = fl(x + ϕ), else 0 */
+JLM_FN int jlm_ph_shift(double xmin, double xmax, double phi, uint64_t *klo, uint64_t *khi,
+                        uint64_t *d3lo) {
+    const int e0 = jlm_biased_exponent(xmin);
+    if (!(xmin > 0.0) || !(xmax >= xmin) || jlm_biased_exponent(xmax) != e0 || e0 == 0x7ff ||
+        e0 - 1023 < 21) /* θ ≥ 2^21 > 2^20·π/2: the Payne–Hanek regime of jl_sin */
+        return 0;
+    const double r = __builtin_ldexp(phi, 1075 - e0); /* ϕ / u, exact */
+    if (!(__builtin_fabs(r) < 0x1p40)) return 0;       /* NaN, huge */
+    const double d0 = __builtin_rint(r);
+    if (__builtin_fabs(r - d0) == 0.5) return 0; /* a tie: fl(x + ϕ) depends on X's parity */
+    const int64_t dl = (int64_t)d0;
+    const int64_t Xmin = (int64_t)((jlm_bits(xmin) & 0x000fffffffffffffull) | (1ull << 52));
+    const int64_t Xmax = (int64_t)((jlm_bits(xmax) & 0x000fffffffffffffull) | (1ull << 52));
+    if (Xmin + dl - 1 < (int64_t)(1ull << 52) || Xmax + dl + 1 > (int64_t)((1ull << 53) - 1))
+        return 0; /* some θ could leave the binade (or round across its edge) */
+    uint64_t a1, a2, a3;
+    jlm_ph_words(e0, &a1, &a2, &a3);
+    const uint64_t D1 = (uint64_t)dl * a1;
+    const jlm_i128 D2 = (jlm_i128)dl * (jlm_i128)(jlm_u128)a2;
+    const jlm_i128 D3 = (jlm_i128)dl * (jlm_i128)(jlm_u128)a3;
+    const jlm_u128 K = ((jlm_u128)D1 << 64) + (jlm_u128)D2 + (jlm_u128)(D3 >> 64);
+    *klo = (uint64_t)K;
+    *khi = (uint64_t)(K >> 64);
+    *d3lo = (uint64_t)D3;
+    return 1;
+}
+/* jl_sin(θ) from the sample's table entry and the evaluation's shift (θ > 0, regime above) */
+JLM_FN double jl_sin_ph_shifted(uint64_t wlo, uint64_t whi, uint64_t a3lo, uint64_t klo,
+                                uint64_t khi, uint64_t d3lo) {
+    const uint64_t c = (uint64_t)(a3lo + d3lo < a3lo);
+    const jlm_u128 w = ((((jlm_u128)whi << 64) | wlo) + (((jlm_u128)khi << 64) | klo)) + c;
+    double hi, lo;
+    const int n = jlm_ph_tail(w, 0, &hi, &lo);
+    return jlm_sin_quadrant(n, hi, lo);
+}
+
 JLM_FN double jl_sin_cwx_nb(double x) {
     double hi, lo;
     const int n = jlm_cwext_nb(x, jlm_poshighword(x), &hi, &lo);

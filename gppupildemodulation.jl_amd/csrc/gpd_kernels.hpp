@@ -81,7 +81,8 @@ struct Param {  // == gpd_param
 struct Info {
     long long nvalid;  // valid samples (shared by every series)
     int mode;          // 0: harmonic, plain ϕ; 1: harmonic, ϕ quantised to the ulp of fl(ωt); 2: exact only
-    int pad;
+    int xpos;          // 1: every valid fl(ωt) is > 0 (none negative, zero or NaN): the exact
+                       // evaluator's Payne–Hanek table may apply (jlm_ph_shift, xmin/xmax below)
     double qbase;      // mode 1: a multiple of that ulp inside the binade of fl(ωt)
     double xmin, xmax; // range of |fl(ω t)| over valid samples
     double phimax;     // mode 1: |ϕ| up to which fl(x+ϕ) stays in the binade of every x
@@ -119,6 +120,9 @@ struct Problem {
     unsigned long long *prof;  // PROF_LEN diagnostic counters (workspace), or nullptr
     int fit_lanes;             // series per k_fit_harmonic wave (0 = GPD_FIT_WAVE_LANES)
     const float *xr32;         // F_FP32: rem(fl(ω t_i), 2π) per sample (k_phase32), or nullptr
+    // exact path: Payne–Hanek table of x_i = fl(ω t_i) (k_ph_table; W lo/hi pairs [2N], then A3
+    // [N]; gpd_jlmath.h jlm_ph_table_entry), or nullptr
+    const uint64_t *pht;
 };
 
 // Column and sample range [s0, s1) of series k.
@@ -284,8 +288,8 @@ constexpr int PREP_PER = 4096;  // samples per k_prepare_part workgroup (256 thr
 __global__ __launch_bounds__(256) void k_prepare_part(Problem pb, double *__restrict__ part)
 #if GPD_OWNS(GPD_U_ENGINE)
 {
-    __shared__ double red[4 * 3];
-    double cnt = 0.0, xmn = 1.0e308, xmx = 0.0;
+    __shared__ double red[4 * 4];
+    double cnt = 0.0, xmn = 1.0e308, xmx = 0.0, bad = 0.0;
     const long long base = (long long)blockIdx.x * PREP_PER + threadIdx.x;
     constexpr int U = PREP_PER / 256;
     double tv[U];
@@ -303,33 +307,38 @@ __global__ __launch_bounds__(256) void k_prepare_part(Problem pb, double *__rest
         const int st = sv[u];
         bool ok = i < pb.N;
         if (pb.state) ok = ok && st != -1 && (!(pb.flags & F_ONLY_HIGH) || st == 3 || st == 2);
-        const double x = fabs(pb.omega * tv[u]);
+        const double xs = pb.omega * tv[u], x = fabs(xs);
         cnt += ok ? 1.0 : 0.0;
+        bad += (ok && !(xs > 0.0)) ? 1.0 : 0.0;  // negative, zero or NaN fl(ωt)
         xmn = ok ? fmin(xmn, x) : xmn;
         xmx = ok ? fmax(xmx, x) : xmx;
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         cnt += __shfl_xor(cnt, off, 64);
+        bad += __shfl_xor(bad, off, 64);
         xmn = fmin(xmn, __shfl_xor(xmn, off, 64));
         xmx = fmax(xmx, __shfl_xor(xmx, off, 64));
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) {
-        red[wave * 3] = cnt;
-        red[wave * 3 + 1] = xmn;
-        red[wave * 3 + 2] = xmx;
+        red[wave * 4] = cnt;
+        red[wave * 4 + 1] = xmn;
+        red[wave * 4 + 2] = xmx;
+        red[wave * 4 + 3] = bad;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int w = 1; w < 4; ++w) {
-            cnt += red[w * 3];
-            xmn = fmin(xmn, red[w * 3 + 1]);
-            xmx = fmax(xmx, red[w * 3 + 2]);
+            cnt += red[w * 4];
+            xmn = fmin(xmn, red[w * 4 + 1]);
+            xmx = fmax(xmx, red[w * 4 + 2]);
+            bad += red[w * 4 + 3];
         }
-        part[3 * blockIdx.x] = cnt;
-        part[3 * blockIdx.x + 1] = xmn;
-        part[3 * blockIdx.x + 2] = xmx;
+        part[4 * blockIdx.x] = cnt;
+        part[4 * blockIdx.x + 1] = xmn;
+        part[4 * blockIdx.x + 2] = xmx;
+        part[4 * blockIdx.x + 3] = bad;
     }
 }
 #else
@@ -340,37 +349,41 @@ __global__ __launch_bounds__(256) void k_prepare_fin(const double *__restrict__ 
                                                      Info *info)
 #if GPD_OWNS(GPD_U_ENGINE)
 {
-    __shared__ double red[4 * 3];
-    double cnt = 0.0, xmn = 1.0e308, xmx = 0.0;
+    __shared__ double red[4 * 4];
+    double cnt = 0.0, xmn = 1.0e308, xmx = 0.0, bad = 0.0;
     for (int b = threadIdx.x; b < nparts; b += 256) {
-        cnt += part[3 * b];
-        xmn = fmin(xmn, part[3 * b + 1]);
-        xmx = fmax(xmx, part[3 * b + 2]);
+        cnt += part[4 * b];
+        xmn = fmin(xmn, part[4 * b + 1]);
+        xmx = fmax(xmx, part[4 * b + 2]);
+        bad += part[4 * b + 3];
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         cnt += __shfl_xor(cnt, off, 64);
+        bad += __shfl_xor(bad, off, 64);
         xmn = fmin(xmn, __shfl_xor(xmn, off, 64));
         xmx = fmax(xmx, __shfl_xor(xmx, off, 64));
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) {
-        red[wave * 3] = cnt;
-        red[wave * 3 + 1] = xmn;
-        red[wave * 3 + 2] = xmx;
+        red[wave * 4] = cnt;
+        red[wave * 4 + 1] = xmn;
+        red[wave * 4 + 2] = xmx;
+        red[wave * 4 + 3] = bad;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int w = 1; w < 4; ++w) {
-            cnt += red[w * 3];
-            xmn = fmin(xmn, red[w * 3 + 1]);
-            xmx = fmax(xmx, red[w * 3 + 2]);
+            cnt += red[w * 4];
+            xmn = fmin(xmn, red[w * 4 + 1]);
+            xmx = fmax(xmx, red[w * 4 + 2]);
+            bad += red[w * 4 + 3];
         }
         Info in;
         in.nvalid = (long long)cnt;
         in.xmin = xmn;
         in.xmax = xmx;
-        in.pad = 0;
+        in.xpos = bad == 0.0 ? 1 : 0;
         in.qbase = 0.0;
         // Rounding of θ = fl(fl(ωt) + ϕ) (src/Modulation.jl:137).  While every |fl(ωt)| ± π sits
         // in one binade [2^e, 2^(e+1)), fl(x+ϕ) = x + round(ϕ to a multiple of ulp 2^(e-52)):
@@ -1956,6 +1969,59 @@ __global__ __launch_bounds__(1024) void k_faint_defer_list(Problem pb, const int
 #endif
 
 
+// k_faint_defer_one: k_faint_defer_count + k_faint_defer_list in one workgroup (r6), for
+// exposures of at most kDeferOneTiles tiles (C5: 3125 tiles, 4 sweeps of 1024): the tiles in
+// sweeps of 1024, each sweep's listed tiles written at the running offset in tile order — the
+// same list and header as the two-kernel form (one launch and its wait instead of two).
+constexpr long long kDeferOneTiles = 16 * 1024;
+__global__ __launch_bounds__(1024) void k_faint_defer_one(Problem pb, int *__restrict__ dlist,
+                                                          int *__restrict__ dhdr)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
+    __shared__ int wcnt[16];
+    __shared__ unsigned smk;
+    __shared__ int sfirst[FST_SLOTS];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const long long nt = (pb.N + MM_TS - 1) / MM_TS;
+    if (tid == 0) smk = 0;
+    if (tid < FST_SLOTS) sfirst[tid] = 0x7fffffff;
+    int base = 0;  // entries listed by the earlier sweeps
+    for (long long j0 = 0; j0 < nt; j0 += 1024) {
+        const long long j = j0 + tid;
+        unsigned dm = 0, sm = 0;
+        int first[FST_SLOTS] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
+        if (j < nt) defer_tile(pb, j, dm, sm, first);
+        const unsigned long long b = __builtin_amdgcn_ballot_w64(dm != 0);
+        const int before = __builtin_popcountll(b & ((1ull << lane) - 1ull));
+        if (lane == 0) wcnt[wave] = __builtin_popcountll(b);
+        __syncthreads();  // (also orders the first sweep after the smk / sfirst initialisation)
+        if (sm) atomicOr(&smk, sm);
+#pragma unroll
+        for (int s = 0; s < FST_SLOTS; ++s)
+            if (first[s] != 0x7fffffff) atomicMin(&sfirst[s], first[s]);
+        int off = base, tot = 0;
+        for (int w = 0; w < 16; ++w) {
+            off += w < wave ? wcnt[w] : 0;
+            tot += wcnt[w];
+        }
+        if (dm) {
+            dlist[2 * (off + before)] = (int)j;
+            dlist[2 * (off + before) + 1] = (int)dm;
+        }
+        base += tot;
+        __syncthreads();  // wcnt is rewritten by the next sweep
+    }
+    if (tid == 0) {
+        dhdr[0] = base;
+        dhdr[1] = (int)smk;
+        for (int s = 0; s < FST_SLOTS; ++s) dhdr[2 + s] = sfirst[s] == 0x7fffffff ? 0 : sfirst[s];
+    }
+}
+#else
+;
+#endif
+
+
 // k_fix_table: cos/sin n x (n = 1..KH, k_table's recurrence) of every sample k_faint_defer
 // lists, once for all series: ftab[(e·32 + sl)·2KH + …] for entry e, sample bit sl.  Launched over
 // every possible entry (⌈N/32⌉·32 threads); threads beyond the list return.
@@ -1991,10 +2057,12 @@ __global__ __launch_bounds__(256) void k_fix_table(Problem pb, const int *__rest
 // k_moments_fix: the unweighted moments q = p̄ d of the samples k_faint_defer lists, per state:
 // fixp[(q·NMOM + row)·P + k], the rows of k_moments_ws (Σq, Σ|q|², then A, B, C, D per
 // harmonic; every state of dhdr[1] written, nothing when the list is empty).  One workgroup
-// per (series, state) (grid P × FST_SLOTS; with an empty list or a state without deferred
-// samples they return at once); thread = (harmonic group hg of 3 harmonics, sample lane sl of 32); lane sl takes
-// sample sl of each listed tile in list order (cos/sin n x from k_fix_table; entries in batches
-// of 4), the lanes are reduced by a fixed xor tree.
+// per series (r6; was one per (series, state): four times the workgroups, each re-reading the
+// listed samples for its one state — 94 → ~25 µs on C5); thread = (harmonic group hg of 3
+// harmonics, sample lane sl of 32); lane sl takes sample sl of each listed tile in list order
+// (cos/sin n x from k_fix_table; entries in batches of 4) and adds it into the accumulators of
+// its state — each state's sums see the same additions in the same order as before — and the
+// lanes are reduced by a fixed xor tree per state.
 __global__ __launch_bounds__(256) void k_moments_fix(Problem pb, const int *__restrict__ dlist,
                                                      const int *__restrict__ dhdr,
                                                      const double *__restrict__ ftab,
@@ -2007,93 +2075,108 @@ __global__ __launch_bounds__(256) void k_moments_fix(Problem pb, const int *__re
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int hg = wave * 2 + (lane >> 5), sl = lane & 31;
     const unsigned smk = (unsigned)dhdr[1];
-    const long long k = blockIdx.x;  // one workgroup per (series, state)
-    const int q = blockIdx.y;
-    if (!((smk >> q) & 1u)) return;
-    {
-        const long long doff = k * pb.ldd, foff = (long long)pb.fcop[k] * pb.ldfc;
-        double acc[12], f0r = 0.0, f0i = 0.0, w2 = 0.0;
-        double sn = 0.0, s1 = 0.0, s2 = 0.0, K = 0.0;  // fixs: the fused statistics' sums
-        if (fixs) {
+    const long long k = blockIdx.x;  // one workgroup per series
+    const long long doff = k * pb.ldd, foff = (long long)pb.fcop[k] * pb.ldfc;
+    double acc[FST_SLOTS][12], f0r[FST_SLOTS], f0i[FST_SLOTS], w2[FST_SLOTS];
+    double sn[FST_SLOTS], s1[FST_SLOTS], s2[FST_SLOTS], K[FST_SLOTS];  // fixs: fused statistics
+#pragma unroll
+    for (int q = 0; q < FST_SLOTS; ++q) {
+#pragma unroll
+        for (int c = 0; c < 12; ++c) acc[q][c] = 0.0;
+        f0r[q] = f0i[q] = w2[q] = sn[q] = s1[q] = s2[q] = K[q] = 0.0;
+        if (fixs && ((smk >> q) & 1u)) {
             const c64 z = d_at(pb, doff + dhdr[2 + q]);
-            K = jl_hypot(z.re, z.im);
+            K[q] = jl_hypot(z.re, z.im);
+        }
+    }
+    // entries in batches of 4 with every load issued up front (a list walk one entry at a
+    // time is a chain of dependent loads per entry); the same order of the sums
+    constexpr int EB = 4;
+    for (int e0 = 0; e0 < cnt; e0 += EB) {
+        long long ii[EB];
+        bool ok[EB];
+#pragma unroll
+        for (int u = 0; u < EB; ++u) {
+            const int e = e0 + u;
+            const unsigned dm = e < cnt ? (unsigned)dlist[2 * e + 1] : 0u;
+            ok[u] = (dm >> sl) & 1u;
+            ii[u] = ok[u] ? (long long)dlist[2 * e] * MM_TS + sl : 0;
+        }
+        c64 fv[EB], dvv[EB];
+        int stv[EB];
+#pragma unroll
+        for (int u = 0; u < EB; ++u) {
+            stv[u] = (int)gld(pb.state + ii[u]);
+            fv[u] = fc_at(pb, foff + ii[u]);
+            dvv[u] = d_at(pb, doff + ii[u]);
         }
 #pragma unroll
-        for (int c = 0; c < 12; ++c) acc[c] = 0.0;
-        // entries in batches of 4 with every load issued up front (a list walk one entry at a
-        // time is a chain of dependent loads per entry); the same order of the sums
-        constexpr int EB = 4;
-        for (int e0 = 0; e0 < cnt; e0 += EB) {
-            long long ii[EB];
-            bool ok[EB];
+        for (int u = 0; u < EB; ++u) {
+            if (!ok[u] || stv[u] < 0 || stv[u] >= FST_SLOTS) continue;
+            const c64 ph = unit_phasor(fv[u]);
+            const c64 dv = dvv[u];
+            const double qr = fma(ph.re, dv.re, ph.im * dv.im);
+            const double qi = fma(ph.re, dv.im, -(ph.im * dv.re));
+            const double *row = ftab + ((long long)(e0 + u) * MM_TS + sl) * (2 * KH) + 6 * hg;
+            double cn[3], snn[3];
 #pragma unroll
-            for (int u = 0; u < EB; ++u) {
-                const int e = e0 + u;
-                const unsigned dm = e < cnt ? (unsigned)dlist[2 * e + 1] : 0u;
-                ok[u] = (dm >> sl) & 1u;
-                ii[u] = ok[u] ? (long long)dlist[2 * e] * MM_TS + sl : 0;
+            for (int h = 0; h < 3; ++h) {
+                cn[h] = row[2 * h];
+                snn[h] = row[2 * h + 1];
             }
-            c64 fv[EB], dvv[EB];
+            const double ab = fs_abs(qr, qi);
 #pragma unroll
-            for (int u = 0; u < EB; ++u) {
-                ok[u] = ok[u] && gld(pb.state + ii[u]) == q;
-                fv[u] = fc_at(pb, foff + ii[u]);
-                dvv[u] = d_at(pb, doff + ii[u]);
-            }
-#pragma unroll
-            for (int u = 0; u < EB; ++u) {
-                if (!ok[u]) continue;
-                const c64 ph = unit_phasor(fv[u]);
-                const c64 dv = dvv[u];
-                const double qr = fma(ph.re, dv.re, ph.im * dv.im);
-                const double qi = fma(ph.re, dv.im, -(ph.im * dv.re));
-                const double *row = ftab + ((long long)(e0 + u) * MM_TS + sl) * (2 * KH) + 6 * hg;
+            for (int q = 0; q < FST_SLOTS; ++q) {
+                if (stv[u] != q) continue;
 #pragma unroll
                 for (int h = 0; h < 3; ++h) {
-                    const double cn = row[2 * h], sn = row[2 * h + 1];
-                    acc[4 * h + 0] = fma(qr, cn, acc[4 * h + 0]);
-                    acc[4 * h + 1] = fma(qi, sn, acc[4 * h + 1]);
-                    acc[4 * h + 2] = fma(qi, cn, acc[4 * h + 2]);
-                    acc[4 * h + 3] = fma(qr, sn, acc[4 * h + 3]);
+                    acc[q][4 * h + 0] = fma(qr, cn[h], acc[q][4 * h + 0]);
+                    acc[q][4 * h + 1] = fma(qi, snn[h], acc[q][4 * h + 1]);
+                    acc[q][4 * h + 2] = fma(qi, cn[h], acc[q][4 * h + 2]);
+                    acc[q][4 * h + 3] = fma(qr, snn[h], acc[q][4 * h + 3]);
                 }
-                f0r += qr;
-                f0i += qi;
-                w2 = fma(qr, qr, fma(qi, qi, w2));
-                const double y = fs_abs(qr, qi) - K;
-                sn += 1.0;
-                s1 += y;
-                s2 = fma(y, y, s2);
+                f0r[q] += qr;
+                f0i[q] += qi;
+                w2[q] = fma(qr, qr, fma(qi, qi, w2[q]));
+                const double y = ab - K[q];
+                sn[q] += 1.0;
+                s1[q] += y;
+                s2[q] = fma(y, y, s2[q]);
             }
         }
+    }
+#pragma unroll
+    for (int q = 0; q < FST_SLOTS; ++q) {
+        if (!((smk >> q) & 1u)) continue;  // uniform
 #pragma unroll
         for (int off = 1; off < 32; off <<= 1) {
 #pragma unroll
-            for (int c = 0; c < 12; ++c) acc[c] += __shfl_xor(acc[c], off, 64);
-            f0r += __shfl_xor(f0r, off, 64);
-            f0i += __shfl_xor(f0i, off, 64);
-            w2 += __shfl_xor(w2, off, 64);
+            for (int c = 0; c < 12; ++c) acc[q][c] += __shfl_xor(acc[q][c], off, 64);
+            f0r[q] += __shfl_xor(f0r[q], off, 64);
+            f0i[q] += __shfl_xor(f0i[q], off, 64);
+            w2[q] += __shfl_xor(w2[q], off, 64);
             if (fixs && hg == 0) {
-                sn += __shfl_xor(sn, off, 64);
-                s1 += __shfl_xor(s1, off, 64);
-                s2 += __shfl_xor(s2, off, 64);
+                sn[q] += __shfl_xor(sn[q], off, 64);
+                s1[q] += __shfl_xor(s1[q], off, 64);
+                s2[q] += __shfl_xor(s2[q], off, 64);
             }
         }
         if (fixs && hg == 0 && sl == 0) {
             double *o = fixs + (long long)q * 3 * pb.P + k;
-            o[0] = sn;
-            o[pb.P] = s1;
-            o[2 * pb.P] = s2;
+            o[0] = sn[q];
+            o[pb.P] = s1[q];
+            o[2 * pb.P] = s2[q];
         }
         if (sl == 0) {
             double *o = fixp + (long long)q * NMOM * pb.P + k;
 #pragma unroll
             for (int h = 0; h < 3; ++h)
 #pragma unroll
-                for (int c = 0; c < 4; ++c) o[(long long)(3 + 4 * (3 * hg + h) + c) * pb.P] = acc[4 * h + c];
+                for (int c = 0; c < 4; ++c) o[(long long)(3 + 4 * (3 * hg + h) + c) * pb.P] = acc[q][4 * h + c];
             if (hg == 0) {
-                o[0] = f0r;
-                o[pb.P] = f0i;
-                o[2 * pb.P] = w2;
+                o[0] = f0r[q];
+                o[pb.P] = f0i[q];
+                o[2 * pb.P] = w2[q];
             }
         }
     }
@@ -2670,7 +2753,21 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 #ifndef GPD_EXACT_NT
 #define GPD_EXACT_NT 1
 #endif
-template <bool FAINT, bool OFFS, bool PHBUF, int UR = CR_UR, int WGT = EXACT_WG>
+// A sample's Payne–Hanek table entry (PHT instances; gpd_jlmath.h jlm_ph_table_entry) and an
+// evaluation's shift of it (jlm_ph_shift)
+template <bool ON> struct PhRaw {
+    uint64_t w0, w1, a3;
+};
+template <> struct PhRaw<false> {};
+struct PhShift {
+    bool on;
+    uint64_t klo, khi, d3;
+};
+// PHT (r6, the one-wave-per-SIMD instances: one exposure at G workgroups per series): with MJD-scale
+// phases, the first pass reads each sample's Payne–Hanek table entry in place of t and forms
+// sin(θ) from it and the evaluation's shift — the bits of jl_sin(fl(fl(ωt) + ϕ)) with two 64-bit
+// adds per sample in place of Payne–Hanek's three 64×64-bit products (gpd_jlmath.h).
+template <bool FAINT, bool OFFS, bool PHBUF, int UR = CR_UR, int WGT = EXACT_WG, bool PHT = false>
 struct ExactChi2 {
     static constexpr bool kOffs = OFFS;
     const Problem *pb;
@@ -2696,6 +2793,9 @@ struct ExactChi2 {
     // exchange (barrier) and the whole fit, per workgroup
     bool prof;
     unsigned long long pc[3];
+    // PHT: the range of fl(ωt) over the valid samples (Info xmin / xmax when every one is > 0;
+    // 0 otherwise: the table is never used)
+    double phx0, phx1;
 
     // Global-address-space views of the problem's arrays, taken once per evaluation: this
     // functor runs out of line, where plain pointers are generic and every flat load's wait
@@ -2719,6 +2819,8 @@ struct ExactChi2 {
         long long s0;
         long long doff, foff;   // series column / raw FC column offsets
         const double *m5, *w5;  // faint power and weight per state (the functor's)
+        const __attribute__((address_space(1))) uint64_t *pht;  // PHT: the Payne–Hanek table
+        long long N;
     };
     __device__ __forceinline__ View view() const {
         View v;
@@ -2738,6 +2840,8 @@ struct ExactChi2 {
         v.foff = foff;
         v.m5 = m5;
         v.w5 = w5;
+        v.pht = (const __attribute__((address_space(1))) uint64_t *)(PHT ? pb->pht : nullptr);
+        v.N = pb->N;
         return v;
     }
     typedef __attribute__((address_space(1))) c64 gmc64;
@@ -2804,6 +2908,7 @@ struct ExactChi2 {
         c64 f, d;
         double t;
         int st;
+        PhRaw<PHT> ph;  // PHT: the table entry (loaded in place of t when the shift applies)
     };
     // FAST (r4): ComplexF64 storage, Float64 arithmetic, and the state
     // array present exactly when FAINT — every load of a sample unconditional, so that the
@@ -2823,6 +2928,19 @@ struct ExactChi2 {
         r.t = v.xr ? (double)v.xr[i] : v.t[i];  // F_FP32: the reduced phase instead of t
         r.f = PHBUF ? ld_s(v.src + i) : (v.fc32 ? ld(v.fc32 + v.foff + i) : ld_s(v.fc + v.foff + i));
         r.d = d_of(v, v.doff + i);
+    }
+    // PHT: the FAST loads with the sample's table entry in place of t
+    __device__ __forceinline__ void load_raw_ph(const View &v, long long i, Raw &r) const {
+        if constexpr (PHT) {
+            typedef uint64_t u2v __attribute__((ext_vector_type(2)));
+            r.st = FAINT ? (int)v.state[i] : 0;
+            const u2v w = *(const __attribute__((address_space(1))) u2v *)(v.pht + 2 * i);
+            r.ph.w0 = w.x;
+            r.ph.w1 = w.y;
+            r.ph.a3 = v.pht[2 * v.N + i];
+            r.f = PHBUF ? ld_s(v.src + i) : ld_s(v.fc + v.foff + i);
+            r.d = ld_s(v.d + v.doff + i);
+        }
     }
     template <bool FAST = false>
     __device__ __forceinline__ void load_res(const View &v, long long i, Raw &r) const {
@@ -2879,8 +2997,8 @@ struct ExactChi2 {
     template <int U>
     __device__ __forceinline__ void model_batch(const View &v, const Raw (&X)[U], double b,
                                                 double phi, c64 (&m)[U]) const {
-        double th[U], s[U], be[U];
-        int ph = 1, cw = 1, sm = 1;
+        double th[U], s[U];
+        int ph = 1, cw = 1;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             th[u] = v.omega * X[u].t;
@@ -2911,6 +3029,27 @@ struct ExactChi2 {
 #pragma unroll
             for (int u = 0; u < U; ++u) s[u] = jl_sin(th[u]);
         }
+        model_tail<U>(v, X, b, s, m);
+    }
+    // model_batch from the samples' Payne–Hanek table entries and the evaluation's shift (PHT,
+    // sh.on): sin(θ) = jl_sin_ph_shifted — jl_sin(fl(fl(ωt) + ϕ))'s bits
+    template <int U>
+    __device__ __forceinline__ void model_batch_ph(const View &v, const Raw (&X)[U], double b,
+                                                   const PhShift &sh, c64 (&m)[U]) const {
+        double s[U];
+        if constexpr (PHT) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                s[u] = jl_sin_ph_shifted(X[u].ph.w0, X[u].ph.w1, X[u].ph.a3, sh.klo, sh.khi, sh.d3);
+        }
+        model_tail<U>(v, X, b, s, m);
+    }
+    // β = b·sin θ, exp(ȷβ) and the model of U samples from their sin θ
+    template <int U>
+    __device__ __forceinline__ void model_tail(const View &v, const Raw (&X)[U], double b,
+                                               const double (&s)[U], c64 (&m)[U]) const {
+        double be[U];
+        int sm = 1;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             be[u] = b * s[u];
@@ -3207,6 +3346,25 @@ struct ExactChi2 {
             },
             tot);
     }
+    // The first pass of an evaluation (the model, its sums, the model cache): from the samples'
+    // Payne–Hanek table entries when the evaluation's shift applies (PHT, FAST), else from t
+    template <int NV, bool FAST, class A>
+    __device__ __forceinline__ void first_pass(const View &V, double b, double phi,
+                                               const PhShift &sh, A &&accum, double (&v)[NV]) {
+        if constexpr (PHT && FAST) {
+            if (sh.on) {  // uniform
+                cr_sum2m<NV>(
+                    [&](long long i, Raw &r) { load_raw_ph(V, i, r); },
+                    [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch_ph(V, X, b, sh, mb); },
+                    accum, v);
+                return;
+            }
+        }
+        cr_sum2m<NV>(
+            [&](long long i, Raw &r) { load_raw<FAST>(V, i, r); },
+            [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch(V, X, b, phi, mb); },
+            accum, v);
+    }
     __device__ double operator()(const double (&xx)[2]) {
         ++nfev;
         const View V = view();
@@ -3218,11 +3376,13 @@ struct ExactChi2 {
     __device__ __forceinline__ double eval(const View &V, const double b, const double phi) {
         const bool mcg = mc != nullptr;  // a model cache
         const unsigned long long tp0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+        PhShift sh{};
+        if constexpr (PHT && FAST)
+            sh.on = V.pht != nullptr && jlm_ph_shift(phx0, phx1, phi, &sh.klo, &sh.khi, &sh.d3);
         if (OFFS) {
             double v[8];  // a11, a12(2), a22, b1(2), b2(2)
-            cr_sum2m<8>(
-                [&](long long i, Raw &r) { load_raw<FAST>(V, i, r); },
-                [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch(V, X, b, phi, mb); },
+            first_pass<8, FAST>(
+                V, b, phi, sh,
                 [&](long long i, const Raw &r, const c64 &m, double (&a)[8]) {
                     if (!valid_st<FAST>(V, r.st)) return;
                     c64 p;
@@ -3278,9 +3438,8 @@ struct ExactChi2 {
             a_im = aa.im;
         } else {
             double v[4];  // num(2), den(2)
-            cr_sum2m<4>(
-                [&](long long i, Raw &r) { load_raw<FAST>(V, i, r); },
-                [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch(V, X, b, phi, mb); },
+            first_pass<4, FAST>(
+                V, b, phi, sh,
                 [&](long long i, const Raw &r, const c64 &m, double (&a)[4]) {
                     if (!valid_st<FAST>(V, r.st)) return;
                     c64 p;
@@ -3444,6 +3603,10 @@ __global__ __launch_bounds__(WGT, MINB) void k_fit_exact(Problem pb, const Info 
     // read/write the same addresses), instead of replicated in every thread's registers
     __shared__ Newuoa<2, 5, true> nwx[WGT / 64];
     const double nvalid = (double)info->nvalid;
+    // the Payne–Hanek table path in the one-wave-per-SIMD instances (registers to spare for the
+    // wider prefetched samples); its range of fl(ωt) when every valid one is > 0
+    constexpr bool kPHT = MINB == 1 && WGT == EXACT_WG;
+    const double phx0 = info->xpos ? info->xmin : 0.0, phx1 = info->xpos ? info->xmax : 0.0;
     if (WGT == EXACT_WG && G > 1) {  // one series per G workgroups
       // one round of gridDim.x / G series (gridDim.x = G·⌈P/8⌉·8: a series' G parts are resident
       // together); written as a loop over rounds of per_round series, model-cache slot k mod
@@ -3453,9 +3616,11 @@ __global__ __launch_bounds__(WGT, MINB) void k_fit_exact(Problem pb, const Info 
         const long long k = xser(bb, G);
         if (k >= pb.P) return;  // uniform per series: all its parts leave together
         const int g = xpart(bb, G);
-        ExactChi2<FAINT, OFFS, PHBUF, (MINB == 2 ? 8 : CR_UR), WGT> f;
+        ExactChi2<FAINT, OFFS, PHBUF, (MINB == 2 ? 8 : CR_UR), WGT, kPHT> f;
         setup_exact(f, pb, k, PHBUF ? phbuf : nullptr, lds, nvalid, G, g,
                     Xchg{xtot + k * (2 * CR_BLOCKS * CR_NV), xcnt + k});
+        f.phx0 = phx0;
+        f.phx1 = phx1;
         if (mcache) f.mc = mcache + (k % per_round) * mstride;
         if (FAINT) {
 #pragma unroll
@@ -3486,8 +3651,10 @@ __global__ __launch_bounds__(WGT, MINB) void k_fit_exact(Problem pb, const Info 
     const long long total = list ? (long long)(*count) : pb.P;
     for (long long idx = blockIdx.x; idx < total; idx += gridDim.x) {
         const long long k = list ? (long long)list[idx] : idx;
-        ExactChi2<FAINT, OFFS, PHBUF, (MINB == 2 ? 8 : CR_UR), WGT> f;
+        ExactChi2<FAINT, OFFS, PHBUF, (MINB == 2 ? 8 : CR_UR), WGT, kPHT> f;
         setup_exact(f, pb, k, PHBUF ? phbuf : nullptr, lds, nvalid);
+        f.phx0 = phx0;
+        f.phx1 = phx1;
         if (mcache) f.mc = mcache + (long long)blockIdx.x * mstride;
         if (FAINT) {
 #pragma unroll
@@ -3721,6 +3888,30 @@ __global__ __launch_bounds__(256) void k_output(Problem pb, const Param *__restr
 
 
 // ---------------------------------------------------------------------------------------
+// k_ph_table: the exact evaluator's Payne–Hanek table (gpd_jlmath.h jlm_ph_table_entry) of
+// x_i = fl(ω t_i), once per call for all series: pht[2i], pht[2i+1] = W (lo, hi), pht[2N+i] = A3.
+// Used by the first pass when every x lies in one binade of the Payne–Hanek regime (MJD-scale
+// timestamps) and the evaluation's ϕ shifts them all by one whole number of ulps (jlm_ph_shift);
+// the values of samples outside that binade are never used.
+__global__ __launch_bounds__(256) void k_ph_table(const double *__restrict__ t, long long N,
+                                                  double omega, uint64_t *__restrict__ pht)
+#if GPD_OWNS(GPD_U_ENGINE)
+{
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= N) return;
+    const double x = omega * t[i];
+    uint64_t wlo = 0, whi = 0, a3 = 0;
+    if (x > 0.0 && jlm_biased_exponent(x) < 0x7ff) jlm_ph_table_entry(x, &wlo, &whi, &a3);
+    pht[2 * i] = wlo;
+    pht[2 * i + 1] = whi;
+    pht[2 * N + i] = a3;
+}
+#else
+;
+#endif
+
+
+// ---------------------------------------------------------------------------------------
 // gpd_libm_eval: the shared Julia-libm restatement evaluated on the device (bitwise tests).
 __global__ __launch_bounds__(256) void k_libm(int fn, long long n, const double *__restrict__ x,
                                               const double *__restrict__ y, double *__restrict__ out)
@@ -3748,6 +3939,13 @@ __global__ __launch_bounds__(256) void k_libm(int fn, long long n, const double 
         jl_sincos_sel(x[i], &s, &c);
         out[2 * i] = s;
         out[2 * i + 1] = c;
+        break;
+    }
+    case 10: {  // the Payne–Hanek table entry of x[i] and the shift (y: klo, khi, d3, on)
+        const uint64_t *ky = (const uint64_t *)y;
+        uint64_t wlo, whi, a3;
+        jlm_ph_table_entry(x[i], &wlo, &whi, &a3);
+        out[i] = ky[3] ? jl_sin_ph_shifted(wlo, whi, a3, ky[0], ky[1], ky[2]) : __builtin_nan("");
         break;
     }
     default: {

@@ -344,7 +344,8 @@ int gpd_synth_fill_dev(int64_t n_samples, int64_t n_pixels, int64_t pixel_offset
  * holds n (s, c) pairs), 3 atan, 4 atan(x[i], y[i]), 5 hypot(x[i], y[i]), 6 rem_pio2 (n triples
  * (quadrant, hi, lo)), 7 hypot(x[i], y[i]) in its branch-free form (the faint statistics'),
  * 8 sin and 9 sincos (pairs) through the branch-free per-regime forms the exact evaluator
- * batches (= fn 0 and 2).  Host arrays (y may be NULL for the one-argument functions),
+ * batches (= fn 0 and 2), 10 sin(fl(x[i] + y[0])) through the exact evaluator's Payne–Hanek
+ * table of x and shift of ϕ = y[0] (= fn 0 of the sum; NaN where the shift does not apply).  Host arrays (y may be NULL for the one-argument functions),
  * synchronous.
  */
 int gpd_libm_eval(int fn, int64_t n, const double *x, const double *y, double *out, int device);

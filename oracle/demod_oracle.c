@@ -668,8 +668,10 @@ int oracle_fit_batch(int64_t n_samples, int64_t n_pixels, const double *t, const
 /* Elementwise evaluation of the shared Julia-libm restatement (tests/test_jlmath.py).
  * fn: 0 sin, 1 cos, 2 sincos → (s, c) pairs in out[2i..2i+1], 3 atan, 4 atan(x[i], y[i]),
  *     5 hypot(x[i], y[i]), 6 rem_pio2 → (n, hi, lo) triples in out[3i..3i+2], 7 hypot_nb,
- *     8 sin through the branch-free regime forms, 9 sincos likewise (pairs) */
+ *     8 sin through the branch-free regime forms, 9 sincos likewise (pairs), 10 sin(fl(x[i] + y[0]))
+ *     through the Payne–Hanek table of x and the shift of ϕ = y[0] (NaN where it does not apply) */
 int oracle_jl_eval(int fn, int64_t n, const double *x, const double *y, double *out) {
+    if ((fn == 4 || fn == 5 || fn == 7 || fn == 10) && n > 0 && !y) return -1;
     for (int64_t i = 0; i < n; ++i) {
         switch (fn) {
         case 0: out[i] = jl_sin(x[i]); break;
@@ -681,6 +683,25 @@ int oracle_jl_eval(int fn, int64_t n, const double *x, const double *y, double *
         case 7: out[i] = jl_hypot_nb(x[i], y[i]); break;
         case 8: out[i] = jl_sin_sel(x[i]); break;
         case 9: jl_sincos_sel(x[i], &out[2 * i], &out[2 * i + 1]); break;
+        case 10: { /* jl_sin(fl(x[i] + y[0])) through the Payne–Hanek table and shift (NaN when
+                    * the shift does not apply to this x range and ϕ; the exact path then takes
+                    * the general forms) */
+            if (i == 0) {
+                double xmin = x[0], xmax = x[0];
+                for (int64_t k = 1; k < n; ++k) {
+                    xmin = x[k] < xmin ? x[k] : xmin;
+                    xmax = x[k] > xmax ? x[k] : xmax;
+                }
+                uint64_t klo, khi, d3;
+                const int on = jlm_ph_shift(xmin, xmax, y[0], &klo, &khi, &d3);
+                for (int64_t k = 0; k < n; ++k) {
+                    uint64_t wlo, whi, a3;
+                    jlm_ph_table_entry(x[k], &wlo, &whi, &a3);
+                    out[k] = on ? jl_sin_ph_shifted(wlo, whi, a3, klo, khi, d3) : __builtin_nan("");
+                }
+            }
+            break;
+        }
         case 6: {
             double hi, lo;
             const int q = jl_rem_pio2(x[i], &hi, &lo);

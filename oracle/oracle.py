@@ -186,7 +186,7 @@ def mean_var_power_fused(states, d, onlyhigh=False):
 
 
 JL_FN = {"sin": 0, "cos": 1, "sincos": 2, "atan": 3, "atan2": 4, "hypot": 5, "rem_pio2": 6, "hypot_nb": 7,
-         "sin_sel": 8, "sincos_sel": 9}
+         "sin_sel": 8, "sincos_sel": 9, "sin_ph_shift": 10}
 
 
 def jl_eval(fn, x, y=None):

@@ -335,6 +335,39 @@ def test_mjd_timestamps_quantised_harmonic(gpu, oracle):
     print(assert_fit_parity(got, ref, perturbed_runs(oracle, B, ulps=HARM_ULPS), label="mjd/harmonic"))
 
 
+@pytest.mark.parametrize("case", ["exposure_g8", "g1", "offsets", "faint", "binade_edge",
+                                  "far_phi"])
+def test_exact_mjd_payne_hanek_table(gpu, oracle, opts, case):
+    """The exact evaluator at MJD-scale timestamps reads each sample's Payne–Hanek table entry
+    in place of t (r6, one-wave-per-SIMD instances; gpd_jlmath.h jlm_ph_shift): every record is
+    the oracle's bit for bit — one exposure at G = 8 workgroups per series, one workgroup per
+    series, fitoffsets, faint states, an exposure whose phases straddle a binade edge (the table
+    declines: the general path), a start far in ϕ — and equals the two-waves-per-SIMD instances,
+    which never use the table."""
+    t0 = 86400.0 * 60000.0
+    P, kw, okw = 32, {}, {}
+    if case == "binade_edge":  # ω t crosses 2^35 inside the exposure
+        t0 = 2.0 ** 35 / 6.283185 - 5.0
+    B = synth.make_batch(5000, P if case != "g1" else 200, seed=33, t0=t0,
+                         offsets=case == "offsets")
+    if case == "offsets":
+        kw = dict(fitoffsets=True)
+        okw = dict(fitoffsets=True)
+    if case == "faint":
+        st = faint_states(5000, seed=5)
+        kw = okw = dict(state=st)
+    if case == "far_phi":
+        kw = okw = dict(xinit=np.array([0.6, 7.3]))
+    ref = oracle_fit(oracle, B, **okw)
+    got = fit(gpu, B, method="exact", **kw)
+    print(assert_exact_bitwise(got, ref, label=f"mjd table/{case}"))
+    opts("exact_g", 1)
+    opts("exact_waves", 2)  # MINB = 2: no table
+    got2 = fit(gpu, B, method="exact", **kw)
+    for f in ("b", "phi", "a", "c", "chi2", "nfev", "status"):
+        np.testing.assert_array_equal(got[f], got2[f], err_msg=f)
+
+
 def test_large_b_falls_back_to_exact(gpu, oracle):
     """NEWUOA probing |b| beyond the expansion's safe range (~4.5) → that series is re-fitted
     by the exact evaluator on device (status FALLBACK), with the same parity."""

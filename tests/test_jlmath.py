@@ -14,7 +14,7 @@ import math
 import os
 import re
 import sys
-from decimal import Decimal, getcontext
+from decimal import Decimal, getcontext, localcontext
 
 import numpy as np
 import pytest
@@ -281,3 +281,86 @@ def test_device_branch_free_trig_equals_oracle(gpu, oracle):
     x = _trig_regime_args(np.random.default_rng(31), 200000)
     assert same_bits(gpu.libm_eval("sin_sel", x), oracle.jl_eval("sin", x))
     assert same_bits(gpu.libm_eval("sincos_sel", x), oracle.jl_eval("sincos", x))
+
+
+PI60 = "3.14159265358979323846264338327950288419716939937510582097494"
+
+
+def _ph_shift_cases(rng):
+    """(x array in one binade, ϕ) pairs: MJD-scale exposures at 500 Hz, ϕ over ±8 rad, θ = x + ϕ
+    next to multiples of π/2 (Payne–Hanek's cancellation cases), the binade's edges, ϕ at exact
+    half-ulp ties and at integer ulps, ±0."""
+    cases = []
+    for _ in range(120):
+        t0 = 86400.0 * rng.uniform(50000, 62000)
+        t = t0 + np.arange(int(rng.integers(2, 2500))) * 0.002
+        x = 6.283185 * t
+        for phi in list(rng.uniform(-8, 8, 4)) + [0.0, -0.0, math.pi, -math.pi / 2]:
+            cases.append((x, phi))
+    # θ within a few ulps of n·π/2 (leading zeros of Payne–Hanek's fraction)
+    for k in range(200):
+        e = int(rng.integers(25, 40))
+        n = int(rng.integers(2 ** (e - 1), 2 ** e)) * 4 + int(rng.integers(0, 4))
+        with localcontext() as ctx:  # the double nearest n·π/2, π to 60 digits
+            ctx.prec = 80
+            th = float(Decimal(n) * Decimal(PI60) / 2)
+        phi = float(rng.uniform(-3, 3))
+        x = np.nextafter(th - phi, np.inf * (k % 2 - 0.5)) + np.zeros(3)
+        x[1] = np.nextafter(x[0], np.inf)
+        x[2] = np.nextafter(x[0], -np.inf)
+        cases.append((x, phi))
+    # the binade's edges, and ϕ exactly on ties / whole ulps of the binade
+    for e in (25, 34, 35, 41):
+        lo, hi = 2.0 ** e, 2.0 ** (e + 1)
+        u = 2.0 ** (e - 52)
+        for base in (lo, hi - 64 * u, lo + 1e3 * u):
+            x = base + np.arange(64) * u
+            for phi in (0.5 * u, -0.5 * u, 7.5 * u, 3 * u, -3 * u, 70 * u, -70 * u, 0.3 * u):
+                cases.append((x, phi))
+    return cases
+
+
+def test_payne_hanek_shift_equals_payne_hanek(oracle):
+    """jl_sin(fl(x + ϕ)) from the per-sample Payne–Hanek table of x and the per-evaluation shift
+    of ϕ (gpd_jlmath.h jlm_ph_table_entry / jlm_ph_shift / jl_sin_ph_shifted, r6: the exact
+    evaluator's MJD path): wherever the shift applies, the bits of jl_sin of the rounded sum; it
+    declines (NaN) exactly where θ's mantissa is not X + rint(ϕ/u) for every x — ties of ϕ/u, a θ
+    that could leave the binade — and everywhere it declines the evaluator takes the general form."""
+    rng = np.random.default_rng(61)
+    n_on = n_all = 0
+    for x, phi in _ph_shift_cases(rng):
+        got = oracle.jl_eval("sin_ph_shift", x, np.full(x.size, phi))
+        ref = oracle.jl_eval("sin", x + phi)
+        on = ~np.isnan(got)
+        assert same_bits(got[on], ref[on]).all(), (x[:3], phi)
+        e = np.frexp(x)[1]
+        u = np.ldexp(1.0, int(e[0]) - 53)
+        r = phi / u
+        tie = abs(r - np.rint(r)) == 0.5
+        one_binade = (e == e[0]).all() and (np.frexp(x + phi)[1] == e[0]).all()
+        if on.any():
+            assert not tie and one_binade
+        elif one_binade and not tie and x.min() > 2 ** 21 and abs(r) < 2 ** 40:
+            # declined only at the binade's edges (X + rint(r) ± 1 outside it)
+            X = np.frexp(x)[0] * 2.0 ** 53
+            assert (X.min() + np.rint(r) - 1 < 2 ** 52) or (X.max() + np.rint(r) + 1 > 2 ** 53 - 1)
+        n_on += int(on.sum())
+        n_all += x.size
+    assert n_on > 0.9 * n_all, (n_on, n_all)
+
+
+@pytest.mark.gpu
+def test_device_payne_hanek_shift_equals_oracle(gpu, oracle):
+    """The device's Payne–Hanek table entry and shifted sin (k_libm fn 10, the code the exact
+    evaluator's first pass runs on MJD-scale phases) give the oracle's bits, and so jl_sin's of
+    the rounded sum, on the same cases as the CPU test."""
+    rng = np.random.default_rng(62)
+    n = 0
+    for x, phi in _ph_shift_cases(rng)[::3]:
+        y = np.full(x.size, phi)
+        got = gpu.libm_eval("sin_ph_shift", x, y)
+        ref = oracle.jl_eval("sin_ph_shift", x, y)
+        on = ~np.isnan(ref)
+        assert (np.isnan(got) == ~on).all() and same_bits(got[on], ref[on]).all(), (x[:2], phi)
+        n += int((~np.isnan(got)).sum())
+    assert n > 0

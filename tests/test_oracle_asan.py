@@ -227,7 +227,7 @@ def test_libm_and_newuoa_under_sanitizers(asan, oracle):
     fns = [(name, code) for name, code in oracle.JL_FN.items()]
     payload = b""
     for name, code in fns:
-        two = name in ("atan2", "hypot", "hypot_nb")
+        two = name in ("atan2", "hypot", "hypot_nb", "sin_ph_shift")
         payload += struct.pack("<iiiq", 5, code, int(two), x.size) + x.tobytes()
         if two:
             payload += y.tobytes()
@@ -238,7 +238,7 @@ def test_libm_and_newuoa_under_sanitizers(asan, oracle):
     out = asan(payload)
     o = 0
     for name, code in fns:
-        two = name in ("atan2", "hypot", "hypot_nb")
+        two = name in ("atan2", "hypot", "hypot_nb", "sin_ph_shift")
         width = {2: 2, 6: 3, 9: 2}.get(code, 1)
         rc = struct.unpack_from("<i", out, o)[0]
         got = np.frombuffer(out, np.float64, x.size * width, o + 4)
