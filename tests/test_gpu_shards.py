@@ -311,3 +311,4 @@ def test_faint_state_pointer_alignment(gpu):
     a, b = fit(aligned), fit(odd)
     _same(b, a)
     assert not np.all(a["status"] & gpu.GPD_ST_NAN)
+
