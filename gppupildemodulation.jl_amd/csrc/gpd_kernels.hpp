@@ -2845,13 +2845,20 @@ struct ExactChi2 {
     // compiler counts the prefetched batch's loads exactly and waits only for the batch in use
     // (with the runtime storage / fp32 / state selects it fell back to waiting for all
     // outstanding loads on every path that might skip one).
-    template <bool FAST = false>
+    // D32 (FAST only, r6): ComplexF32 storage read as 8-B elements (the widened values, as the
+    // general form's d_of gives them)
+    template <bool FAST = false, bool D32 = false>
     __device__ __forceinline__ void load_raw(const View &v, long long i, Raw &r) const {
         if constexpr (FAST) {
             r.st = FAINT ? (int)v.state[i] : 0;
             r.t = v.t[i];
-            r.f = PHBUF ? ld_s(v.src + i) : ld_s(v.fc + v.foff + i);
-            r.d = ld_s(v.d + v.doff + i);
+            if constexpr (D32) {
+                r.f = PHBUF ? ld_s(v.src + i) : ld(v.fc32 + v.foff + i);
+                r.d = ld(v.d32 + v.doff + i);
+            } else {
+                r.f = PHBUF ? ld_s(v.src + i) : ld_s(v.fc + v.foff + i);
+                r.d = ld_s(v.d + v.doff + i);
+            }
             return;
         }
         r.st = v.state ? (int)v.state[i] : 0;
@@ -2872,12 +2879,15 @@ struct ExactChi2 {
             r.d = ld_s(v.d + v.doff + i);
         }
     }
-    template <bool FAST = false>
+    template <bool FAST = false, bool D32 = false>
     __device__ __forceinline__ void load_res(const View &v, long long i, Raw &r) const {
         if constexpr (FAST) {
             r.st = FAINT ? (int)v.state[i] : 0;
             r.f = ld_s(v.mc + (i - v.s0));
-            r.d = ld_s(v.d + v.doff + i);
+            if constexpr (D32)
+                r.d = ld(v.d32 + v.doff + i);
+            else
+                r.d = ld_s(v.d + v.doff + i);
             return;
         }
         r.st = v.state ? (int)v.state[i] : 0;
@@ -3278,10 +3288,10 @@ struct ExactChi2 {
     }
     // The first pass of an evaluation (the model, its sums, the model cache): from the samples'
     // Payne–Hanek table entries when the evaluation's shift applies (PHT, FAST), else from t
-    template <int NV, bool FAST, class A>
+    template <int NV, bool FAST, bool D32, class A>
     __device__ __forceinline__ void first_pass(const View &V, double b, double phi,
                                                const PhShift &sh, A &&accum, double (&v)[NV]) {
-        if constexpr (PHT && FAST) {
+        if constexpr (PHT && FAST && !D32) {
             if (sh.on) {  // uniform
                 cr_sum2m<NV>(
                     [&](long long i, Raw &r) { load_raw_ph(V, i, r); },
@@ -3291,18 +3301,109 @@ struct ExactChi2 {
             }
         }
         cr_sum2m<NV>(
-            [&](long long i, Raw &r) { load_raw<FAST>(V, i, r); },
+            [&](long long i, Raw &r) { load_raw<FAST, D32>(V, i, r); },
             [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch(V, X, b, phi, mb); },
             accum, v);
     }
     __device__ double operator()(const double (&xx)[2]) {
         ++nfev;
         const View V = view();
-        const bool fast = V.d32 == nullptr && V.fc32 == nullptr && !fp32 &&
-                          (FAINT == (V.state != nullptr)) && !(pb->flags & F_NOFAST);
-        return fast ? eval<true>(V, xx[0], xx[1]) : eval<false>(V, xx[0], xx[1]);
+        const bool nofast = (pb->flags & F_NOFAST) != 0;
+        if constexpr (!OFFS && !PHBUF) {
+            // F_FP32 with unconditional loads and a Float32 model cache (r6): ComplexF32 or
+            // ComplexF64 storage, the state array present exactly when FAINT, a model cache
+            if (fp32 && !nofast && V.mc != nullptr && (FAINT == (V.state != nullptr)) &&
+                (V.d32 != nullptr) == (V.fc32 != nullptr))
+                return V.d32 ? eval32f<true>(V, xx[0], xx[1]) : eval32f<false>(V, xx[0], xx[1]);
+        }
+        const bool fast_base = !fp32 && (FAINT == (V.state != nullptr)) && !nofast;
+        if (fast_base && V.d32 == nullptr && V.fc32 == nullptr) return eval<true>(V, xx[0], xx[1]);
+        // ComplexF32 storage, Float64 arithmetic (r6): the FAST form on 8-B elements
+        if (fast_base && V.d32 != nullptr && (PHBUF || V.fc32 != nullptr))
+            return eval<true, true>(V, xx[0], xx[1]);
+        return eval<false>(V, xx[0], xx[1]);
     }
-    template <bool FAST>
+    // ---- F_FP32, FAST form (r6).  The general form (eval<false>) selects per sample between
+    // the storage types, the phase table and the optional state, so the compiler waits for every
+    // outstanding load at each of those branches, and its model cache holds Float64 copies of the
+    // Float32 model.  Here every load is unconditional (the storage type C32 a template
+    // argument), the model cache holds the Float32 model itself (8 B per sample instead of 16:
+    // the residual pass widens the same Float32 values, so the same sums), and the stored
+    // ComplexF32 series (C32) are read as 8-B elements — the same records bit for bit as the
+    // general form (tests/test_gpu_fp32.py).
+    template <bool C32>
+    __device__ __forceinline__ void load_raw32f(const View &v, long long i, Raw &r) const {
+        r.st = FAINT ? (int)v.state[i] : 0;
+        r.t = (double)v.xr[i];
+        if constexpr (C32) {
+            r.f = ld(v.fc32 + v.foff + i);
+            r.d = ld(v.d32 + v.doff + i);
+        } else {
+            r.f = ld_s(v.fc + v.foff + i);
+            r.d = ld_s(v.d + v.doff + i);
+        }
+    }
+    typedef float nv2f __attribute__((ext_vector_type(2)));
+    template <bool C32>
+    __device__ __forceinline__ void load_res32f(const View &v, long long i, Raw &r) const {
+        r.st = FAINT ? (int)v.state[i] : 0;
+#if GPD_EXACT_NT
+        const nv2f m = __builtin_nontemporal_load(
+            (const __attribute__((address_space(1))) nv2f *)v.mc + (i - v.s0));
+#else
+        const nv2f m = ((const __attribute__((address_space(1))) nv2f *)v.mc)[i - v.s0];
+#endif
+        r.f = c64{(double)m.x, (double)m.y};
+        if constexpr (C32)
+            r.d = ld(v.d32 + v.doff + i);
+        else
+            r.d = ld_s(v.d + v.doff + i);
+    }
+    static __device__ __forceinline__ void mc_put32(const View &v, long long i, const c64 &m) {
+        const nv2f x = {(float)m.re, (float)m.im};  // the Float32 model (exact: m holds floats)
+        __attribute__((address_space(1))) nv2f *p = (__attribute__((address_space(1))) nv2f *)v.mc + (i - v.s0);
+#if GPD_EXACT_NT
+        __builtin_nontemporal_store(x, p);
+#else
+        *p = x;
+#endif
+    }
+    template <bool C32>
+    __device__ __forceinline__ double eval32f(const View &V, const double b, const double phi) {
+        double v[4];  // num(2), den(2): Float32 products, Float64 sums
+        cr_sum2m<4>(
+            [&](long long i, Raw &r) { load_raw32f<C32>(V, i, r); },
+            [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch32(V, X, b, phi, mb); },
+            [&](long long i, const Raw &r, const c64 &m, double (&a)[4]) {
+                if (!valid_st<true>(V, r.st)) return;
+                mc_put32(V, i, m);
+                const float w = weight32(V, r.st);
+                const f2 m2 = {(float)m.re, (float)m.im}, d2 = {(float)r.d.re, (float)r.d.im};
+                const f2 mwc = {m2.re * w, -(m2.im * w)};
+                const f2 xv = fmul2(mwc, d2), yv = fmul2(mwc, m2);
+                a[0] += (double)xv.re;
+                a[1] += (double)xv.im;
+                a[2] += (double)yv.re;
+                a[3] += (double)yv.im;
+            },
+            v);
+        const c64 aa = cdiv(c64{v[0], v[1]}, c64{v[2], v[3]});
+        c_re = c_im = 0.0;
+        a_re = aa.re;
+        a_im = aa.im;
+        double s[1];
+        const f2 a2 = {(float)a_re, (float)a_im};
+        cr_sum2<1, UR>([&](long long i, Raw &r) { load_res32f<C32>(V, i, r); },
+                       [&](long long i, const Raw &r, double (&a)[1]) {
+                           if (!valid_st<true>(V, r.st)) return;
+                           const f2 mm = fmul2(a2, f2{(float)r.f.re, (float)r.f.im});
+                           const float rr = mm.re - (float)r.d.re, ri = mm.im - (float)r.d.im;
+                           a[0] += (double)(weight32(V, r.st) * (rr * rr + ri * ri));
+                       },
+                       s);
+        return s[0] / nvalid;
+    }
+    template <bool FAST, bool D32 = false>
     __device__ __forceinline__ double eval(const View &V, const double b, const double phi) {
         const bool mcg = mc != nullptr;  // a model cache
         const unsigned long long tp0 = prof ? __builtin_amdgcn_s_memtime() : 0;
@@ -3311,7 +3412,7 @@ struct ExactChi2 {
             sh.on = V.pht != nullptr && jlm_ph_shift(phx0, phx1, phi, &sh.klo, &sh.khi, &sh.d3);
         if (OFFS) {
             double v[8];  // a11, a12(2), a22, b1(2), b2(2)
-            first_pass<8, FAST>(
+            first_pass<8, FAST, D32>(
                 V, b, phi, sh,
                 [&](long long i, const Raw &r, const c64 &m, double (&a)[8]) {
                     if (!valid_st<FAST>(V, r.st)) return;
@@ -3347,7 +3448,7 @@ struct ExactChi2 {
         } else if (!FAST && fp32) {
             double v[4];  // num(2), den(2): Float32 products, Float64 sums
             cr_sum2m<4>(
-                [&](long long i, Raw &r) { load_raw<FAST>(V, i, r); },
+                [&](long long i, Raw &r) { load_raw<FAST, D32>(V, i, r); },
                 [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch32(V, X, b, phi, mb); },
                 [&](long long i, const Raw &r, const c64 &m, double (&a)[4]) {
                     if (!valid_st<FAST>(V, r.st)) return;
@@ -3368,7 +3469,7 @@ struct ExactChi2 {
             a_im = aa.im;
         } else {
             double v[4];  // num(2), den(2)
-            first_pass<4, FAST>(
+            first_pass<4, FAST, D32>(
                 V, b, phi, sh,
                 [&](long long i, const Raw &r, const c64 &m, double (&a)[4]) {
                     if (!valid_st<FAST>(V, r.st)) return;
@@ -3412,7 +3513,7 @@ struct ExactChi2 {
                 a[0] += (double)(w * (rr * rr + ri * ri));
             };
             if (mcg) {
-                cr_sum2<1, UR>([&](long long i, Raw &r) { load_res<FAST>(V, i, r); },
+                cr_sum2<1, UR>([&](long long i, Raw &r) { load_res<FAST, D32>(V, i, r); },
                                   [&](long long i, const Raw &r, double (&a)[1]) {
                                       if (!valid_st<FAST>(V, r.st)) return;
                                       resid32(f2{(float)r.f.re, (float)r.f.im}, r.d,
@@ -3420,7 +3521,7 @@ struct ExactChi2 {
                                   },
                                   s);
             } else {
-                cr_sum2<1, UR>([&](long long i, Raw &r) { load_raw<FAST>(V, i, r); },
+                cr_sum2<1, UR>([&](long long i, Raw &r) { load_raw<FAST, D32>(V, i, r); },
                                   [&](long long i, const Raw &r, double (&a)[1]) {
                                       if (!valid_st<FAST>(V, r.st)) return;
                                       const f2 m2 = model32((float)r.t, power_phasor32(V, r),
@@ -3430,7 +3531,7 @@ struct ExactChi2 {
                                   s);
             }
         } else if (mcg) {  // the model the same thread wrote for element i in the first pass
-            cr_sum2<1, UR>([&](long long i, Raw &r) { load_res<FAST>(V, i, r); },
+            cr_sum2<1, UR>([&](long long i, Raw &r) { load_res<FAST, D32>(V, i, r); },
                        [&](long long i, const Raw &r, double (&a)[1]) {
                            if (!valid_st<FAST>(V, r.st)) return;
                            resid(r.f, r.d, weight_of(V, r.st), a);
@@ -3441,7 +3542,7 @@ struct ExactChi2 {
             // 8 GB): the residual pass evaluates the first pass's batched model again — the same
             // values, so the same sums (r5: 82 → 66 B per sample-evaluation, twice the model's
             // VALU work)
-            cr_sum2m<1>([&](long long i, Raw &r) { load_raw<FAST>(V, i, r); },
+            cr_sum2m<1>([&](long long i, Raw &r) { load_raw<FAST, D32>(V, i, r); },
                         [&](const Raw (&X)[CR_U], c64 (&mb)[CR_U]) { model_batch(V, X, b, phi, mb); },
                         [&](long long i, const Raw &r, const c64 &m, double (&a)[1]) {
                             if (!valid_st<FAST>(V, r.st)) return;

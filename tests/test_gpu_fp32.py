@@ -57,3 +57,29 @@ def test_fp32_rejects_offsets_and_harmonic(gpu):
     args = (B["t"], B["d"], B["fc"], B["fc_of_pixel"])
     with pytest.raises(gpu.GpdError):
         gpu.fit_batch(*args, method="fp32", fitoffsets=True)
+
+
+@pytest.mark.parametrize("storage", ["c64", "c32"])
+@pytest.mark.parametrize("faint", [False, True])
+def test_fp32_fast_form_equals_general_form(gpu, opts, storage, faint):
+    """The Float32-arithmetic evaluator's FAST form (r6: unconditional loads, the ComplexF32
+    series read as 8-B elements, a Float32 model cache) gives the general form's records bit for
+    bit (option exact_fast = 0 forces the general form), for both storage types, faint or not,
+    at one and at two waves per SIMD."""
+    N, P = 12_000, 40
+    B = synth.make_batch(N, P, seed=17)
+    st = None
+    if faint:
+        st = faint_states(N, seed=6)
+        B["d"] = B["d"] * np.where(st == 3, 1.1, np.where(st == 1, 0.01, 0.1))[None, :]
+    d, fc = B["d"], B["fc"]
+    if storage == "c32":
+        d, fc = d.astype(np.complex64), fc.astype(np.complex64)
+    args = (B["t"], d, fc, B["fc_of_pixel"])
+    for waves in (1, 2):
+        opts("exact_waves", waves)
+        opts("exact_fast", 1)
+        fast = gpu.fit_batch(*args, state=st, method="fp32")
+        opts("exact_fast", 0)
+        gen = gpu.fit_batch(*args, state=st, method="fp32")
+        assert fast.tobytes() == gen.tobytes(), (storage, faint, waves)

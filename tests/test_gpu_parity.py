@@ -636,6 +636,18 @@ def test_exact_fast_loads_equal_the_general_path(gpu, oracle, opts, faint, fitof
     assert nomc.tobytes() == fast.tobytes()
     ref = oracle_fit(oracle, B, state=st, fitoffsets=fitoffsets)
     print(assert_exact_bitwise(fast, ref, label=f"exact fast faint={faint} offsets={fitoffsets}"))
+    # ComplexF32 storage (r6: the FAST form on 8-B elements): the general form's bits, which are
+    # the ComplexF64 entry point's on the widened data (tests/test_gpu_c32.py)
+    B32 = dict(B)
+    B32["d"], B32["fc"] = B["d"].astype(np.complex64), B["fc"].astype(np.complex64)
+    W = dict(B)
+    W["d"], W["fc"] = B32["d"].astype(np.complex128), B32["fc"].astype(np.complex128)
+    f32 = fit(gpu, B32, method="exact", state=st, fitoffsets=fitoffsets)
+    opts("exact_fast", 0)
+    g32 = fit(gpu, B32, method="exact", state=st, fitoffsets=fitoffsets)
+    opts("exact_fast", 1)
+    assert f32.tobytes() == g32.tobytes()
+    assert f32.tobytes() == fit(gpu, W, method="exact", state=st, fitoffsets=fitoffsets).tobytes()
 
 
 @pytest.mark.parametrize("xinit,b_range", [(None, (0.3, 2.5)), ((8.0, 0.3), (0.3, 2.5)),
