@@ -476,7 +476,27 @@ def c2_block(gpd, t, d, fc, args, log, reps=5):
     cases["demodulateall"] = {"host_call_ms": ms, "release_of_the_output_ms": rel,
                               "what": "output = copy(data) with the 32 demodulated columns "
                                       "written in place, records, likelihood (a fresh output "
-                                      "per call; its release by the caller timed apart)"}
+                                      "per call; its release by the caller timed apart); "
+                                      "pageable data: one part (option h2d_parts automatic)"}
+    # the same exposure in page-locked host memory (a caller that pins its buffers once): the
+    # library then cuts the call into 2 parts, part 1's H2D DMA'd under part 0's kernels and
+    # part 0's output back meanwhile (option h2d_parts automatic); and with h2d_parts = 1
+    pin = torch.empty((40, N), dtype=torch.complex128, pin_memory=True).numpy()
+    pin[:] = cols
+    pdata = pin.T  # N x 40, column-major, page-locked
+    ms, k, rel = med_kept(lambda: gpd.demodulateall(th, pdata))
+    cases["demodulateall_pinned_input"] = {"host_call_ms": ms, "release_of_the_output_ms": rel,
+                                           "h2d_parts": 2}
+    parts = gpd.get_option("h2d_parts")
+    gpd.set_option("h2d_parts", 1)
+    try:
+        ms, k, rel = med_kept(lambda: gpd.demodulateall(th, pdata))
+        cases["demodulateall_pinned_input_one_part"] = {"host_call_ms": ms,
+                                                        "release_of_the_output_ms": rel}
+    finally:
+        gpd.set_option("h2d_parts", parts)
+    _, par_p, _ = gpd.demodulateall(th, pdata)
+    same_pinned = [(p.a, p.b, p.ϕ) for p in par_p] == [(p.a, p.b, p.ϕ) for p in gpd.demodulateall(th, data)[1]]
     ms, k, rel = med_kept(lambda: gpd.demodulateall(th, data, fitoffsets=True))
     cases["demodulateall_fitoffsets"] = {
         "host_call_ms": ms, "release_of_the_output_ms": rel,
@@ -502,6 +522,7 @@ def c2_block(gpd, t, d, fc, args, log, reps=5):
             "host_bytes_out": int(dd.nbytes), "cases": cases,
             "kernels_ms_fit_only": {a: round(b, 3) for a, b in kern.items()},
             "records_equal_fit_only": same,
+            "records_equal_pinned_two_parts": same_pinned,
             "host_memory": "pageable numpy arrays (column-major, as a Julia Matrix)",
             "note": "PCIe-inclusive host-buffer calls; not the headline (which is HBM-resident)"}
 

@@ -74,6 +74,8 @@ enum OptId {
     O_HOST_PROF,     // 1: wall-clock split of the host-buffer calls on stderr (diagnostics)
     O_FIT_MCACHE,    // 1: harmonic fit reads the series' moments from LDS where they fit; 0: L2
     O_STAGE_PINNED,  // 1: demodulated columns staged through a pinned ring; 0: pageable ring (tests)
+    O_H2D_PARTS,     // 0: automatic (2 parts for pinned host data, else 1); n: host-buffer harmonic
+                     // calls cut into n parts, H2D / compute / D2H pipelined
     O_COUNT
 };
 struct OptDef {
@@ -86,10 +88,10 @@ constexpr OptDef kOpt[O_COUNT] = {
     {"exact_mcache", 1}, {"xspin_test", 0},    {"units", 0},         {"upw", 0},
     {"fit_lanes", 0},    {"fit_lps", 0},       {"fit_wpb", 0},       {"cohorts", 1},       {"harm_min_span", 256}, {"fs_cohort_mb", 4096},
     {"moments", 0},      {"fit_prof", 0},      {"sync_debug", 0},    {"host_prof", 0},
-    {"fit_mcache", 1},   {"stage_pinned", 1}};
+    {"fit_mcache", 1},   {"stage_pinned", 1},  {"h2d_parts", 0}};
 std::atomic<long long> g_opt[O_COUNT] = {{1}, {0}, {0},   {0},    {0}, {0}, {0}, {1}, {1}, {0}, {0},
                                           {0}, {0}, {0},   {0},    {1}, {256}, {4096}, {0}, {0}, {0},
-                                          {0}, {1}, {1}};
+                                          {0}, {1}, {1}, {0}};
 inline long long opt(OptId o) { return g_opt[o].load(std::memory_order_relaxed); }
 int opt_find(const char *name) {
     if (!name) return -1;
@@ -117,6 +119,7 @@ constexpr int kMaxTimers = 8 * kMaxCohorts + 16;
 // workgroups per CU (one round of those); below, the 256-thread workgroup's lower latency per
 // evaluation wins (r3: 32 series 0.98 vs 1.56 ms; 16 000 windows 41.6 vs 17.0 ms)
 constexpr long long kOneWaveMinSeriesPerCU = 2;
+constexpr int kMaxParts = 8;  // parts of a pipelined host-buffer call (option h2d_parts)
 
 struct DevCtx {
     int dev = -1;
@@ -151,6 +154,11 @@ struct DevCtx {
     char *hpin = nullptr;
     bool hpin_pinned = false, hpin_nopin = false;
     hipEvent_t hpin_ev[4] = {};  // each slot's chunk has arrived (host copy pipelined)
+    // H2D pipelining of host-buffer harmonic calls (option h2d_parts): part k's columns go up on
+    // cstream (event up[k]) while part k−1 computes on hstream (event fin[k−1]); the staged
+    // demodulated columns come back on ostream, which waits for fin[k]
+    hipStream_t cstream = nullptr, ostream = nullptr;
+    hipEvent_t up[kMaxParts] = {}, fin[kMaxParts] = {};
     // the last fit call's faint statistics in the workspace (gpd_last_faint_stats; tests)
     const double *last_fstat = nullptr;
     long long last_fstat_P = 0;
@@ -628,6 +636,8 @@ int gpd_release(int device) {
     std::lock_guard<std::mutex> lk(cx->mu);
     if (hipSetDevice(device) != hipSuccess) return GPD_E_HIP;
     if (cx->hstream) (void)hipStreamSynchronize(cx->hstream);
+    if (cx->cstream) (void)hipStreamSynchronize(cx->cstream);
+    if (cx->ostream) (void)hipStreamSynchronize(cx->ostream);
     if (cx->done) (void)hipEventSynchronize(cx->done);
     (void)hipFree(cx->ws);
     (void)hipFree(cx->harena);
@@ -967,7 +977,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                 k_fix_table<<<ftab_grid, 256, 0, stream>>>(pb, dlist, dhdr, ftab);
                 mark("faint_defer");
             }
-            if (faint) k_moments_fix<<<dim3((unsigned)n, FST_SLOTS), 256, 0, stream>>>(sp, dlist, dhdr, ftab, fix_c, fixs_c);
+            if (faint) k_moments_fix<<<(unsigned)n, 256, 0, stream>>>(sp, dlist, dhdr, ftab, fix_c, fixs_c);
             if (faint && is_c32 && tm)
                 k_moments_ws<0, false, c32, 2, true, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, smask, fsp_c, fcnt, dhdr);
             else if (faint && tm)
@@ -1069,7 +1079,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             if (faint) {  // the deferred samples of the state-split pass (usually none)
                 faint_defer();
                 k_fix_table<<<ftab_grid, 256, 0, stream>>>(pb, dlist, dhdr, ftab);
-                k_moments_fix<<<dim3((unsigned)P, FST_SLOTS), 256, 0, stream>>>(pb, dlist, dhdr, ftab, fixp, fixs);
+                k_moments_fix<<<(unsigned)P, 256, 0, stream>>>(pb, dlist, dhdr, ftab, fixp, fixs);
                 mark("faint_defer");
             }
             if (faint && is_c32 && tmix)  // faint series: the producer/consumer kernel, state-split
@@ -1527,6 +1537,29 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
         const int64_t nfc = (int64_t)cmax - cmin + 1;
         std::vector<int32_t> fcop_l(fc_of_pixel + p0, fc_of_pixel + p1);
         for (auto &c : fcop_l) c -= cmin;
+        // H2D pipelining (option h2d_parts, r6): a harmonic fit call in series mode is cut into
+        // K parts at multiples of 4 series.  Part k's diode columns — and the FC columns it is the
+        // first to reference — go up on the copy stream while part k−1 computes on s, and the
+        // staged demodulated columns of part k−1 come back on the output stream meanwhile (PCIe is
+        // full duplex).  The records do not depend on the cut (fixed sample units, whole-series
+        // fits: the shard tests), so K changes the time only.  Exact-evaluator calls stay whole
+        // (their fit spreads each series over up to 8 CUs; parts would serialise those fits).
+        // Automatic (0): 2 parts when the caller's data is pinned (page-locked: the copies are
+        // DMA'd asynchronously), 1 for pageable data — a pageable H2D is staged by the runtime
+        // and did not overlap the previous part's kernels (measured, r6: C2 3.3 → 4.0 ms at K = 2)
+        const bool harm_call = window == 0 && !bphi && !(flags & (GPD_METHOD_EXACT | GPD_FP32)) &&
+                               (!(flags & GPD_FIT_OFFSETS) || (flags & GPD_METHOD_HARMONIC));
+        long long kopt = opt(O_H2D_PARTS);
+        if (kopt <= 0) {
+            hipPointerAttribute_t pa;
+            const bool pinned = hipPointerGetAttributes(&pa, d) == hipSuccess && pa.type == hipMemoryTypeHost;
+            (void)hipGetLastError();  // unregistered host memory reports an error: not pinned
+            kopt = pinned ? 2 : 1;
+        }
+        int K = harm_call ? (int)std::min<long long>(kMaxParts, kopt) : 1;
+        K = (int)std::min<int64_t>(K, (P + 3) / 4);
+        std::vector<int64_t> q(K + 1);  // part k: the shard's series [q[k], q[k + 1])
+        for (int k = 0; k <= K; ++k) q[k] = std::min<int64_t>(P, (P * k / K + 3) / 4 * 4);
         DevCtx *cx = ctx_for(dev);
         std::lock_guard<std::mutex> hlk(cx->hmu);  // shards sharing a device run in turn
         size_t off = 0;
@@ -1539,13 +1572,22 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
                      o_fc = take((size_t)nfc * N * esz), o_fcop = take(P * sizeof(int32_t)),
                      o_par = take(nrec * sizeof(Param)), o_st = take(state ? N : 0),
                      o_bphi = take(bphi ? 2 * P * sizeof(double) : 0),
-                     o_out = take(out_demod ? (size_t)P * N * sizeof(c64) : 0);
+                     o_out = take(out_demod ? (size_t)P * N * sizeof(c64) : 0),
+                     o_fst = take(state && K > 1 ? (size_t)P * 16 * sizeof(double) : 0);
         if (!cx->hstream && !chk(hipStreamCreateWithFlags(&cx->hstream, hipStreamNonBlocking),
                                  "hipStreamCreate"))
             return fail(GPD_E_HIP);
         hipStream_t s = cx->hstream;
         if (cx->harena_cap < off) {
             if (cx->harena) {
+                {  // gpd_last_faint_stats must not read the arena being freed
+                    std::lock_guard<std::mutex> lk(cx->mu);
+                    if (cx->last_fstat && (const char *)cx->last_fstat >= cx->harena &&
+                        (const char *)cx->last_fstat < cx->harena + cx->harena_cap) {
+                        cx->last_fstat = nullptr;
+                        cx->last_fstat_P = 0;
+                    }
+                }
                 (void)hipStreamSynchronize(s);
                 (void)hipFree(cx->harena);
                 cx->harena = nullptr;
@@ -1567,98 +1609,189 @@ static int host_batch(int64_t n_samples, int64_t n_pixels, const double *t, cons
         int8_t *dst = state ? (int8_t *)(A + o_st) : nullptr;
         double *dbphi = bphi ? (double *)(A + o_bphi) : nullptr;
         c64 *dout = out_demod ? (c64 *)(A + o_out) : nullptr;
-        bool ok = chk(hipMemcpyAsync(dt, t + s0, N * sizeof(double), hipMemcpyHostToDevice, s), "H2D t") &&
-             chk(hipMemcpy2DAsync(dd, N * esz, d + (p0 * ldd + s0) * esz, ldd * esz, N * esz, P,
-                                  hipMemcpyHostToDevice, s), "H2D d") &&
-             chk(hipMemcpy2DAsync(dfc, N * esz, fc + ((int64_t)cmin * ldfc + s0) * esz,
-                                  ldfc * esz, N * esz, nfc, hipMemcpyHostToDevice, s), "H2D fc") &&
+        bool ok = true;
+        if (K > 1) {
+            ok = (cx->cstream || chk(hipStreamCreateWithFlags(&cx->cstream, hipStreamNonBlocking), "hipStreamCreate")) &&
+                 (cx->ostream || chk(hipStreamCreateWithFlags(&cx->ostream, hipStreamNonBlocking), "hipStreamCreate"));
+            for (int k = 0; ok && k < kMaxParts; ++k)
+                ok = (cx->up[k] || chk(hipEventCreateWithFlags(&cx->up[k], hipEventDisableTiming), "hipEventCreate")) &&
+                     (cx->fin[k] || chk(hipEventCreateWithFlags(&cx->fin[k], hipEventDisableTiming), "hipEventCreate"));
+            if (!ok) return fail(GPD_E_HIP);
+        }
+        hipStream_t cs = K > 1 ? cx->cstream : s, os = K > 1 ? cx->ostream : s;
+        ok = chk(hipMemcpyAsync(dt, t + s0, N * sizeof(double), hipMemcpyHostToDevice, s), "H2D t") &&
              chk(hipMemcpyAsync(dfcop, fcop_l.data(), P * sizeof(int32_t), hipMemcpyHostToDevice, s),
                  "H2D fcop") &&
              (!state || chk(hipMemcpyAsync(dst, state + s0, N, hipMemcpyHostToDevice, s), "H2D state")) &&
              (!bphi || chk(hipMemcpyAsync(dbphi, bphi + 2 * p0, 2 * P * sizeof(double),
                                           hipMemcpyHostToDevice, s), "H2D bphi"));
+        std::vector<char> fc_up(nfc, 0);  // FC column already sent
+        auto h2d_part = [&](int k) {
+            const int64_t a = q[k], b = q[k + 1];
+            bool r = chk(hipMemcpy2DAsync(dd + (size_t)a * N * esz, N * esz, d + ((p0 + a) * ldd + s0) * esz,
+                                          ldd * esz, N * esz, b - a, hipMemcpyHostToDevice, cs), "H2D d");
+            std::vector<char> need(nfc, 0);
+            for (int64_t i = a; i < b; ++i) need[fcop_l[i]] = !fc_up[fcop_l[i]];
+            for (int64_t c = 0; r && c < nfc;) {  // runs of consecutive columns
+                if (!need[c]) {
+                    ++c;
+                    continue;
+                }
+                int64_t e = c;
+                while (e < nfc && need[e]) fc_up[e++] = 1;
+                r = chk(hipMemcpy2DAsync(dfc + (size_t)c * N * esz, N * esz, fc + ((cmin + c) * ldfc + s0) * esz,
+                                         ldfc * esz, N * esz, e - c, hipMemcpyHostToDevice, cs), "H2D fc");
+                c = e;
+            }
+            return r && (K == 1 || chk(hipEventRecord(cx->up[k], cs), "hipEventRecord"));
+        };
+        const bool hprof = opt(O_HOST_PROF) != 0;
+        auto hnow = [] { return std::chrono::steady_clock::now(); };
+        // the staged output (out_kind 1/2): the P×N demodulated columns (contiguous on the device)
+        // come back in chunks through the device's staging ring — chunk c into slot
+        // c mod kStageSlots, an event after each; the host pool copies chunk c into the caller's
+        // columns (ldo; rounded to ComplexF32 for kind 2) while chunks c + 1 … are in flight, then
+        // the slot takes chunk c + kStageSlots.  Each part's columns in ≥ ⌈4 / K⌉ chunks (C2: 4 ×
+        // 12.8 MB), at most one slot each; a chunk is issued on the output stream after its part's
+        // compute, as soon as its slot is free.
+        const bool staged = out_demod && out_kind != 0;
+        struct Chunk {
+            int64_t e0, e1;
+            int part;
+        };
+        std::vector<Chunk> chunks;
+        if (staged) {
+            const int64_t per_slot = (int64_t)(kStageSlotBytes / sizeof(c64));
+            for (int k = 0; k < K; ++k) {
+                const int64_t f0 = q[k] * N, f1 = q[k + 1] * N, tot = f1 - f0;
+                if (tot <= 0) continue;
+                const int64_t n = std::max<int64_t>(std::min<int64_t>((kStageSlots + K - 1) / K, tot),
+                                                    (tot + per_slot - 1) / per_slot);
+                for (int64_t c = 0; c < n; ++c) chunks.push_back({f0 + tot * c / n, f0 + tot * (c + 1) / n, k});
+            }
+            ok = ok && ensure_stage(cx);
+            if (!ok) set_err(errbuf_l, errlen_l, "output staging ring: out of host memory");
+            for (int c = 0; ok && c < kStageSlots; ++c)
+                if (!cx->hpin_ev[c])
+                    ok = chk(hipEventCreateWithFlags(&cx->hpin_ev[c], hipEventDisableTiming), "hipEventCreate");
+        }
+        const int64_t nch = (int64_t)chunks.size();
+        int64_t issued = 0;
+        auto issue = [&](int64_t c) {
+            const Chunk &h = chunks[c];
+            const int sl = (int)(c % kStageSlots);
+            return (K == 1 || chk(hipStreamWaitEvent(os, cx->fin[h.part], 0), "hipStreamWaitEvent")) &&
+                   chk(hipMemcpyAsync(cx->hpin + (size_t)sl * kStageSlotBytes, dout + h.e0,
+                                      (size_t)(h.e1 - h.e0) * sizeof(c64), hipMemcpyDeviceToHost, os),
+                       "D2H out (staged)") &&
+                   chk(hipEventRecord(cx->hpin_ev[sl], os), "hipEventRecord");
+        };
+        // the first touch of the caller's destination columns (a fresh output's page faults — the
+        // kernel zeroing each page — are most of an unpipelined host copy), on the host pool from
+        // a helper thread while this thread issues the (pageable, host-blocking) H2D copies; one
+        // store per page inside the columns only (never the ldo gaps), joined before the chunk
+        // copies overwrite those pages
+        const size_t des = out_kind == 2 ? sizeof(gpd_c32) : sizeof(gpd_c64);
+        char *dst0 = staged ? (char *)out_demod + ((size_t)p0 * ldo + s0) * des : nullptr;
+        struct Joiner {
+            std::thread t;
+            ~Joiner() {
+                if (t.joinable()) t.join();
+            }
+        } toucher;
+        std::chrono::steady_clock::time_point ht0, ht1;
+        if (ok && staged)
+            toucher.t = std::thread([&] {
+                ht0 = hnow();
+                pool_touch_cols(dst0, des, ldo, N, P);
+                ht1 = hnow();
+            });
+        const auto h0 = hnow();
+        std::vector<double> hpart;  // host_prof: ms at each part's H2D issued, compute launched
+        auto ms_since = [&](std::chrono::steady_clock::time_point a) {
+            return std::chrono::duration<double, std::milli>(hnow() - a).count();
+        };
+        for (int k = 0; ok && k < K; ++k) {
+            const int64_t a = q[k], b = q[k + 1];
+            if (b <= a) continue;
+            ok = h2d_part(k) && (K == 1 || chk(hipStreamWaitEvent(s, cx->up[k], 0), "hipStreamWaitEvent"));
+            if (hprof) hpart.push_back(ms_since(h0));
+            if (!ok) break;
+            const int r = pipeline_dev(N, K == 1 ? P : b - a, dt, dd + (size_t)a * N * esz, N, dfc, nfc, N,
+                                       dfcop + a, dst, omega, xinit, flags, maxfun,
+                                       (gpd_param *)(dpar + a), dout ? (gpd_c64 *)(dout + a * N) : nullptr,
+                                       N, dbphi, dev, s, errbuf_l, errlen_l, window, is_c32);
+            if (r != GPD_OK) {
+                cleanup();
+                return fail(r);
+            }
+            if (K > 1 && state) {  // the part's faint statistics, kept for gpd_last_faint_stats
+                std::lock_guard<std::mutex> lk(cx->mu);
+                ok = cx->last_fstat &&
+                     chk(hipMemcpyAsync(A + o_fst + (size_t)a * 16 * sizeof(double), cx->last_fstat,
+                                        (size_t)(b - a) * 16 * sizeof(double), hipMemcpyDeviceToDevice, s),
+                         "D2D faint statistics");
+                if (ok && b == P) {
+                    cx->last_fstat = (const double *)(A + o_fst);
+                    cx->last_fstat_P = P;
+                }
+            }
+            if (K > 1) ok = ok && chk(hipEventRecord(cx->fin[k], s), "hipEventRecord");
+            while (ok && issued < std::min<int64_t>(nch, kStageSlots) && chunks[issued].part <= k)
+                ok = issue(issued++);
+            if (hprof) hpart.push_back(ms_since(h0));
+        }
         if (!ok) {
             cleanup();
             return fail(GPD_E_HIP);
         }
-        const bool hprof = opt(O_HOST_PROF) != 0;
-        auto hnow = [] { return std::chrono::steady_clock::now(); };
-        const auto h0 = hnow();
-        if (hprof) (void)hipStreamSynchronize(s);
+        // the records (and the unstaged output) into the caller's pageable memory: a host-blocking
+        // copy that waits for the last part's fit — after the staged chunks' host copies, which
+        // overlap the device's work
+        auto d2h_tail = [&] {
+            return chk(hipMemcpyAsync(out_params + o0, dpar, nrec * sizeof(Param), hipMemcpyDeviceToHost, s),
+                       "D2H params") &&
+                   (!out_demod || out_kind != 0 ||
+                    chk(hipMemcpy2DAsync(out_demod + p0 * ldo + s0, ldo * sizeof(gpd_c64), dout,
+                                         N * sizeof(c64), N * sizeof(c64), P,
+                                         hipMemcpyDeviceToHost, s), "D2H out"));
+        };
+        if (!staged) ok = d2h_tail();
         const auto h1 = hnow();
-        int r = pipeline_dev(N, P, dt, dd, N, dfc, nfc, N, dfcop, dst, omega, xinit, flags, maxfun,
-                             (gpd_param *)dpar, (gpd_c64 *)dout, N, dbphi, dev, s, errbuf_l,
-                             errlen_l, window, is_c32);
-        if (r != GPD_OK) {
-            cleanup();
-            return fail(r);
-        }
-        ok = chk(hipMemcpyAsync(out_params + o0, dpar, nrec * sizeof(Param), hipMemcpyDeviceToHost, s),
-                 "D2H params") &&
-             (!out_demod || out_kind != 0 ||
-              chk(hipMemcpy2DAsync(out_demod + p0 * ldo + s0, ldo * sizeof(gpd_c64), dout,
-                                   N * sizeof(c64), N * sizeof(c64), P,
-                                   hipMemcpyDeviceToHost, s), "D2H out"));
-        if (hprof) (void)hipStreamSynchronize(s);
+        if (hprof && !staged) (void)hipStreamSynchronize(s);
         const auto h2 = hnow();
         auto h3 = h2, h4 = h2;
-        if (ok && out_demod && out_kind != 0) {
-            // staged: the P×N demodulated columns (contiguous on the device) come back in chunks
-            // through the device's staging ring — chunk c into slot c mod kStageSlots, an event
-            // after each; the host pool copies chunk c into the caller's columns (ldo; rounded to
-            // ComplexF32 for kind 2) while chunks c + 1 … are in flight, then the slot takes
-            // chunk c + kStageSlots.  At least 4 chunks (C2: 4 × 12.8 MB), at most one slot each.
-            const int64_t total = P * N;  // c64 elements
-            const int64_t per_slot = (int64_t)(kStageSlotBytes / sizeof(c64));
-            const int64_t nch = std::max<int64_t>(std::min<int64_t>(4, total),
-                                                  (total + per_slot - 1) / per_slot);
-            ok = ensure_stage(cx);
-            if (!ok) set_err(errbuf_l, errlen_l, "output staging ring: out of host memory");
-            for (int c = 0; ok && c < kStageSlots; ++c)
-                if (!cx->hpin_ev[c])
-                    ok = chk(hipEventCreateWithFlags(&cx->hpin_ev[c], hipEventDisableTiming),
-                             "hipEventCreate");
-            auto chunk = [&](int64_t c, int64_t &e0, int64_t &e1) {
-                e0 = total * c / nch;
-                e1 = total * (c + 1) / nch;
-            };
-            auto issue = [&](int64_t c) {
-                int64_t e0, e1;
-                chunk(c, e0, e1);
-                const int sl = (int)(c % kStageSlots);
-                return chk(hipMemcpyAsync(cx->hpin + (size_t)sl * kStageSlotBytes, dout + e0,
-                                          (size_t)(e1 - e0) * sizeof(c64), hipMemcpyDeviceToHost,
-                                          s), "D2H out (staged)") &&
-                       chk(hipEventRecord(cx->hpin_ev[sl], s), "hipEventRecord");
-            };
-            for (int64_t c = 0; ok && c < std::min<int64_t>(nch, kStageSlots); ++c) ok = issue(c);
-            const size_t des = out_kind == 2 ? sizeof(gpd_c32) : sizeof(gpd_c64);
-            char *dst0 = (char *)out_demod + ((size_t)p0 * ldo + s0) * des;
-            // while the device still computes and copies: the first touch of the caller's
-            // destination columns (a fresh output's page faults — the kernel zeroing each page —
-            // are most of an unpipelined host copy); one store per page, inside the columns only
-            // (never the ldo gaps), each later overwritten by the copy below
-            if (ok) pool_touch_cols(dst0, des, ldo, N, P);
+        if (ok && staged) {
+            toucher.t.join();
             h3 = hnow();
             for (int64_t c = 0; ok && c < nch; ++c) {
                 const int sl = (int)(c % kStageSlots);
-                int64_t e0, e1;
-                chunk(c, e0, e1);
                 ok = chk(hipEventSynchronize(cx->hpin_ev[sl]), "hipEventSynchronize");
                 if (ok)
                     pool_copy_range(dst0, des, ldo, cx->hpin + (size_t)sl * kStageSlotBytes, N,
-                                    e0, e1);
+                                    chunks[c].e0, chunks[c].e1);
                 if (ok && c + kStageSlots < nch) ok = issue(c + kStageSlots);
             }
+            ok = ok && d2h_tail();
             h4 = hnow();
         }
         if (hprof) {
             auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-            fprintf(stderr, "host_prof dev %d: H2D issue %.3f ms, H2D wait %.3f ms, pipeline %.3f ms, "
-                    "output touch %.3f ms, D2H + host copy %.3f ms (pool %d threads)\n", dev, ms(hs, h0),
-                    ms(h0, h1), ms(h1, h2), ms(h2, h3), ms(h3, h4), HostPool::get().size());
+            fprintf(stderr, "host_prof dev %d: setup %.3f ms, H2D + launches issued %.3f ms (%d parts), "
+                    "device wait %.3f ms, output touch %.3f ms, D2H + host copy %.3f ms (pool %d "
+                    "threads)\n", dev, ms(hs, h0), ms(h0, h1), K, ms(h1, h2), ms(h2, h3), ms(h3, h4),
+                    HostPool::get().size());
+            for (size_t i = 0; i + 1 < hpart.size(); i += 2)
+                fprintf(stderr, "host_prof   part %zu: H2D issued at %.3f ms, compute launched at %.3f ms\n",
+                        i / 2, hpart[i], hpart[i + 1]);
+            if (staged)
+                fprintf(stderr, "host_prof   output touch (helper thread) %.3f .. %.3f ms\n", ms(h0, ht0), ms(h0, ht1));
         }
         ok = ok && chk(hipStreamSynchronize(s), "hipStreamSynchronize");
+        if (K > 1) {  // nothing of this call may still write the arena or the ring (error paths)
+            (void)hipStreamSynchronize(cs);
+            (void)hipStreamSynchronize(os);
+        }
         cleanup();
         if (!ok) return fail(GPD_E_HIP);
     };

@@ -105,8 +105,8 @@ int gpd_release(int device);
  * call.  Names and defaults (INTEGRATION.md lists them): mix 1, faint_stats 0, faint_side 0,
  * fake_gpus 0, exact_g 0, exact_waves 0, exact_wgt 0, exact_fast 1, exact_mcache 1,
  * xspin_test 0, units 0, upw 0, fit_lanes 0, fit_lps 0, fit_wpb 0, cohorts 1, harm_min_span 256, fs_cohort_mb 4096,
- * moments 0, fit_prof 0, sync_debug 0, host_prof 0, fit_mcache 1, stage_pinned 1 (0 = automatic
- * where a count is meant).
+ * moments 0, fit_prof 0, sync_debug 0, host_prof 0, fit_mcache 1, stage_pinned 1, h2d_parts 0
+ * (0 = automatic where a count is meant).
  * gpd_set_option / gpd_get_option: GPD_OK, or GPD_E_ARG for an unknown name.
  * gpd_option_name(i): the i-th option's name, NULL past the last. */
 int gpd_set_option(const char *name, int64_t value);

@@ -189,6 +189,7 @@ def test_cohort_pipeline_records_bitwise(gpu, opts, faint, storage):
         d, fc = d.astype(np.complex64), fc.astype(np.complex64)
     args = (B["t"], d, fc, B["fc_of_pixel"])
     recs = {}
+    opts("h2d_parts", 1)  # one device pipeline over the whole batch (parts would be cohorts' size)
     for c in ("1", "2", "3", "5"):
         opts("cohorts", int(c))
         recs[c] = gpu.fit_batch(*args, state=st, method="harmonic")
@@ -312,3 +313,52 @@ def test_faint_state_pointer_alignment(gpu):
     _same(b, a)
     assert not np.all(a["status"] & gpu.GPD_ST_NAN)
 
+
+
+@pytest.mark.parametrize("faint", [False, True])
+def test_h2d_parts_bit_identical(gpu, opts, faint):
+    """Host-buffer harmonic calls cut into parts (option h2d_parts, r6: part k's columns cross
+    PCIe on a copy stream while part k−1 computes, the staged output returns on a third stream)
+    give the one-part call's records, output and faint statistics bit for bit — for a ragged
+    batch (P = 70: parts at multiples of 4, a short last part), for parts inside device shards,
+    and for the exact method (which never splits)."""
+    N, P = 5003, 70
+    B = synth.make_batch(N, P, seed=66)
+    st = faint_states(N, seed=5) if faint else None
+    args = (B["t"], B["d"], B["fc"], B["fc_of_pixel"])
+    opts("h2d_parts", 1)
+    ref, ref_out = gpu.fit_batch(*args, state=st, want_output=True)
+    ref_fs = gpu.last_faint_stats(P) if faint else None
+    for parts in (2, 3, 4, 8):
+        opts("h2d_parts", parts)
+        got, out = gpu.fit_batch(*args, state=st, want_output=True)
+        _same(got, ref)
+        np.testing.assert_array_equal(out, ref_out)
+        if faint:
+            for a, b in zip(gpu.last_faint_stats(P), ref_fs):
+                np.testing.assert_array_equal(a, b)
+    opts("fake_gpus", 1)
+    opts("h2d_parts", 3)
+    got, out = gpu.fit_batch(*args, state=st, want_output=True, n_gpus=2)
+    _same(got, ref)
+    np.testing.assert_array_equal(out, ref_out)
+
+
+@pytest.mark.parametrize("storage", ["c64", "c32"])
+def test_demodulateall_h2d_parts_bit_identical(gpu, opts, storage):
+    """gpd_demodulateall with its H2D, compute and staged D2H pipelined over 1, 2, 4 and 8 parts:
+    every output column (FC included), record and likelihood equal across part counts — also for
+    an exposure whose demodulated columns exceed the staging ring (200 000 samples: each part's
+    chunks cycle through the 4 slots)."""
+    for N, seed in ((20_011, 67), (200_000, 68)):
+        t, data = _exposure(gpu, N, seed)
+        if storage == "c32":
+            data = np.asfortranarray(data.astype(np.complex64))
+        opts("h2d_parts", 1)
+        out1, par1, lk1 = gpu.demodulateall(t, data)
+        for parts in (2, 4, 8):
+            opts("h2d_parts", parts)
+            out, par, lk = gpu.demodulateall(t, data)
+            np.testing.assert_array_equal(out, out1)
+            np.testing.assert_array_equal(lk, lk1)
+            assert [(p.a, p.b, p.ϕ) for p in par] == [(p.a, p.b, p.ϕ) for p in par1]

@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for _p in (ROOT, os.path.join(ROOT, "tests")):
     sys.path.insert(0, _p)
 import numpy as np  # noqa: E402
-import torch  # noqa: F401,E402  (HIP runtime order, as in the tests)
+import torch  # noqa: E402  (HIP runtime order, as in the tests; pinned host memory)
 
 import gpdemod_loader  # noqa: E402
 import synth  # noqa: E402
@@ -36,6 +36,7 @@ def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 7
     gpd = gpdemod_loader.load()
     L = gpd.load()
+    gpd.options_from_env()  # GPD_OPTS="name=value,..." (A/B runs, e.g. h2d_parts=1)
     N = 100_000
     B = synth.make_batch(N, 32, seed=42)
     data = np.empty((N, 40), dtype=np.complex128, order="F")
@@ -56,6 +57,12 @@ def main():
     n_kept = len(kept)
     kept.clear()
     out["release_of_one_output_ms"] = round(1e3 * (time.perf_counter() - t0) / n_kept, 3)
+    # the exposure in page-locked memory (a caller that pins its buffers): two parts by default
+    pin = torch.empty((40, N), dtype=torch.complex128, pin_memory=True).numpy()
+    pin[:] = cols
+    pdata = pin.T
+    out["demodulateall_pinned_kept_ms"] = med(lambda: kept.append(gpd.demodulateall(t, pdata)), reps)
+    kept.clear()
     reuse = np.empty((40, N), dtype=np.complex128)
     par = np.zeros(32, dtype=gpd.PARAM_DTYPE)
     import ctypes
@@ -74,6 +81,8 @@ def main():
     gpd.demodulateall(t, data)
     print("--- host_prof: reused output", file=sys.stderr, flush=True)
     call_reuse()
+    print("--- host_prof: pinned input, fresh output", file=sys.stderr, flush=True)
+    gpd.demodulateall(t, pdata)
     gpd.set_option("host_prof", 0)
     print(json.dumps(out), flush=True)
 

@@ -45,7 +45,9 @@ def main():
     st = c5_states(gpd, t.cpu().numpy())
     power = torch.tensor([POWER[int(s)] for s in st], dtype=torch.float64, device=dev)
     d.mul_(power[None, :, None])
-    d.add_(torch.randn(d.shape, dtype=torch.float64, device=dev), alpha=0.02 / np.sqrt(2.0))
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(11)  # seeded noise: A/B builds compare record hashes
+    d.add_(torch.randn(d.shape, dtype=torch.float64, device=dev, generator=gen), alpha=0.02 / np.sqrt(2.0))
     if args.c32:
         d, fc = d.float(), fc.float()
     std = torch.from_numpy(st).to(dev)
@@ -68,7 +70,13 @@ def main():
         wall.append(round((time.perf_counter() - t0) * 1e3, 3))
         out.append({k: round(v, 3) for k, v in gpd.timings(0).items()})
     rec = params.cpu().numpy().reshape(-1).view(gpd.PARAM_DTYPE)
-    print(json.dumps({"series": P, "samples": N, "c32": args.c32, "method": args.method,
+    import hashlib
+    fs = np.empty((P, 16))
+    gpd._lib.check(L.gpd_last_faint_stats(0, gpd._lib.ptr(fs), P))
+    # hashes of the records and of the faint statistics: A/B builds that must give the same bits
+    sha = {"records_sha": hashlib.sha256(rec.tobytes()).hexdigest()[:16],
+           "faint_stats_sha": hashlib.sha256(fs.tobytes()).hexdigest()[:16]}
+    print(json.dumps({"series": P, "samples": N, "c32": args.c32, "method": args.method, **sha,
                       "kernels_ms": out[-1], "wall_ms": wall,
                       "faint_stats_ms": [o.get("faint_stats") for o in out],
                       "mean_nfev": round(float(rec["nfev"].mean()), 3)}))
