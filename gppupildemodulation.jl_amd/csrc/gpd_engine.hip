@@ -977,7 +977,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
                 k_fix_table<<<ftab_grid, 256, 0, stream>>>(pb, dlist, dhdr, ftab);
                 mark("faint_defer");
             }
-            if (faint) k_moments_fix<<<(unsigned)n, 256, 0, stream>>>(sp, dlist, dhdr, ftab, fix_c, fixs_c);
+            if (faint) k_moments_fix<<<dim3((unsigned)n, FST_SLOTS), 256, 0, stream>>>(sp, dlist, dhdr, ftab, fix_c, fixs_c);
             if (faint && is_c32 && tm)
                 k_moments_ws<0, false, c32, 2, true, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, smask, fsp_c, fcnt, dhdr);
             else if (faint && tm)
@@ -1079,7 +1079,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             if (faint) {  // the deferred samples of the state-split pass (usually none)
                 faint_defer();
                 k_fix_table<<<ftab_grid, 256, 0, stream>>>(pb, dlist, dhdr, ftab);
-                k_moments_fix<<<(unsigned)P, 256, 0, stream>>>(pb, dlist, dhdr, ftab, fixp, fixs);
+                k_moments_fix<<<dim3((unsigned)P, FST_SLOTS), 256, 0, stream>>>(pb, dlist, dhdr, ftab, fixp, fixs);
                 mark("faint_defer");
             }
             if (faint && is_c32 && tmix)  // faint series: the producer/consumer kernel, state-split

@@ -2004,12 +2004,10 @@ __global__ __launch_bounds__(256) void k_fix_table(Problem pb, const int *__rest
 // k_moments_fix: the unweighted moments q = p̄ d of the samples k_faint_defer lists, per state:
 // fixp[(q·NMOM + row)·P + k], the rows of k_moments_ws (Σq, Σ|q|², then A, B, C, D per
 // harmonic; every state of dhdr[1] written, nothing when the list is empty).  One workgroup
-// per series, every state at once (r6: was one per (series, state), grid P × FST_SLOTS, each
-// reloading every listed sample to keep its state's; C5 0.114 ms); thread = (harmonic group hg
-// of 3 harmonics, sample lane sl of 32); lane sl takes sample sl of each listed tile in list order
-// (cos/sin n x from k_fix_table; entries in batches of 4) into its state's accumulators — each
-// state's sums see the same samples in the same order as before, so the same bits — and the
-// lanes are reduced by a fixed xor tree per state.
+// per (series, state) (grid P × FST_SLOTS; with an empty list or a state without deferred
+// samples they return at once); thread = (harmonic group hg of 3 harmonics, sample lane sl of 32); lane sl takes
+// sample sl of each listed tile in list order (cos/sin n x from k_fix_table; entries in batches
+// of 4), the lanes are reduced by a fixed xor tree.
 __global__ __launch_bounds__(256) void k_moments_fix(Problem pb, const int *__restrict__ dlist,
                                                      const int *__restrict__ dhdr,
                                                      const double *__restrict__ ftab,
@@ -2022,106 +2020,93 @@ __global__ __launch_bounds__(256) void k_moments_fix(Problem pb, const int *__re
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int hg = wave * 2 + (lane >> 5), sl = lane & 31;
     const unsigned smk = (unsigned)dhdr[1];
-    const long long k = blockIdx.x;  // one workgroup per series
-    const long long doff = k * pb.ldd, foff = (long long)pb.fcop[k] * pb.ldfc;
-    double acc[FST_SLOTS][12], f0r[FST_SLOTS], f0i[FST_SLOTS], w2[FST_SLOTS];
-    double sn[FST_SLOTS], s1[FST_SLOTS], s2[FST_SLOTS], K[FST_SLOTS];  // fixs: the fused statistics' sums
-#pragma unroll
-    for (int q = 0; q < FST_SLOTS; ++q) {
-#pragma unroll
-        for (int c = 0; c < 12; ++c) acc[q][c] = 0.0;
-        f0r[q] = f0i[q] = w2[q] = sn[q] = s1[q] = s2[q] = K[q] = 0.0;
-        if (fixs && ((smk >> q) & 1u)) {
+    const long long k = blockIdx.x;  // one workgroup per (series, state)
+    const int q = blockIdx.y;
+    if (!((smk >> q) & 1u)) return;
+    {
+        const long long doff = k * pb.ldd, foff = (long long)pb.fcop[k] * pb.ldfc;
+        double acc[12], f0r = 0.0, f0i = 0.0, w2 = 0.0;
+        double sn = 0.0, s1 = 0.0, s2 = 0.0, K = 0.0;  // fixs: the fused statistics' sums
+        if (fixs) {
             const c64 z = d_at(pb, doff + dhdr[2 + q]);
-            K[q] = jl_hypot(z.re, z.im);
-        }
-    }
-    // entries in batches of 4 with every load issued up front (a list walk one entry at a
-    // time is a chain of dependent loads per entry); the same order of the sums
-    constexpr int EB = 4;
-    for (int e0 = 0; e0 < cnt; e0 += EB) {
-        long long ii[EB];
-        bool ok[EB];
-#pragma unroll
-        for (int u = 0; u < EB; ++u) {
-            const int e = e0 + u;
-            const unsigned dm = e < cnt ? (unsigned)dlist[2 * e + 1] : 0u;
-            ok[u] = (dm >> sl) & 1u;
-            ii[u] = ok[u] ? (long long)dlist[2 * e] * MM_TS + sl : 0;
-        }
-        c64 fv[EB], dvv[EB];
-        int sv[EB];
-#pragma unroll
-        for (int u = 0; u < EB; ++u) {
-            sv[u] = (int)gld(pb.state + ii[u]);  // a listed sample's state: valid, in smk
-            fv[u] = fc_at(pb, foff + ii[u]);
-            dvv[u] = d_at(pb, doff + ii[u]);
+            K = jl_hypot(z.re, z.im);
         }
 #pragma unroll
-        for (int u = 0; u < EB; ++u) {
-            if (!ok[u]) continue;
-            const c64 ph = unit_phasor(fv[u]);
-            const c64 dv = dvv[u];
-            const double qr = fma(ph.re, dv.re, ph.im * dv.im);
-            const double qi = fma(ph.re, dv.im, -(ph.im * dv.re));
-            const double *row = ftab + ((long long)(e0 + u) * MM_TS + sl) * (2 * KH) + 6 * hg;
-            double cs[6];
+        for (int c = 0; c < 12; ++c) acc[c] = 0.0;
+        // entries in batches of 4 with every load issued up front (a list walk one entry at a
+        // time is a chain of dependent loads per entry); the same order of the sums
+        constexpr int EB = 4;
+        for (int e0 = 0; e0 < cnt; e0 += EB) {
+            long long ii[EB];
+            bool ok[EB];
 #pragma unroll
-            for (int h = 0; h < 6; ++h) cs[h] = row[h];
-            const double qa = fs_abs(qr, qi);
+            for (int u = 0; u < EB; ++u) {
+                const int e = e0 + u;
+                const unsigned dm = e < cnt ? (unsigned)dlist[2 * e + 1] : 0u;
+                ok[u] = (dm >> sl) & 1u;
+                ii[u] = ok[u] ? (long long)dlist[2 * e] * MM_TS + sl : 0;
+            }
+            c64 fv[EB], dvv[EB];
 #pragma unroll
-            for (int q = 0; q < FST_SLOTS; ++q) {
-                if (sv[u] != q) continue;
+            for (int u = 0; u < EB; ++u) {
+                ok[u] = ok[u] && gld(pb.state + ii[u]) == q;
+                fv[u] = fc_at(pb, foff + ii[u]);
+                dvv[u] = d_at(pb, doff + ii[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < EB; ++u) {
+                if (!ok[u]) continue;
+                const c64 ph = unit_phasor(fv[u]);
+                const c64 dv = dvv[u];
+                const double qr = fma(ph.re, dv.re, ph.im * dv.im);
+                const double qi = fma(ph.re, dv.im, -(ph.im * dv.re));
+                const double *row = ftab + ((long long)(e0 + u) * MM_TS + sl) * (2 * KH) + 6 * hg;
 #pragma unroll
                 for (int h = 0; h < 3; ++h) {
-                    const double cn = cs[2 * h], sn_ = cs[2 * h + 1];
-                    acc[q][4 * h + 0] = fma(qr, cn, acc[q][4 * h + 0]);
-                    acc[q][4 * h + 1] = fma(qi, sn_, acc[q][4 * h + 1]);
-                    acc[q][4 * h + 2] = fma(qi, cn, acc[q][4 * h + 2]);
-                    acc[q][4 * h + 3] = fma(qr, sn_, acc[q][4 * h + 3]);
+                    const double cn = row[2 * h], sn = row[2 * h + 1];
+                    acc[4 * h + 0] = fma(qr, cn, acc[4 * h + 0]);
+                    acc[4 * h + 1] = fma(qi, sn, acc[4 * h + 1]);
+                    acc[4 * h + 2] = fma(qi, cn, acc[4 * h + 2]);
+                    acc[4 * h + 3] = fma(qr, sn, acc[4 * h + 3]);
                 }
-                f0r[q] += qr;
-                f0i[q] += qi;
-                w2[q] = fma(qr, qr, fma(qi, qi, w2[q]));
-                const double y = qa - K[q];
-                sn[q] += 1.0;
-                s1[q] += y;
-                s2[q] = fma(y, y, s2[q]);
+                f0r += qr;
+                f0i += qi;
+                w2 = fma(qr, qr, fma(qi, qi, w2));
+                const double y = fs_abs(qr, qi) - K;
+                sn += 1.0;
+                s1 += y;
+                s2 = fma(y, y, s2);
             }
         }
-    }
-#pragma unroll
-    for (int q = 0; q < FST_SLOTS; ++q) {
-        if (!((smk >> q) & 1u)) continue;
 #pragma unroll
         for (int off = 1; off < 32; off <<= 1) {
 #pragma unroll
-            for (int c = 0; c < 12; ++c) acc[q][c] += __shfl_xor(acc[q][c], off, 64);
-            f0r[q] += __shfl_xor(f0r[q], off, 64);
-            f0i[q] += __shfl_xor(f0i[q], off, 64);
-            w2[q] += __shfl_xor(w2[q], off, 64);
+            for (int c = 0; c < 12; ++c) acc[c] += __shfl_xor(acc[c], off, 64);
+            f0r += __shfl_xor(f0r, off, 64);
+            f0i += __shfl_xor(f0i, off, 64);
+            w2 += __shfl_xor(w2, off, 64);
             if (fixs && hg == 0) {
-                sn[q] += __shfl_xor(sn[q], off, 64);
-                s1[q] += __shfl_xor(s1[q], off, 64);
-                s2[q] += __shfl_xor(s2[q], off, 64);
+                sn += __shfl_xor(sn, off, 64);
+                s1 += __shfl_xor(s1, off, 64);
+                s2 += __shfl_xor(s2, off, 64);
             }
         }
         if (fixs && hg == 0 && sl == 0) {
             double *o = fixs + (long long)q * 3 * pb.P + k;
-            o[0] = sn[q];
-            o[pb.P] = s1[q];
-            o[2 * pb.P] = s2[q];
+            o[0] = sn;
+            o[pb.P] = s1;
+            o[2 * pb.P] = s2;
         }
         if (sl == 0) {
             double *o = fixp + (long long)q * NMOM * pb.P + k;
 #pragma unroll
             for (int h = 0; h < 3; ++h)
 #pragma unroll
-                for (int c = 0; c < 4; ++c) o[(long long)(3 + 4 * (3 * hg + h) + c) * pb.P] = acc[q][4 * h + c];
+                for (int c = 0; c < 4; ++c) o[(long long)(3 + 4 * (3 * hg + h) + c) * pb.P] = acc[4 * h + c];
             if (hg == 0) {
-                o[0] = f0r[q];
-                o[pb.P] = f0i[q];
-                o[2 * pb.P] = w2[q];
+                o[0] = f0r;
+                o[pb.P] = f0i;
+                o[2 * pb.P] = w2;
             }
         }
     }
