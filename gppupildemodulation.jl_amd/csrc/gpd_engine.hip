@@ -343,7 +343,7 @@ Layout plan(long long N, long long P, long long n_fc, bool faint, bool harmonic,
     L.smask = take(fsplit ? (size_t)U * sizeof(unsigned) : 0);
     // (+ the header, + k_faint_defer_count's 6 ints per block of 1024 tiles)
     L.dlist = take(fsplit ? (size_t)(2 * ((N + MM_TS - 1) / MM_TS) + 6 +
-                             6 * ((N + MM_TS - 1) / MM_TS / 1024 + 1)) * sizeof(int) : 0);
+                             6 * ((N + MM_TS - 1) / MM_TS / DEFER_TILES + 1)) * sizeof(int) : 0);
     L.fixp = take(fsplit ? (size_t)FST_SLOTS * NMOM * P * sizeof(double) : 0);
     L.ftab = take(fsplit ? (size_t)((N + MM_TS - 1) / MM_TS) * MM_TS * 2 * KH * sizeof(double) : 0);
     // fused faint statistics: per (unit, state) slot, S1/S2 of the two sample halves per series,
@@ -919,10 +919,10 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
     int *dlist = (int *)(ws + L.dlist);
     int *dhdr = dlist + 2 * ((N + MM_TS - 1) / MM_TS);
     int *dbsum = dhdr + 6;
-    const unsigned defer_blocks = (unsigned)(((N + MM_TS - 1) / MM_TS + 1023) / 1024);
+    const unsigned defer_blocks = (unsigned)(((N + MM_TS - 1) / MM_TS + DEFER_TILES - 1) / DEFER_TILES);
     auto faint_defer = [&]() {
-        k_faint_defer_count<<<defer_blocks, 1024, 0, stream>>>(pb, dbsum);
-        k_faint_defer_list<<<defer_blocks, 1024, 0, stream>>>(pb, dbsum, dlist, dhdr);
+        k_faint_defer_count<<<defer_blocks, 256, 0, stream>>>(pb, dbsum);
+        k_faint_defer_list<<<defer_blocks, 256, 0, stream>>>(pb, dbsum, dlist, dhdr);
     };
     double *fixp = (double *)(ws + L.fixp), *ftab = (double *)(ws + L.ftab);
     const unsigned ftab_grid = (unsigned)((N + MM_TS - 1) / MM_TS * MM_TS / 256 + 1);

@@ -1849,119 +1849,135 @@ __global__ __launch_bounds__(256) void k_faint_fused_fin(Problem pb, int units,
 // OR of 1 << state over them.  States depend on the sample only, so the list serves every series
 // (and every shard: the order is that of the tiles).  dhdr[2 + s]: the first valid sample of
 // state s (the shift of the fused faint statistics, k_moments_ws<FAINT>; 0 when the state has
-// none).  Two launches over blocks of 1024 tiles (r4; was one latency-bound workgroup walking
-// every tile): k_faint_defer_count writes each block's count / state mask / first samples into
-// bsum[6b …], k_faint_defer_list writes the entries at the block's offset (the sum of the
-// counts before it) in tile order, and its block 0 the header.
-__device__ __forceinline__ void defer_tile(const Problem &pb, long long j, unsigned &dm,
-                                           unsigned &sm, int (&first)[FST_SLOTS]) {
-    const long long N = pb.N;
-    // the tile's 32 state bytes in two 16-B loads when the array is 16-B aligned
-    unsigned w[8];
-    const long long nb = N - j * MM_TS;
-    if (nb >= MM_TS && (((unsigned long long)pb.state) & 15) == 0) {
-        const uint4 *src = (const uint4 *)(pb.state + j * MM_TS);
-        const uint4 a = src[0], b = src[1];
-        w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
-        w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
-    } else {
-        for (int q = 0; q < 8; ++q) w[q] = 0;
-        for (int s = 0; s < nb && s < MM_TS; ++s)
-            w[s >> 2] |= (unsigned)(unsigned char)pb.state[j * MM_TS + s] << (8 * (s & 3));
+// none).  Two launches over blocks of DEFER_TILES tiles, one sample per thread (r6; r4 had a
+// thread walk each tile's 32 samples, blocks of 1024 tiles: 36 µs for C5's 3125 tiles):
+// k_faint_defer_count writes each block's count / state mask / first samples into bsum[6b …],
+// k_faint_defer_list writes the entries at the block's offset (the sum of the counts before it,
+// summed by the block in parallel) in tile order, and its block 0 the header.
+constexpr int DEFER_TILES = 8;  // 32-sample tiles per 256-thread block
+static_assert(MM_TS == 32, "k_faint_defer: a tile is a half-wave of 32 lanes");
+struct DeferLane {
+    unsigned dm;    // this tile's deferred-sample bits (same on the tile's 32 lanes)
+    unsigned sm;    // OR of 1 << state over them
+    int first[FST_SLOTS];  // the tile's first valid sample of each state (INT_MAX if none)
+};
+// The per-tile masks of the 32-lane half-wave holding tile j = sample i >> 5 (lane s = i & 31).
+__device__ __forceinline__ DeferLane defer_lane(const Problem &pb, long long i) {
+    const int lane = (int)threadIdx.x & 63, sh = lane & 32;
+    int st = -1;
+    if (i < pb.N) st = (int)(signed char)pb.state[i];
+    const bool v = i < pb.N && fst_valid(pb.flags, st);
+    const unsigned hv = (unsigned)(__ballot(v) >> sh);
+    const int f = hv ? __builtin_ctz(hv) : 0;
+    const int ds = __shfl(st, sh + f, 64);
+    const bool diff = v && st != ds;
+    DeferLane r;
+    r.dm = (unsigned)(__ballot(diff) >> sh);
+    r.sm = 0;
+    const long long j0 = (i >> 5) << 5;
+#pragma unroll
+    for (int q = 0; q < FST_SLOTS; ++q) {
+        const unsigned mq = (unsigned)(__ballot(v && st == q) >> sh);
+        r.first[q] = mq ? (int)(j0 + __builtin_ctz(mq)) : 0x7fffffff;
+        if ((unsigned)(__ballot(diff && st == q) >> sh)) r.sm |= 1u << q;
     }
-    int ds = -1;
-    unsigned fm = 0;
-    dm = sm = 0;
-    for (int s = 0; s < MM_TS; ++s) {
-        if (s >= nb) break;
-        const int st = (int)(signed char)(w[s >> 2] >> (8 * (s & 3)));
-        if (!fst_valid(pb.flags, st)) continue;
-        if (!((fm >> st) & 1u)) {  // the tile's first sample of state st
-            fm |= 1u << st;
-            first[st] = min(first[st], (int)(j * MM_TS + s));
-        }
-        if (ds < 0) {
-            ds = st;
-        } else if (st != ds) {
-            dm |= 1u << s;
-            sm |= 1u << st;
-        }
-    }
+    return r;
 }
 
-__global__ __launch_bounds__(1024) void k_faint_defer_count(Problem pb, int *__restrict__ bsum)
+__global__ __launch_bounds__(256) void k_faint_defer_count(Problem pb, int *__restrict__ bsum)
 #if GPD_OWNS(GPD_U_ENGINE)
 {
-    __shared__ int wcnt[16];
-    __shared__ unsigned smk;
-    __shared__ int sfirst[FST_SLOTS];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const long long nt = (pb.N + MM_TS - 1) / MM_TS, j = (long long)blockIdx.x * 1024 + tid;
-    if (tid == 0) smk = 0;
-    if (tid < FST_SLOTS) sfirst[tid] = 0x7fffffff;
-    __syncthreads();
-    unsigned dm = 0, sm = 0;
-    int first[FST_SLOTS] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
-    if (j < nt) defer_tile(pb, j, dm, sm, first);
-    const unsigned long long b = __builtin_amdgcn_ballot_w64(dm != 0);
-    if (lane == 0) wcnt[wave] = __builtin_popcountll(b);
-    if (sm) atomicOr(&smk, sm);
-#pragma unroll
-    for (int s = 0; s < FST_SLOTS; ++s)
-        if (first[s] != 0x7fffffff) atomicMin(&sfirst[s], first[s]);
+    __shared__ int tcnt[DEFER_TILES];
+    __shared__ unsigned tsm[DEFER_TILES];
+    __shared__ int tfirst[DEFER_TILES][FST_SLOTS];
+    const int tid = threadIdx.x, t = tid >> 5;
+    const DeferLane r = defer_lane(pb, (long long)blockIdx.x * 256 + tid);
+    if ((tid & 31) == 0) {
+        tcnt[t] = r.dm != 0;
+        tsm[t] = r.sm;
+        for (int q = 0; q < FST_SLOTS; ++q) tfirst[t][q] = r.first[q];
+    }
     __syncthreads();
     if (tid == 0) {
-        int tot = 0;
-        for (int w = 0; w < 16; ++w) tot += wcnt[w];
+        int c = 0;
+        unsigned sm = 0;
+        int first[FST_SLOTS] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
+        for (int u = 0; u < DEFER_TILES; ++u) {
+            c += tcnt[u];
+            sm |= tsm[u];
+            for (int q = 0; q < FST_SLOTS; ++q) first[q] = min(first[q], tfirst[u][q]);
+        }
         int *o = bsum + 6 * blockIdx.x;
-        o[0] = tot;
-        o[1] = (int)smk;
-        for (int s = 0; s < FST_SLOTS; ++s) o[2 + s] = sfirst[s];
+        o[0] = c;
+        o[1] = (int)sm;
+        for (int q = 0; q < FST_SLOTS; ++q) o[2 + q] = first[q];
     }
 }
 #else
 ;
 #endif
 
-__global__ __launch_bounds__(1024) void k_faint_defer_list(Problem pb, const int *__restrict__ bsum,
-                                                           int *__restrict__ dlist,
-                                                           int *__restrict__ dhdr)
+__global__ __launch_bounds__(256) void k_faint_defer_list(Problem pb, const int *__restrict__ bsum,
+                                                          int *__restrict__ dlist,
+                                                          int *__restrict__ dhdr)
 #if GPD_OWNS(GPD_U_ENGINE)
 {
-    __shared__ int wcnt[16];
-    __shared__ int sbase;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const long long nt = (pb.N + MM_TS - 1) / MM_TS, j = (long long)blockIdx.x * 1024 + tid;
-    if (tid == 0) {
-        int off = 0;
-        for (unsigned q = 0; q < blockIdx.x; ++q) off += bsum[6 * q];
-        sbase = off;
-        if (blockIdx.x == 0) {  // the header: totals over every block
-            int tot = 0;
-            unsigned sm = 0;
-            int first[FST_SLOTS] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
-            for (unsigned q = 0; q < gridDim.x; ++q) {
-                tot += bsum[6 * q];
-                sm |= (unsigned)bsum[6 * q + 1];
-                for (int s = 0; s < FST_SLOTS; ++s) first[s] = min(first[s], bsum[6 * q + 2 + s]);
+    __shared__ int wsum[4];
+    __shared__ unsigned tdm[DEFER_TILES];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, t = tid >> 5;
+    const long long i = (long long)blockIdx.x * 256 + tid;
+    // the block's offset: the counts of the blocks before it, summed by the whole block
+    int part = 0;
+    for (unsigned q = tid; q < blockIdx.x; q += 256) part += bsum[6 * q];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) part += __shfl_xor(part, o, 64);
+    if (lane == 0) wsum[wave] = part;
+    if (blockIdx.x == 0) {  // the header: totals over every block
+        int tot = 0;
+        unsigned sm = 0;
+        int first[FST_SLOTS] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
+        for (unsigned q = tid; q < gridDim.x; q += 256) {
+            tot += bsum[6 * q];
+            sm |= (unsigned)bsum[6 * q + 1];
+            for (int s = 0; s < FST_SLOTS; ++s) first[s] = min(first[s], bsum[6 * q + 2 + s]);
+        }
+        __shared__ int htot[4];
+        __shared__ unsigned hsm[4];
+        __shared__ int hfirst[4][FST_SLOTS];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            tot += __shfl_xor(tot, o, 64);
+            sm |= (unsigned)__shfl_xor((int)sm, o, 64);
+            for (int s = 0; s < FST_SLOTS; ++s) first[s] = min(first[s], __shfl_xor(first[s], o, 64));
+        }
+        if (lane == 0) {
+            htot[wave] = tot;
+            hsm[wave] = sm;
+            for (int s = 0; s < FST_SLOTS; ++s) hfirst[wave][s] = first[s];
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int T = 0;
+            unsigned M = 0;
+            int F[FST_SLOTS] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
+            for (int w = 0; w < 4; ++w) {
+                T += htot[w];
+                M |= hsm[w];
+                for (int s = 0; s < FST_SLOTS; ++s) F[s] = min(F[s], hfirst[w][s]);
             }
-            dhdr[0] = tot;
-            dhdr[1] = (int)sm;
-            for (int s = 0; s < FST_SLOTS; ++s) dhdr[2 + s] = first[s] == 0x7fffffff ? 0 : first[s];
+            dhdr[0] = T;
+            dhdr[1] = (int)M;
+            for (int s = 0; s < FST_SLOTS; ++s) dhdr[2 + s] = F[s] == 0x7fffffff ? 0 : F[s];
         }
     }
-    unsigned dm = 0, sm = 0;
-    int first[FST_SLOTS] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
-    if (j < nt) defer_tile(pb, j, dm, sm, first);
-    const unsigned long long b = __builtin_amdgcn_ballot_w64(dm != 0);
-    const int before = __builtin_popcountll(b & ((1ull << lane) - 1ull));
-    if (lane == 0) wcnt[wave] = __builtin_popcountll(b);
+    const DeferLane r = defer_lane(pb, i);
+    if ((tid & 31) == 0) tdm[t] = r.dm;
     __syncthreads();
-    int off = sbase;
-    for (int w = 0; w < wave; ++w) off += wcnt[w];
-    if (dm) {
-        dlist[2 * (off + before)] = (int)j;
-        dlist[2 * (off + before) + 1] = (int)dm;
+    if ((tid & 31) == 0 && r.dm) {
+        int off = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        for (int u = 0; u < t; ++u) off += tdm[u] != 0;
+        dlist[2 * off] = (int)(i >> 5);
+        dlist[2 * off + 1] = (int)r.dm;
     }
 }
 #else
