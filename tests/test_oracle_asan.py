@@ -8,6 +8,7 @@ lengths, faint states with empty and one-sample states, NaNs, fitoffsets, xinit,
 edge cases, every libm regime) and require (1) a clean exit with no sanitizer report and (2) the
 same results as the ordinary liboracle.so, bit for bit.  CPU only.
 """
+import fcntl
 import os
 import struct
 import subprocess
@@ -23,8 +24,13 @@ DRIVER = os.path.join(ROOT, "oracle", "_asan", "asan_driver")
 
 @pytest.fixture(scope="module")
 def asan():
-    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "asan"],
-                       capture_output=True, text=True)
+    # one build at a time (pytest-xdist workers would otherwise relink the driver while another
+    # worker runs it)
+    os.makedirs(os.path.dirname(DRIVER), exist_ok=True)
+    with open(DRIVER + ".lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "asan"],
+                           capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     assert os.path.exists(DRIVER)
 
