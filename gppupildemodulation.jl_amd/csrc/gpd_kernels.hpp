@@ -2528,8 +2528,11 @@ __device__ __forceinline__ void harm_offsets(F &f, const Problem &pb, long long 
 // columns), copied in by the group's lanes before the fit — the objective reads them there
 // (HarmL).  Series whose NEWUOA probes leave the expansion's safe range are appended to `list`
 // for the exact evaluator.
+#ifndef GPD_FIT_MINW
+#define GPD_FIT_MINW 1  // A/B builds: -DGPD_FIT_MINW=2 (two fit waves per SIMD, 256 registers)
+#endif
 template <int LPS, bool MC>
-__global__ __launch_bounds__(256, 1) void k_fit_harmonic(Problem pb, const Info *__restrict__ info,
+__global__ __launch_bounds__(256, GPD_FIT_MINW) void k_fit_harmonic(Problem pb, const Info *__restrict__ info,
                                                          const double *__restrict__ mom,
                                                          const double *__restrict__ aux,
                                                          const double *__restrict__ momG, long long PG,
