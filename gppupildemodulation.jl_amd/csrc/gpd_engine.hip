@@ -5,6 +5,7 @@
 // per device; gpd_fit_batch_dev enqueues the whole pipeline on the caller's stream without a
 // host round trip (the harmonic → exact fallback list is consumed on device).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <sched.h>
 
@@ -76,6 +77,9 @@ enum OptId {
     O_STAGE_PINNED,  // 1: demodulated columns staged through a pinned ring; 0: pageable ring (tests)
     O_H2D_PARTS,     // 0: automatic (2 parts for pinned host data, else 1); n: host-buffer harmonic
                      // calls cut into n parts, H2D / compute / D2H pipelined
+    O_MOM_CUS,       // 0: the moment pass on the caller's stream; n: on a stream masked to n CUs (A/B)
+    O_FIT_CUS,       // 0: off; r > 0: pipelined cohorts (option cohorts) keep r CUs per XCD for
+                     // the fits of all but the last cohort, the moment pass on the others
     O_COUNT
 };
 struct OptDef {
@@ -88,10 +92,11 @@ constexpr OptDef kOpt[O_COUNT] = {
     {"exact_mcache", 1}, {"xspin_test", 0},    {"units", 0},         {"upw", 0},
     {"fit_lanes", 0},    {"fit_lps", 0},       {"fit_wpb", 0},       {"cohorts", 1},       {"harm_min_span", 256}, {"fs_cohort_mb", 4096},
     {"moments", 0},      {"fit_prof", 0},      {"sync_debug", 0},    {"host_prof", 0},
-    {"fit_mcache", 1},   {"stage_pinned", 1},  {"h2d_parts", 0}};
+    {"fit_mcache", 1},   {"stage_pinned", 1},  {"h2d_parts", 0},   {"mom_cus", 0},
+    {"fit_cus", 0}};
 std::atomic<long long> g_opt[O_COUNT] = {{1}, {0}, {0},   {0},    {0}, {0}, {0}, {1}, {1}, {0}, {0},
                                           {0}, {0}, {0},   {0},    {1}, {256}, {4096}, {0}, {0}, {0},
-                                          {0}, {1}, {1}, {0}};
+                                          {0}, {1}, {1}, {0}, {0}, {0}};
 inline long long opt(OptId o) { return g_opt[o].load(std::memory_order_relaxed); }
 int opt_find(const char *name) {
     if (!name) return -1;
@@ -136,6 +141,12 @@ struct DevCtx {
     // CUs as soon as they free up)
     hipStream_t side = nullptr;
     hipEvent_t fork[kMaxCohorts] = {}, join = nullptr;
+    // CU-masked streams (options mom_cus / fit_cus): `mstream` on the low mbits bits of the CU
+    // mask, `fstream` on the bits above them (gfx950: bit i of the mask is a CU of XCD i mod 8,
+    // so the top 8r bits are r CUs of every XCD — tools/probes/cumask.hip)
+    hipStream_t mstream = nullptr, fstream = nullptr;
+    int mbits = 0;
+    hipEvent_t mev[4] = {};
     bool have_timers = false;
     int n_cu = 0;  // compute units (wave-quantisation of the moment grid)
     // gpd_buildstates_dev: pinned staging of the timer lists, reused once its copy has run
@@ -900,6 +911,30 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         if (e == hipSuccess) e = hipEventCreateWithFlags(&cx->join, hipEventDisableTiming);
         return e;
     };
+    // CU-masked streams: mstream on mask bits [0, mb), fstream on [mb, n_cu) (created once per
+    // device context, re-created when mb changes; A/B options mom_cus and fit_cus)
+    auto ensure_masked = [&](int mb) -> hipError_t {
+        if (cx->mstream && cx->mbits == mb) return hipSuccess;
+        hipError_t e = hipSuccess;
+        if (cx->mstream) {
+            e = hipStreamSynchronize(cx->mstream);
+            if (e == hipSuccess && cx->fstream) e = hipStreamSynchronize(cx->fstream);
+            if (e != hipSuccess) return e;
+            (void)hipStreamDestroy(cx->mstream);
+            if (cx->fstream) (void)hipStreamDestroy(cx->fstream);
+            cx->mstream = cx->fstream = nullptr;
+        }
+        const int words = (cx->n_cu + 31) / 32;
+        std::vector<uint32_t> lo(words, 0), hi(words, 0);
+        for (int i = 0; i < cx->n_cu; ++i) (i < mb ? lo : hi)[i / 32] |= 1u << (i % 32);
+        e = hipExtStreamCreateWithCUMask(&cx->mstream, (uint32_t)words, lo.data());
+        if (e == hipSuccess && mb < cx->n_cu)
+            e = hipExtStreamCreateWithCUMask(&cx->fstream, (uint32_t)words, hi.data());
+        for (int i = 0; i < 4 && e == hipSuccess; ++i)
+            if (!cx->mev[i]) e = hipEventCreateWithFlags(&cx->mev[i], hipEventDisableTiming);
+        if (e == hipSuccess) cx->mbits = mb;
+        return e;
+    };
     // faint whole-exposure series on the MFMA kernel: state-split moments (k_moments_ws<FAINT>,
     // weighted in k_reduce_moments).  GPD_FAINT_SIDE=1 runs the statistics beside the moment
     // pass on the side stream — measured on C5 (r3): no gain, both passes stream HBM (statistics
@@ -938,6 +973,20 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
         mark("table");
         int *ccount = list + P + 64;  // one fallback counter per cohort
         HIP_TRY(hipMemsetAsync(ccount, 0, kMaxCohorts * sizeof(int), stream));
+        // option fit_cus = r (A/B, non-faint): r CUs of every XCD run the fits of all but the
+        // last cohort on a CU-masked stream, the moment passes run on the other CUs (a masked
+        // stream of their own); the last cohort's fit on the side stream, every CU
+        const int resv = faint ? 0 : (int)std::min<long long>(cx->n_cu / 2, 8 * opt(O_FIT_CUS));
+        hipStream_t ms = stream, fs = side;
+        int mcu = cx->n_cu;
+        if (resv > 0) {
+            HIP_TRY(ensure_masked(cx->n_cu - resv));
+            HIP_TRY(hipEventRecord(cx->mev[0], stream));
+            HIP_TRY(hipStreamWaitEvent(cx->mstream, cx->mev[0], 0));
+            ms = cx->mstream;
+            fs = cx->fstream;
+            mcu = cx->n_cu - resv;
+        }
         const bool fs1 = L.fs1 && fse != 2;
         const long long step = ((P + cohorts - 1) / cohorts + MM_PIX - 1) / MM_PIX * MM_PIX;
         int c = 0;
@@ -970,7 +1019,7 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             }
             int units, nch;
             long long ulen, chunk;
-            moment_grid(N, n, cx->n_cu, true, true, units, ulen, chunk, nch, faint);
+            moment_grid(N, n, mcu, true, true, units, ulen, chunk, nch, faint);
             dim3 g((unsigned)((n + MM_PIX - 1) / MM_PIX), (unsigned)nch);
             if (faint && c == 0) {
                 faint_defer();
@@ -987,43 +1036,52 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             else if (faint)
                 k_moments_ws<0, false, c64, 2, false, true><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c, smask, fsp_c, fcnt, dhdr);
             else if (!tm && is_c32)
-                k_moments_ws<0, false, c32, 2, false><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c);
+                k_moments_ws<0, false, c32, 2, false><<<g, 512, 0, ms>>>(sp, tab, chunk, ulen, part_c);
             else if (!tm)
-                k_moments_ws<0, false, c64, 2, false><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c);
+                k_moments_ws<0, false, c64, 2, false><<<g, 512, 0, ms>>>(sp, tab, chunk, ulen, part_c);
             else if (is_c32)
-                k_moments_ws<0, false, c32, 2><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c);
+                k_moments_ws<0, false, c32, 2><<<g, 512, 0, ms>>>(sp, tab, chunk, ulen, part_c);
             else
-                k_moments_ws<0, false, c64, 2><<<g, 512, 0, stream>>>(sp, tab, chunk, ulen, part_c);
-            mark("moments");
+                k_moments_ws<0, false, c64, 2><<<g, 512, 0, ms>>>(sp, tab, chunk, ulen, part_c);
+            if (ms == stream) mark("moments");
             if (fused) {
                 k_faint_fused_fin<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(
                     sp, units, fsp_c, fcnt, smask, part_c, fixs_c, fix_c, dhdr, fs_c);
                 mark("faint_stats");
             }
             dim3 gr((unsigned)((n + 255) / 256), (unsigned)NMOM);
-            k_reduce_moments<<<gr, 256, 0, stream>>>(part_c, units, n, info, fs_c, faint ? 2 : 0,
-                                                     mom_c, aux_c, smask, fix_c, dhdr);
-            mark("reduce");
-            // the cohort's fit on the side stream, after its moments
-            HIP_TRY(hipEventRecord(cx->fork[c], stream));
-            HIP_TRY(hipStreamWaitEvent(side, cx->fork[c], 0));
-            const int b0 = rec(side);
-            HIP_TRY(launch_fit(fit_shape(n, cx->n_cu, (sp.flags & F_OFFSETS) != 0), sp, info, mom_c, aux_c, nullptr, n_fc,
-                               nullptr, out_c, raw_c, list_c, count_c, side));
-            const int b1 = mark_on(side, b0, "fit_harmonic");
-            const unsigned xg = (unsigned)std::min<long long>(n, 1024);
+            k_reduce_moments<<<gr, 256, 0, ms>>>(part_c, units, n, info, fs_c, faint ? 2 : 0,
+                                                 mom_c, aux_c, smask, fix_c, dhdr);
+            if (ms == stream) mark("reduce");
+            // the cohort's fit on the side stream (fit_cus: all but the last on the reserved
+            // CUs), after its moments
+            const bool on_resv = resv > 0 && k0 + step < P;
+            hipStream_t fst = on_resv ? fs : side;
+            HIP_TRY(hipEventRecord(cx->fork[c], ms));
+            HIP_TRY(hipStreamWaitEvent(fst, cx->fork[c], 0));
+            const int b0 = rec(fst);
+            HIP_TRY(launch_fit(fit_shape(n, on_resv ? resv : cx->n_cu, (sp.flags & F_OFFSETS) != 0), sp, info, mom_c, aux_c, nullptr, n_fc,
+                               nullptr, out_c, raw_c, list_c, count_c, fst));
+            const int b1 = mark_on(fst, b0, "fit_harmonic");
+            const unsigned xg = (unsigned)std::min<long long>(n, on_resv ? resv : 1024);
             if (fused)  // the fallback series' two-pass statistics (as above, one cohort)
-                k_faint_stats_list<<<xg, 256, 0, side>>>(sp, list_c, count_c, fs_c);
+                k_faint_stats_list<<<xg, 256, 0, fst>>>(sp, list_c, count_c, fs_c);
             if (faint)
-                k_fit_exact<true, false, false><<<xg, EXACT_WG, 0, side>>>(
+                k_fit_exact<true, false, false><<<xg, EXACT_WG, 0, fst>>>(
                     sp, info, nullptr, fs_c, list_c, count_c, out_c, raw_c, ST_FALLBACK);
             else
-                k_fit_exact<false, false, false><<<xg, EXACT_WG, 0, side>>>(
+                k_fit_exact<false, false, false><<<xg, EXACT_WG, 0, fst>>>(
                     sp, info, nullptr, fs_c, list_c, count_c, out_c, raw_c, ST_FALLBACK);
-            mark_on(side, b1, "fit_fallback");
+            mark_on(fst, b1, "fit_fallback");
         }
         HIP_TRY(hipEventRecord(cx->join, side));
         HIP_TRY(hipStreamWaitEvent(stream, cx->join, 0));
+        if (resv > 0) {  // the reserved CUs' fits and the masked moment stream join too
+            HIP_TRY(hipEventRecord(cx->mev[2], fs));
+            HIP_TRY(hipStreamWaitEvent(stream, cx->mev[2], 0));
+            HIP_TRY(hipEventRecord(cx->mev[3], ms));
+            HIP_TRY(hipStreamWaitEvent(stream, cx->mev[3], 0));
+        }
         mark("fit_tail");  // the last cohort's fit, exposed
     } else if (faint && !fused) {
         // whole-exposure series: one pass over the series, one hypot per sample (k_faint_p1/p2/
@@ -1076,6 +1134,15 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             mark("moments_win");
         } else if (use_mfma) {
             dim3 g((unsigned)((P + MM_PIX - 1) / MM_PIX), (unsigned)L.nch);
+            // option mom_cus (A/B): the non-faint moment pass on a stream masked to that many CUs
+            hipStream_t mst = stream;
+            const long long mcus = opt(O_MOM_CUS);
+            if (!faint && mcus > 0 && mcus < cx->n_cu) {
+                HIP_TRY(ensure_masked((int)mcus));
+                HIP_TRY(hipEventRecord(cx->mev[0], stream));
+                HIP_TRY(hipStreamWaitEvent(cx->mstream, cx->mev[0], 0));
+                mst = cx->mstream;
+            }
             if (faint) {  // the deferred samples of the state-split pass (usually none)
                 faint_defer();
                 k_fix_table<<<ftab_grid, 256, 0, stream>>>(pb, dlist, dhdr, ftab);
@@ -1098,11 +1165,11 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             else if (faint)
                 k_moments_ws<0, false, c64, 2, false, true><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part, smask, fsp, fcnt, dhdr);
             else if (!tmix && is_c32)  // all-f64 MFMA variants (option mix = 0)
-                k_moments_ws<0, false, c32, 2, false><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
+                k_moments_ws<0, false, c32, 2, false><<<g, 512, 0, mst>>>(pb, tab, L.chunk, L.unit_len, part);
             else if (!tmix)
-                k_moments_ws<0, false, c64, 2, false><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
+                k_moments_ws<0, false, c64, 2, false><<<g, 512, 0, mst>>>(pb, tab, L.chunk, L.unit_len, part);
             else if (is_c32)  // Float32 storage: the producer/consumer kernel on 8-B elements
-                k_moments_ws<0, false, c32, 2><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
+                k_moments_ws<0, false, c32, 2><<<g, 512, 0, mst>>>(pb, tab, L.chunk, L.unit_len, part);
 #ifdef GPD_DIAG
             // timing variants (results invalid), diagnostics build only (build.py --diag)
             else if (mk == 2)  // ws_nomfma
@@ -1128,7 +1195,11 @@ static int pipeline_dev(int64_t n_samples, int64_t n_pixels, const double *t, co
             }
 #endif
             else  // the production kernel
-                k_moments_ws<0, false, c64, 2><<<g, 512, 0, stream>>>(pb, tab, L.chunk, L.unit_len, part);
+                k_moments_ws<0, false, c64, 2><<<g, 512, 0, mst>>>(pb, tab, L.chunk, L.unit_len, part);
+            if (mst != stream) {
+                HIP_TRY(hipEventRecord(cx->mev[1], mst));
+                HIP_TRY(hipStreamWaitEvent(stream, cx->mev[1], 0));
+            }
         } else {
             dim3 g((unsigned)((P + 63) / 64), (unsigned)L.units);
             if (faint)

@@ -53,7 +53,7 @@ def test_options_api_and_no_environment(gpd):
                 "fit_wpb": 0, "cohorts": 1,
                 "harm_min_span": 256, "fs_cohort_mb": 4096, "moments": 0, "fit_prof": 0,
                 "sync_debug": 0, "host_prof": 0, "fit_mcache": 1,
-                "stage_pinned": 1, "h2d_parts": 0}
+                "stage_pinned": 1, "h2d_parts": 0, "mom_cus": 0, "fit_cus": 0}
     gpd.reset_options()
     assert gpd.option_names() == list(defaults)
     assert {k: gpd.get_option(k) for k in defaults} == defaults
