@@ -202,6 +202,28 @@ def test_cohort_pipeline_records_bitwise(gpu, opts, faint, storage):
     assert "fit_tail" in t and t["moments"] > 0, t  # the cohort path ran
 
 
+@pytest.mark.parametrize("storage", ["c64", "c32"])
+def test_cu_masked_streams_records_bitwise(gpu, opts, storage):
+    """The CU-masked A/B paths (options mom_cus: the moment pass on a stream masked to n CUs;
+    fit_cus with cohorts: the fits of all but the last cohort on r CUs per XCD, the moments on the
+    others — DESIGN.md §15) give the default path's records bit for bit, c64 and c32."""
+    N, P = 12_000, 1000
+    B = synth.make_batch(N, P, seed=23)
+    d, fc = B["d"], B["fc"]
+    if storage == "c32":
+        d, fc = d.astype(np.complex64), fc.astype(np.complex64)
+    args = (B["t"], d, fc, B["fc_of_pixel"])
+    opts("h2d_parts", 1)
+    ref = gpu.fit_batch(*args, method="harmonic")
+    for setting in ({"mom_cus": 192}, {"mom_cus": 248}, {"cohorts": 3, "fit_cus": 2},
+                    {"cohorts": 5, "fit_cus": 1}):
+        for k, v in setting.items():
+            opts(k, v)
+        _same(gpu.fit_batch(*args, method="harmonic"), ref)
+        for k in setting:
+            opts(k, 0 if k != "cohorts" else 1)
+
+
 def test_series_per_fit_wave_does_not_change_records(gpu, opts):
     """The harmonic fit's shape follows the batch (fit_shape, gpd_engine.hip): lanes per series
     (1, 2, 4, 8 — the objective's harmonic slots and NEWUOA's 49-angle searches split across
