@@ -1102,7 +1102,11 @@ __device__ __forceinline__ bool fst_valid(unsigned flags, int st) {
 // would be cheaper still but is ~2^-25 relative: tools/probes/sqrt_ulp.hip).
 __device__ __forceinline__ double fs_abs(double re, double im) {
     const double r2 = fma(re, re, im * im);
+#ifdef GPD_FS_RSQ32  // A/B: the seed from the single-precision rsq (r2 within float's range)
+    const double y = (double)__builtin_amdgcn_rsqf((float)fmax(r2, 0x1p-126));
+#else
     const double y = __builtin_amdgcn_rsq(fmax(r2, 0x1p-1022));
+#endif
     double g = r2 * y, h = 0.5 * y;
     const double r = fma(-g, h, 0.5);
     g = fma(g, r, g);
