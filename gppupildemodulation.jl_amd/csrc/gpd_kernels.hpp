@@ -1758,7 +1758,19 @@ __global__ __launch_bounds__(256) void k_reduce_moments(const double *__restrict
                 if ((dm >> q) & 1u) s += f[q] * fixp[((long long)q * NMOM + m) * P + k];
         }
     } else {
-        for (int c = 0; c < nch; ++c) s += part[((long long)c * NMOM + m) * P + k];
+        // 8 partials in flight per thread, then summed in chunk order (the same additions as
+        // one load at a time, which waited out a full HBM round trip per chunk: 0.43 ms on C3)
+        const double *pk = part + (long long)m * P + k;
+        const long long cs = (long long)NMOM * P;
+        int c = 0;
+        for (; c + 8 <= nch; c += 8) {
+            double v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = __builtin_nontemporal_load(pk + (c + j) * cs);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s += v[j];
+        }
+        for (; c < nch; ++c) s += __builtin_nontemporal_load(pk + c * cs);
     }
     mom[(long long)m * P + k] = s;
     if (m == 2) {
